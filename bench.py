@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py -- ipo-hip headline benchmark.
+
+Metric (BASELINE.json): IPM iterations/sec on netlib dfl001, HSD method
+(hsd.c, configs[2]), fp64, one MI355X per rank.  A "step" is one
+interior-point iteration (KKT assembly + supernodal LDL' + two refined
+solves + the O(m+n) step/centering/ratio/update kernels).  The timed region
+is one HSD solve from the reference's start point with the problem already
+resident in HBM (setup = upload + host symbolic analysis, reported apart),
+capped at --steps iterations; the solve converges (mu < 1e-12) after 117
+iterations, which is the default.
+
+N > 1: dfl001 does not shard, so ranks run independent
+replicas; value = all ranks' iterations / max wall time over ranks.
+
+Also reported:
+  roofline      -- the dominant kernel (k_update, the left-looking gather of
+                   the supernodal factorisation), measured live with HIP events
+                   on its own stream during the timed region;
+  cpu_baseline  -- the CPU oracle (oracle/, a single-threaded restatement of
+                   the reference's ipo) timed on this host over a bounded
+                   sample of the same workload (rank 0, N = 1).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "linear-programming-vanderbei_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+METRIC = "IPM iterations/sec (ADA^T factor+solve) on netlib dfl001; duality gap ≤1e-8"
+FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, spec
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak, MI355X_MICROARCH.md
+
+
+def dist_env():
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+class Dist:
+    """barrier / max-reduce over ranks; a no-op for a single process."""
+
+    def __init__(self, backend=None):
+        self.rank, self.world, self.local = dist_env()
+        self.dist = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            if backend is None:
+                backend = "nccl" if torch.cuda.is_available() else "gloo"
+            if backend == "nccl":
+                torch.cuda.set_device(self.local)
+            dist.init_process_group(backend=backend)
+            self.dist, self.torch, self.backend = dist, torch, backend
+
+    def _t(self, v):
+        t = self.torch.tensor([float(v)], dtype=self.torch.float64)
+        return t.cuda() if self.backend == "nccl" else t
+
+    def barrier(self):
+        if self.dist:
+            self.dist.all_reduce(self._t(0.0))
+
+    def max(self, v):
+        if not self.dist:
+            return v
+        t = self._t(v)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v):
+        if not self.dist:
+            return v
+        t = self._t(v)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def timed_replicas(d: Dist, run_step_block, sync):
+    """Barrier + sync, run the block, sync + barrier; returns (local result, max seconds over ranks)."""
+    sync()
+    d.barrier()
+    t0 = time.perf_counter()
+    res = run_step_block()
+    sync()
+    d.barrier()
+    dt = time.perf_counter() - t0
+    return res, d.max(dt)
+
+
+def cpu_baseline(mps, iters):
+    """Oracle (single-threaded C restatement of ipo) on `iters` HSD iterations of dfl001."""
+    import oracle_lib
+
+    class Run(C.Structure):
+        _fields_ = [("trace", C.c_void_p), ("max_iter", C.c_int), ("iters", C.c_int), ("t_setup", C.c_double),
+                    ("t_total", C.c_double), ("final_mu", C.c_double), ("final_pobj", C.c_double),
+                    ("final_dobj", C.c_double), ("final_pinf", C.c_double), ("final_dinf", C.c_double)]
+    oracle_lib.build()
+    L = oracle_lib.lib()
+    L.orc_ipo_run.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.POINTER(Run)]
+    L.orc_ipo_run.restype = C.c_int
+    r = Run()
+    r.max_iter = iters
+    L.orc_ipo_run(mps.encode(), 0, None, C.byref(r))
+    loop = r.t_total - r.t_setup
+    return {"value": r.iters / loop, "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": f"dfl001 hsd iterations 0..{r.iters - 1} ({r.iters} of 117), oracle/ C restatement, "
+                      f"single thread, symbolic setup {r.t_setup:.2f}s excluded, {loop:.1f}s timed",
+            "host_cpus": os.cpu_count()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=117, help="IPM iterations timed (capped by convergence)")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed IPM iterations before the timed solve")
+    ap.add_argument("--problem", default="dfl001")
+    ap.add_argument("--cpu-iters", type=int, default=3, help="HSD iterations of the CPU oracle sample (0 = skip)")
+    ap.add_argument("--no-timing", action="store_true", help="disable per-kernel HIP-event timing in the timed run")
+    args = ap.parse_args()
+
+    d = Dist()
+    import ipo_amd
+    from conftest import mps_path
+    ipo_amd.require_gpu()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.set_device(d.local)
+            sync = torch.cuda.synchronize
+        else:
+            sync = lambda: None  # noqa: E731
+    except ImportError:
+        sync = lambda: None  # noqa: E731
+
+    path = mps_path(args.problem)
+    p = ipo_amd.load_mps(path)
+    ctx = ipo_amd.Context(p)                       # upload + symbolic (not timed)
+    if args.warmup > 0:
+        ctx.run("hsd", max_iter=args.warmup)
+    (status, st, _), elapsed = timed_replicas(d, lambda: ctx.run("hsd", max_iter=args.steps, timing=not args.no_timing),
+                                              sync)
+    iters = st["iters"]
+    total_iters = d.sum(iters)
+    value = total_iters / elapsed
+
+    # dominant kernel: the supernodal gather (k_update); algorithmic flops/bytes
+    # per factorisation from the symbolic plan, device time from HIP events
+    roof = None
+    if st["update_ms"] > 0 and st["update_launches"] > 0:
+        nfac = st["factors"]
+        secs = st["update_ms"] * 1e-3
+        flops = st["flops_update"] * nfac
+        byts = st["bytes_update"] * nfac
+        t_flop = flops / (FP64_PEAK_TFLOPS * 1e12)
+        t_byte = byts / (HBM_PEAK_GBS * 1e9)
+        per_launch_s = secs / st["update_launches"]
+        if t_flop >= t_byte:
+            ach = flops / secs / 1e12
+            roof = {"bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": ach / FP64_PEAK_TFLOPS, "traffic": None}
+        else:
+            ach = byts / secs / 1e9
+            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": None}
+        roof.update({"kernel": "k_update", "avg_launch_us": per_launch_s * 1e6,
+                     "launches": st["update_launches"],
+                     "algorithmic_flops_per_factor": st["flops_update"],
+                     "algorithmic_bytes_per_factor": st["bytes_update"],
+                     "share_of_timed_region": secs / max(st["t_solve_s"], 1e-12),
+                     "panel_kernel_ms": st["panel_ms"], "sweep_ms": st["sweep_ms"]})
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": d.world, "steps": iters,
+        "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / max(iters, 1), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": f"netlib {args.problem}.mps (reference problems/netlib, tests/golden copy)",
+        "config": {"workload": f"{args.problem} hsd (BASELINE configs[2])", "method": "hsd", "m": p.m, "n": p.n,
+                   "nz": p.nz, "parallelism": f"replicas{d.world}", "status": ipo_amd.STATUS_TEXT.get(status, status),
+                   "iterations": iters, "golden_iterations": 117 if args.problem == "dfl001" else None,
+                   "final_mu": st["final_mu"], "final_pobj": st["final_pobj"], "final_dobj": st["final_dobj"],
+                   "setup_s": ctx.setup_seconds, "lnz": st["lnz"], "nsup": st["nsup"], "levels": st["nlevels"],
+                   "factor_ms_total": st["factor_ms"], "solve_ms_total": st["solve_ms"],
+                   "refine_passes": st["refine_passes"], "kernel_timing": not args.no_timing},
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if d.rank == 0 and d.world == 1 and args.cpu_iters > 0:
+        try:
+            out["cpu_baseline"] = cpu_baseline(path, args.cpu_iters)
+            out["config"]["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+        except Exception as e:  # the GPU number stands on its own
+            out["cpu_baseline"] = {"error": str(e)}
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    d.close()
+
+
+if __name__ == "__main__":
+    main()

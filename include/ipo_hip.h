@@ -1,0 +1,122 @@
+/*
+ * ipo_hip.h -- C ABI of libipo_hip.so, the MI355X interior-point core.
+ *
+ * Drop-in boundary: the symbols below are exactly the plug-in points the
+ * reference ipo binary links (src/ipo/makefile:49,56-63: $(METHOD) $(LU)).
+ * Linking libipo_hip.so in place of hsd.o/intpt.o (and ldlt.o) leaves the
+ * MPS/AMPL front end (src/common, src/amplsolver) unchanged.  All pointers
+ * are host pointers with the reference's meaning; nothing here exposes
+ * device or torch types.
+ */
+#ifndef IPO_HIP_H
+#define IPO_HIP_H
+
+#include <stdio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- METHOD plug-in ------------------------------------------------------
+ * Replaces solver() of src/ipo/hsd.c:27-29 (default, like makefile:57) and
+ * src/ipo/intpt.c:33-35 (set IPO_HIP_METHOD=intpt); prototype from
+ * src/common/solve.c:24-26.  Solves  max c'x + f  s.t.  Ax <= b, x >= 0,
+ * A m x n CSC (kA[n+1], iA[nz], A[nz]), 0-based.  x, z: n; y, w: m (the
+ * caller may allocate more, as solve.c:194-197 does).  Prints the banner
+ * and one trace line per iteration to stdout in the reference format.
+ * Returns 0 optimal, 2 primal infeasible, 4 dual infeasible, 5 iteration
+ * limit, 7 on a device error (the reference would exit(1)).
+ * Unlike hsd.c:290-291 it does NOT free w and z (they belong to the caller). */
+int solver(int m, int n, int nz, int *iA, int *kA, double *A, double *b, double *c, double f,
+           double *x, double *y, double *w, double *z);
+
+/* ---- LU plug-in ------------------------------------------------------------
+ * Replaces src/ipo/ldlt.h:1-20 (ldlt.c:124-162 and ldlt.c:311-319) with the
+ * reference's argument convention: ldltfac(m, n, kA, iA, A, dn, dm, kAt,
+ * iAt, At, verbose) factors  [ -diag(dn)  A' ; A  diag(dm) ]  where A is
+ * m x n (CSC kA/iA/A, transpose kAt/iAt/At), dn has n entries, dm has m.
+ * The first call performs the symbolic analysis and keeps it for the rest
+ * of the process (one pattern per process, like ldlt.c:108-120).
+ * forwardbackward(Dn, Dm, dx, dy) solves in place with iterative refinement
+ * (dx: n entries, dy: m entries), ldlt.c:327-425. */
+void ldltfac(int m, int n, int *kA, int *iA, double *A, double *dn, double *dm,
+             int *kAt, int *iAt, double *At, int verbose);
+void forwardbackward(double *Dn, double *Dm, double *dx, double *dy);
+/* releases the LU plug-in state (ldlt.c:507-513) */
+void inv_clo(void);
+
+/* ---- extended interface (not in the reference) ---------------------------- */
+typedef struct {
+    int    iters;            /* trace lines printed                           */
+    int    status;
+    double t_setup_s;        /* host symbolic analysis + uploads              */
+    double t_solve_s;        /* iteration loop wall time                      */
+    double factor_ms;        /* device time in factorisations (if timing)     */
+    double solve_ms;         /* device time in refined solves (if timing)     */
+    long   factors, solves, rawsolves, refine_passes;
+    double final_mu, final_pobj, final_dobj, final_pinf, final_dinf;
+    long   lnz;              /* nnz of L (reference pattern)                  */
+    double narth;            /* reference op count, ldlt.c:1243-1248          */
+    int    nsup, nlevels;
+    double flops_factor;     /* flops of one numeric factorisation            */
+    double lx_bytes;         /* bytes of the supernodal factor storage        */
+    double update_ms;        /* device time of the left-looking gather kernel (timing) */
+    double panel_ms;         /* device time of the panel LDL'+trsm kernel (timing)     */
+    double sweep_ms;         /* device time of triangular substitution sweeps (timing) */
+    long   update_launches, panel_launches;
+    double flops_update;     /* algorithmic flops of the gather kernel per factorisation */
+    double bytes_update;     /* algorithmic bytes of the gather kernel per factorisation */
+} ipo_hip_stats;
+
+/* method: 0 = hsd, 1 = intpt.  trace may be NULL (silent).  timing != 0
+ * records per-phase HIP-event times. */
+int ipo_hip_solve(int method, int m, int n, int nz, const int *iA, const int *kA, const double *A,
+                  const double *b, const double *c, double f, double *x, double *y, double *w, double *z,
+                  FILE *trace, int max_iter, int timing, ipo_hip_stats *stats);
+
+/* Persistent context: uploads the problem to HBM and runs the symbolic
+ * analysis once (setup); ipo_hip_ctx_run then iterates from the reference's
+ * start point with everything device-resident (used by bench.py). */
+typedef struct ipo_hip_ctx ipo_hip_ctx;
+ipo_hip_ctx *ipo_hip_ctx_create(int m, int n, const int *kA, const int *iA, const double *A,
+                                const double *b, const double *c, double f);
+int  ipo_hip_ctx_run(ipo_hip_ctx *ctx, int method, int max_iter, FILE *trace, int timing, ipo_hip_stats *stats);
+void ipo_hip_ctx_download(ipo_hip_ctx *ctx, double *x, double *y, double *w, double *z);
+void ipo_hip_ctx_destroy(ipo_hip_ctx *ctx);
+double ipo_hip_ctx_setup_seconds(const ipo_hip_ctx *ctx);
+
+/* Read an MPS file, normalise it like solvelp() (src/common/solve.c:28-205)
+ * and solve it; prints exactly what `ipo file.mps` prints (main.c:16-58)
+ * minus the .out file.  Returns the status (3 = free variable). */
+int ipo_hip_run_mps(const char *path, int method, FILE *out, int timing, ipo_hip_stats *stats);
+
+/* Dimensions of an MPS file after normalisation (for tests/harnesses).
+ * Returns 0, 3 (free variable) or the reader's error number. */
+int ipo_hip_mps_dims(const char *path, int *m0, int *n0, int *nz0, int *m, int *n, int *nz);
+
+/* Normalised problem export: caller passes NULL to query sizes first. */
+int ipo_hip_mps_load(const char *path, int *m, int *n, int *nz, int *kA, int *iA, double *A,
+                     double *b, double *c, double *f);
+
+/* KKT factor handle: symbolic + device numeric LDL' of K(E, D) for tests. */
+typedef struct ipo_hip_kkt ipo_hip_kkt;
+ipo_hip_kkt *ipo_hip_kkt_create(int m, int n, const int *kA, const int *iA, const double *A);
+void   ipo_hip_kkt_destroy(ipo_hip_kkt *k);
+int    ipo_hip_kkt_factor(ipo_hip_kkt *k, const double *E, const double *D);
+int    ipo_hip_kkt_solve(ipo_hip_kkt *k, const double *E, const double *D, double *fy, double *fx);
+int    ipo_hip_kkt_info(const ipo_hip_kkt *k, long *lnz, double *narth, int *nsup, int *nlevels, int *denwin,
+                        int *pdf, double *epsdiag, int *ndep, int *passes);
+int    ipo_hip_kkt_perm(const ipo_hip_kkt *k, int *perm);
+
+/* Host-only symbolic analysis (no GPU needed): reference ordering stats. */
+int ipo_hip_symbolic(int m, int n, const int *kA, const int *iA, int *perm, long *lnz, double *narth,
+                     int *denwin, int *pdf, int *nsup, int *nlevels);
+
+int ipo_hip_device_count(void);
+const char *ipo_hip_last_error(void);
+const char *ipo_hip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IPO_HIP_H */

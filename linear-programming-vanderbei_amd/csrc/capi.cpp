@@ -1,0 +1,426 @@
+// capi.cpp -- the C ABI of libipo_hip.so (include/ipo_hip.h).
+#include "../../include/ipo_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ipm.h"
+#include "kkt_device.h"
+#include "lp_io.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const std::string& s) { g_err = s; }
+
+const char* kStatusText[] = {"optimal solution", "primal unbounded", "primal infeasible", "dual unbounded",
+                             "dual infeasible",  "iteration limit",  "infinite lower bounds - not implemented",
+                             "suboptimal solution"};
+
+ipo::Method method_from_env() {
+    const char* e = std::getenv("IPO_HIP_METHOD");
+    if (e && !std::strcmp(e, "intpt")) return ipo::Method::Intpt;
+    return ipo::Method::Hsd;
+}
+
+// hsd.c:70-92 / intpt.c:70-92: tiny problems are echoed before the banner
+void print_small(FILE* tr, int m, int n, const int* kA, const int* iA, const double* A, const double* b,
+                 const double* c) {
+    if (!tr || !(m < 20 && n < 20)) return;
+    double AA[20][20];
+    for (int j = 0; j < n; j++) for (int i = 0; i < m; i++) AA[i][j] = 0;
+    for (int j = 0; j < n; j++) for (int k = kA[j]; k < kA[j + 1]; k++) AA[iA[k]][j] = A[k];
+    std::fprintf(tr, "A <= b: \n");
+    for (int i = 0; i < m; i++) {
+        for (int j = 0; j < n; j++) std::fprintf(tr, " %5.1f", AA[i][j]);
+        std::fprintf(tr, "<= %5.1f \n", b[i]);
+    }
+    std::fprintf(tr, "\n");
+    std::fprintf(tr, "c: \n");
+    for (int j = 0; j < n; j++) std::fprintf(tr, " %5.1f", c[j]);
+    std::fprintf(tr, "\n");
+}
+
+void fill_stats(ipo_hip_stats* st, const ipo::IpmResult& r, const ipo::KktPlan* P) {
+    if (!st) return;
+    std::memset(st, 0, sizeof(*st));
+    st->iters = r.iters;
+    st->status = r.status;
+    st->t_setup_s = r.t_setup_s;
+    st->t_solve_s = r.t_solve_s;
+    st->factor_ms = r.kkt.factor_ms;
+    st->solve_ms = r.kkt.solve_ms;
+    st->factors = r.kkt.factors;
+    st->solves = r.kkt.solves;
+    st->rawsolves = r.kkt.rawsolves;
+    st->refine_passes = r.refine_passes;
+    st->final_mu = r.final_mu;
+    st->final_pobj = r.final_pobj;
+    st->final_dobj = r.final_dobj;
+    st->final_pinf = r.final_pinf;
+    st->final_dinf = r.final_dinf;
+    st->update_ms = r.kkt.update_ms;
+    st->panel_ms = r.kkt.panel_ms;
+    st->sweep_ms = r.kkt.sweep_ms;
+    st->update_launches = r.kkt.update_launches;
+    st->panel_launches = r.kkt.panel_launches;
+    if (P) {
+        st->flops_update = P->flops_update;
+        st->bytes_update = P->bytes_update;
+        st->lnz = P->lnz;
+        st->narth = P->narth;
+        st->nsup = P->nsup;
+        st->nlevels = P->nlevels;
+        st->flops_factor = P->flops_factor;
+        st->lx_bytes = 8.0 * static_cast<double>(P->lx_size);
+    }
+}
+
+int solve_impl(ipo::Method method, int m, int n, int nz, const int* iA, const int* kA, const double* A,
+               const double* b, const double* c, double f, double* x, double* y, double* w, double* z, FILE* trace,
+               int max_iter, int timing, ipo_hip_stats* stats) {
+    try {
+        print_small(trace, m, n, kA, iA, A, b, c);
+        ipo::IpmSolver S(m, n, kA, iA, A, b, c, f);
+        ipo::IpmOptions opt;
+        opt.method = method;
+        opt.trace = trace;
+        opt.max_iter = max_iter > 0 ? max_iter : 200;
+        opt.timing = timing != 0;
+        ipo::IpmResult res;
+        (void)nz;
+        const int status = S.run(opt, &res);
+        S.download(x, y, w, z);
+        fill_stats(stats, res, &S.kkt().plan());
+        return status;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        if (trace) std::fprintf(trace, "ipo_hip: %s\n", e.what());
+        return 7;
+    }
+}
+
+// --- LU plug-in state: one pattern per process, like ldlt.c:108-120
+struct LuState {
+    std::unique_ptr<ipo::KktDevice> kkt;
+    hipStream_t stream = nullptr;
+    int ms = 0, ns = 0;                 // solver-side dimensions
+    ipo::DevBuf<double> E, D, fy, fx;
+};
+LuState* g_lu = nullptr;
+
+}  // namespace
+
+struct ipo_hip_ctx {
+    std::unique_ptr<ipo::IpmSolver> solver;
+};
+
+struct ipo_hip_kkt {
+    std::unique_ptr<ipo::KktDevice> kkt;
+    hipStream_t stream = nullptr;
+    int m = 0, n = 0;
+    ipo::DevBuf<double> E, D, fy, fx;
+};
+
+extern "C" {
+
+int solver(int m, int n, int nz, int* iA, int* kA, double* A, double* b, double* c, double f, double* x, double* y,
+           double* w, double* z) {
+    return solve_impl(method_from_env(), m, n, nz, iA, kA, A, b, c, f, x, y, w, z, stdout, 200, 0, nullptr);
+}
+
+int ipo_hip_solve(int method, int m, int n, int nz, const int* iA, const int* kA, const double* A, const double* b,
+                  const double* c, double f, double* x, double* y, double* w, double* z, FILE* trace, int max_iter,
+                  int timing, ipo_hip_stats* stats) {
+    return solve_impl(method == 1 ? ipo::Method::Intpt : ipo::Method::Hsd, m, n, nz, iA, kA, A, b, c, f, x, y, w, z,
+                      trace, max_iter, timing, stats);
+}
+
+ipo_hip_ctx* ipo_hip_ctx_create(int m, int n, const int* kA, const int* iA, const double* A, const double* b,
+                                const double* c, double f) {
+    try {
+        auto* ctx = new ipo_hip_ctx();
+        ctx->solver = std::make_unique<ipo::IpmSolver>(m, n, kA, iA, A, b, c, f);
+        return ctx;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return nullptr;
+    }
+}
+
+int ipo_hip_ctx_run(ipo_hip_ctx* ctx, int method, int max_iter, FILE* trace, int timing, ipo_hip_stats* stats) {
+    try {
+        ipo::IpmOptions opt;
+        opt.method = method == 1 ? ipo::Method::Intpt : ipo::Method::Hsd;
+        opt.trace = trace;
+        opt.max_iter = max_iter > 0 ? max_iter : 200;
+        opt.timing = timing != 0;
+        ipo::IpmResult res;
+        const int st = ctx->solver->run(opt, &res);
+        fill_stats(stats, res, &ctx->solver->kkt().plan());
+        return st;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return 7;
+    }
+}
+
+void ipo_hip_ctx_download(ipo_hip_ctx* ctx, double* x, double* y, double* w, double* z) {
+    ctx->solver->download(x, y, w, z);
+}
+
+void ipo_hip_ctx_destroy(ipo_hip_ctx* ctx) { delete ctx; }
+
+double ipo_hip_ctx_setup_seconds(const ipo_hip_ctx* ctx) { return ctx->solver->setup_seconds(); }
+
+int ipo_hip_run_mps(const char* path, int method, FILE* out, int timing, ipo_hip_stats* stats) {
+    if (out) {
+        std::fprintf(out, "%s\n%s\n%s%5s%s\n%s\n%s\n", "\t+-------------------------------------------------+",
+                     "\t                                                   ", "\t   ", "./ipo",
+                     ":   Version 1.00 : (Copyright) 1995        ",
+                     "\t                                                   ",
+                     "\t+-------------------------------------------------+");
+        std::fflush(out);
+    }
+    ipo::MpsProblem p;
+    std::string err;
+    const int rc = ipo::read_mps(path, p, &err);
+    if (rc) {
+        set_err(err);
+        if (out) std::fprintf(out, "ERROR(%d): %s\n\n", rc, err.c_str());
+        return -rc;
+    }
+    if (out) std::fprintf(out, "m = %d,n = %d,nz = %d \n", p.m, p.n, p.kA.empty() ? 0 : p.kA[p.n]);
+    ipo::SolverForm s;
+    int status = ipo::to_solver_form(p, s);
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    if (status == 0) {
+        if (out && s.m < 7 && s.n < 7) {   // solve.c:210-222
+            std::fprintf(out, "A: \n");
+            for (int j = 0; j < s.n; j++) {
+                for (int k = s.kA[j]; k < s.kA[j + 1]; k++) std::fprintf(out, "%5d %10.5f \n", s.iA[k], s.A[k]);
+                std::fprintf(out, "\n");
+            }
+            std::fprintf(out, "\n");
+            std::fprintf(out, "b: \n");
+            for (int i = 0; i < s.m; i++) std::fprintf(out, "%10.5f \n", s.b[i]);
+            std::fprintf(out, "\n");
+            std::fprintf(out, "c: \n");
+            for (int j = 0; j < s.n; j++) std::fprintf(out, "%10.5f \n", s.c[j]);
+            std::fprintf(out, "\n");
+        }
+        std::vector<double> x(s.n + s.m, 0.0), y(s.n + s.m, 0.0), w(s.m > 0 ? s.m : 1, 0.0), z(s.n > 0 ? s.n : 1, 0.0);
+        status = solve_impl(method == 1 ? ipo::Method::Intpt : ipo::Method::Hsd, s.m, s.n, s.nz, s.iA.data(),
+                            s.kA.data(), s.A.data(), s.b.data(), s.c.data(), s.f, x.data(), y.data(), w.data(),
+                            z.data(), out, 200, timing, stats);
+    }
+    if (out) { std::fprintf(out, "%s \n", kStatusText[status]); std::fflush(out); }
+    return status;
+}
+
+int ipo_hip_mps_dims(const char* path, int* m0, int* n0, int* nz0, int* m, int* n, int* nz) {
+    ipo::MpsProblem p;
+    std::string err;
+    const int rc = ipo::read_mps(path, p, &err);
+    if (rc) { set_err(err); return rc; }
+    ipo::SolverForm s;
+    const int st = ipo::to_solver_form(p, s);
+    if (m0) *m0 = p.m;
+    if (n0) *n0 = p.n;
+    if (nz0) *nz0 = p.kA.empty() ? 0 : p.kA[p.n];
+    if (m) *m = s.m;
+    if (n) *n = s.n;
+    if (nz) *nz = s.nz;
+    return st;
+}
+
+int ipo_hip_mps_load(const char* path, int* m, int* n, int* nz, int* kA, int* iA, double* A, double* b, double* c,
+                     double* f) {
+    ipo::MpsProblem p;
+    std::string err;
+    const int rc = ipo::read_mps(path, p, &err);
+    if (rc) { set_err(err); return rc; }
+    ipo::SolverForm s;
+    const int st = ipo::to_solver_form(p, s);
+    if (st) return st;
+    if (m) *m = s.m;
+    if (n) *n = s.n;
+    if (nz) *nz = s.nz;
+    if (kA) std::memcpy(kA, s.kA.data(), sizeof(int) * (s.n + 1));
+    if (iA) std::memcpy(iA, s.iA.data(), sizeof(int) * s.nz);
+    if (A) std::memcpy(A, s.A.data(), sizeof(double) * s.nz);
+    if (b) std::memcpy(b, s.b.data(), sizeof(double) * s.m);
+    if (c) std::memcpy(c, s.c.data(), sizeof(double) * s.n);
+    if (f) *f = s.f;
+    return 0;
+}
+
+// ---- LU plug-in (ldlt.h).  In the reference's own naming the matrix is
+// A_l (m x n) with its transpose; solver-side this is A_s = A_l' with
+// E = dn (n entries) and D = dm (m entries), so KktDevice gets kAt/iAt/At.
+void ldltfac(int m, int n, int* kA, int* iA, double* A, double* dn, double* dm, int* kAt, int* iAt, double* At,
+             int verbose) {
+    (void)kA; (void)iA; (void)A; (void)verbose;
+    try {
+        if (!g_lu) {
+            g_lu = new LuState();
+            IPO_HIP_CHECK(hipStreamCreateWithFlags(&g_lu->stream, hipStreamNonBlocking));
+            g_lu->ms = n;
+            g_lu->ns = m;
+            g_lu->kkt = std::make_unique<ipo::KktDevice>(n, m, kAt, iAt, At, g_lu->stream);
+            g_lu->E.alloc(n > 0 ? n : 1);
+            g_lu->fy.alloc(n > 0 ? n : 1);
+            g_lu->D.alloc(m > 0 ? m : 1);
+            g_lu->fx.alloc(m > 0 ? m : 1);
+        }
+        g_lu->E.upload(dn, g_lu->ms, g_lu->stream);
+        g_lu->D.upload(dm, g_lu->ns, g_lu->stream);
+        g_lu->kkt->factor(g_lu->E.get(), g_lu->D.get());
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        std::fprintf(stderr, "ipo_hip ldltfac: %s\n", e.what());
+        std::exit(1);   // the reference exits on allocation failure (myalloc.h:16-44)
+    }
+}
+
+void forwardbackward(double* Dn, double* Dm, double* dx, double* dy) {
+    try {
+        if (!g_lu) throw std::runtime_error("forwardbackward before ldltfac");
+        LuState& L = *g_lu;
+        L.E.upload(Dn, L.ms, L.stream);
+        L.D.upload(Dm, L.ns, L.stream);
+        L.fy.upload(dx, L.ms, L.stream);
+        L.fx.upload(dy, L.ns, L.stream);
+        L.kkt->solve(L.E.get(), L.D.get(), L.fy.get(), L.fx.get());
+        L.fy.download(dx, L.ms, L.stream);
+        L.fx.download(dy, L.ns, L.stream);
+        IPO_HIP_CHECK(hipStreamSynchronize(L.stream));
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        std::fprintf(stderr, "ipo_hip forwardbackward: %s\n", e.what());
+        std::exit(1);
+    }
+}
+
+void inv_clo(void) {
+    if (!g_lu) return;
+    g_lu->kkt.reset();
+    if (g_lu->stream) (void)hipStreamDestroy(g_lu->stream);
+    delete g_lu;
+    g_lu = nullptr;
+}
+
+// ---- KKT handle for tests
+ipo_hip_kkt* ipo_hip_kkt_create(int m, int n, const int* kA, const int* iA, const double* A) {
+    try {
+        auto* k = new ipo_hip_kkt();
+        IPO_HIP_CHECK(hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking));
+        k->m = m;
+        k->n = n;
+        k->kkt = std::make_unique<ipo::KktDevice>(m, n, kA, iA, A, k->stream);
+        k->E.alloc(m > 0 ? m : 1);
+        k->fy.alloc(m > 0 ? m : 1);
+        k->D.alloc(n > 0 ? n : 1);
+        k->fx.alloc(n > 0 ? n : 1);
+        return k;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return nullptr;
+    }
+}
+
+void ipo_hip_kkt_destroy(ipo_hip_kkt* k) {
+    if (!k) return;
+    k->kkt.reset();
+    if (k->stream) (void)hipStreamDestroy(k->stream);
+    delete k;
+}
+
+int ipo_hip_kkt_factor(ipo_hip_kkt* k, const double* E, const double* D) {
+    try {
+        k->E.upload(E, k->m, k->stream);
+        k->D.upload(D, k->n, k->stream);
+        k->kkt->factor(k->E.get(), k->D.get());
+        return 0;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
+
+int ipo_hip_kkt_solve(ipo_hip_kkt* k, const double* E, const double* D, double* fy, double* fx) {
+    try {
+        k->E.upload(E, k->m, k->stream);
+        k->D.upload(D, k->n, k->stream);
+        k->fy.upload(fy, k->m, k->stream);
+        k->fx.upload(fx, k->n, k->stream);
+        const int ok = k->kkt->solve(k->E.get(), k->D.get(), k->fy.get(), k->fx.get());
+        k->fy.download(fy, k->m, k->stream);
+        k->fx.download(fx, k->n, k->stream);
+        IPO_HIP_CHECK(hipStreamSynchronize(k->stream));
+        return ok;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
+
+int ipo_hip_kkt_info(const ipo_hip_kkt* k, long* lnz, double* narth, int* nsup, int* nlevels, int* denwin, int* pdf,
+                     double* epsdiag, int* ndep, int* passes) {
+    const ipo::KktPlan& P = k->kkt->plan();
+    if (lnz) *lnz = P.lnz;
+    if (narth) *narth = P.narth;
+    if (nsup) *nsup = P.nsup;
+    if (nlevels) *nlevels = P.nlevels;
+    if (denwin) *denwin = P.denwin;
+    if (pdf) *pdf = P.pdf;
+    if (epsdiag) *epsdiag = k->kkt->epsdiag();
+    if (ndep) *ndep = k->kkt->ndep();
+    if (passes) *passes = k->kkt->last_passes();
+    return 0;
+}
+
+int ipo_hip_kkt_perm(const ipo_hip_kkt* k, int* perm) {
+    const ipo::KktPlan& P = k->kkt->plan();
+    std::memcpy(perm, P.perm.data(), sizeof(int) * P.T);
+    return 0;
+}
+
+int ipo_hip_symbolic(int m, int n, const int* kA, const int* iA, int* perm, long* lnz, double* narth, int* denwin,
+                     int* pdf, int* nsup, int* nlevels) {
+    try {
+        std::vector<int> kat, iat;
+        std::vector<double> at, a(kA[n], 1.0);
+        ipo::csc_transpose(m, n, kA, iA, a.data(), kat, iat, at);
+        ipo::KktPlan P = ipo::build_kkt_plan(m, n, kA, iA, kat.data(), iat.data());
+        if (perm) std::memcpy(perm, P.perm.data(), sizeof(int) * P.T);
+        if (lnz) *lnz = P.lnz;
+        if (narth) *narth = P.narth;
+        if (denwin) *denwin = P.denwin;
+        if (pdf) *pdf = P.pdf;
+        if (nsup) *nsup = P.nsup;
+        if (nlevels) *nlevels = P.nlevels;
+        return 0;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
+
+int ipo_hip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* ipo_hip_last_error(void) { return g_err.c_str(); }
+const char* ipo_hip_version(void) { return "ipo-hip 0.1 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+// dev_common.h -- device helpers: deterministic block reductions (fixed
+// grid, fixed tree) for dots and max-norms, shared by the KKT and IPM code.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ipo {
+
+constexpr int kRedBlocks = 256;    // fixed partial count -> reproducible sums
+constexpr int kRedThreads = 256;
+
+// the reference's MAX(x,y) = (x > y ? x : y) (macros.h); NaN in x loses
+__device__ __forceinline__ double ref_max(double x, double y) { return x > y ? x : y; }
+__device__ __forceinline__ double ref_abs(double x) { return x > 0 ? x : -x; }
+
+__device__ __forceinline__ double wave_sum(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_down(v, o, 64));
+    return v;
+}
+
+// Sum over a 256-thread block; result valid in thread 0.
+__device__ __forceinline__ double block_sum(double v, double* sh /* >= 4 */) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+    __syncthreads();
+    return r;
+}
+__device__ __forceinline__ double block_max(double v, double* sh) {
+    v = wave_max(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) r = fmax(fmax(sh[0], sh[1]), fmax(sh[2], sh[3]));
+    __syncthreads();
+    return r;
+}
+
+// partials laid out part[q * kRedBlocks + block]; bit q of maxmask selects
+// max instead of sum.  One 256-thread block finishes nq quantities.
+__global__ void __launch_bounds__(kRedThreads)
+k_finish_reduce(const double* __restrict__ part, int nq, unsigned maxmask, double* __restrict__ out);
+
+// Multi-job dot / max-abs partials: job j reduces a[j][i]*b[j][i] (dot) or
+// |a[j][i]| (maxabs, b == nullptr) over i < len[j].
+struct RedJobs {
+    const double* a[8];
+    const double* b[8];
+    int len[8];
+    int op[8];    // 0 = dot, 1 = maxabs, 2 = max(-a/b) (ratio test)
+    int nj;
+};
+__global__ void __launch_bounds__(kRedThreads)
+k_reduce_jobs(RedJobs jobs, double* __restrict__ part);
+
+// Host helper: run jobs, finish into out[0..nj) (device), async on stream.
+void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st);
+
+}  // namespace ipo

@@ -1,0 +1,75 @@
+// ipm.h -- device-resident interior-point drivers behind solver().
+//
+//   Method::Hsd    homogeneous self-dual predictor-corrector, src/ipo/hsd.c:27-311
+//   Method::Intpt  primal-dual path following,               src/ipo/intpt.c:33-261
+//
+// The host keeps the handful of scalars the reference keeps (phi, psi, mu,
+// theta, ...) and prints the reference's per-iteration trace; every O(m+n)
+// vector, both SpMVs and the KKT factor/solve live on the GPU.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <memory>
+
+#include "hip_util.h"
+#include "kkt_device.h"
+
+namespace ipo {
+
+enum class Method { Hsd = 0, Intpt = 1 };
+
+struct IpmOptions {
+    Method method = Method::Hsd;
+    int max_iter = 200;          // MAX_ITER, hsd.c:25 / intpt.c:31
+    FILE* trace = nullptr;       // banner + one line per iteration, reference format
+    bool timing = false;         // per-phase HIP-event timing
+};
+
+struct IpmResult {
+    int status = 5;
+    int iters = 0;
+    double t_setup_s = 0.0;      // symbolic analysis + uploads (first ldltfac in the reference)
+    double t_solve_s = 0.0;      // iteration loop, wall clock
+    double final_mu = 0.0, final_pobj = 0.0, final_dobj = 0.0, final_pinf = 0.0, final_dinf = 0.0;
+    double phi = 1.0, psi = 1.0;
+    KktTimers kkt;
+    long refine_passes = 0;
+};
+
+// Problem uploaded to HBM once; run() iterates from the reference's start
+// point and can be called repeatedly (the bench times run()).
+class IpmSolver {
+  public:
+    IpmSolver(int m, int n, const int* kA, const int* iA, const double* A, const double* b, const double* c,
+              double f, hipStream_t stream = nullptr);
+    ~IpmSolver();
+    int run(const IpmOptions& opt, IpmResult* res);
+    // copy x (n), y (m), w (m), z (n) of the last run to the host
+    void download(double* x, double* y, double* w, double* z) const;
+    KktDevice& kkt() { return *kkt_; }
+    double setup_seconds() const { return t_setup_; }
+
+  private:
+    int run_hsd(const IpmOptions& opt, IpmResult* res);
+    int run_intpt(const IpmOptions& opt, IpmResult* res);
+    void reduce(const struct RedJobs& j, int nout);
+
+    int m_, n_;
+    double f_;
+    hipStream_t stream_;
+    bool own_stream_ = false;
+    double t_setup_ = 0.0;
+    std::unique_ptr<KktDevice> kkt_;
+    DevBuf<double> b_, c_, x_, y_, w_, z_;
+    DevBuf<double> rho_, sig_, D_, E_, fx_, fy_, gx_, gy_, dx_, dy_, dz_, dw_;
+    DevBuf<double> part_, scal_;
+    double* hs_ = nullptr;       // pinned scalars
+};
+
+// Whole-pipeline convenience used by the C ABI: host arrays in, host out.
+int ipm_solve_host(int m, int n, int nz, const int* iA, const int* kA, const double* A, const double* b,
+                   const double* c, double f, double* x, double* y, double* w, double* z, const IpmOptions& opt,
+                   IpmResult* res);
+
+}  // namespace ipo

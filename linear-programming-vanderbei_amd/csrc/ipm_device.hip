@@ -1,0 +1,429 @@
+// ipm_device.hip -- HSD and path-following iterations on gfx950.
+//
+// Fused O(m+n) kernels (HBM-bound; coalesced CSR/CSC gathers, one pass per
+// phase) + the KKT factor/solve of kkt_device.hip.  Per iteration the host
+// reads back only the scalars the reference prints or branches on.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+
+#include "dev_common.h"
+#include "ipm.h"
+
+namespace ipo {
+
+namespace {
+
+constexpr int NT = 256;
+
+__global__ void __launch_bounds__(NT) k_fill(int n, double v, double* __restrict__ a) {
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (i < n) a[i] = v;
+}
+
+// ---------------------------------------------------------------- HSD
+// rows i < m (hsd.c:182-189, 216, 221, 226):
+//   r1 = (A x)_i - b_i phi + w_i ;  ||r1||^2 partial
+//   rho = -(1-delta) r1 + w - delta mu / y ;  E = w / y ;  fy = rho ;  gy = -b
+// cols j < n (hsd.c:191-198, 215, 220, 225):
+//   s1 = -(A'y)_j + c_j phi + z_j ;  ||s1||^2 partial
+//   sigma = -(1-delta) s1 + z - delta mu / x ;  D = z / x ;  fx = -sigma ;  gx = -c
+__global__ void __launch_bounds__(NT)
+k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
+                const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
+                const double* __restrict__ b, const double* __restrict__ c, const double* __restrict__ x,
+                const double* __restrict__ y, const double* __restrict__ w, const double* __restrict__ z, double phi,
+                double delta, double mu, double* __restrict__ E, double* __restrict__ D, double* __restrict__ fy,
+                double* __restrict__ fx, double* __restrict__ gy, double* __restrict__ gx, double* __restrict__ part) {
+    __shared__ double sh[4];
+    double sr = 0.0, ss = 0.0;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
+        if (i < m) {
+            double ax = 0.0;
+            for (int k = kAt[i]; k < kAt[i + 1]; k++) ax += At[k] * x[iAt[k]];
+            const double r1 = ax - b[i] * phi + w[i];
+            sr += r1 * r1;
+            const double rho = -(1 - delta) * r1 + w[i] - delta * mu / y[i];
+            E[i] = w[i] / y[i];
+            fy[i] = rho;
+            gy[i] = -b[i];
+        } else {
+            const int j = i - m;
+            double aty = 0.0;
+            for (int k = kA[j]; k < kA[j + 1]; k++) aty += A[k] * y[iA[k]];
+            const double s1 = -aty + c[j] * phi + z[j];
+            ss += s1 * s1;
+            const double sg = -(1 - delta) * s1 + z[j] - delta * mu / x[j];
+            D[j] = z[j] / x[j];
+            fx[j] = -sg;
+            gx[j] = -c[j];
+        }
+    }
+    sr = block_sum(sr, sh);
+    ss = block_sum(ss, sh);
+    if (threadIdx.x == 0) { part[blockIdx.x] = sr; part[kRedBlocks + blockIdx.x] = ss; }
+}
+
+// directions + ratio test (hsd.c:233-237, 249-256)
+__global__ void __launch_bounds__(NT)
+k_hsd_directions(int m, int n, double dphi, double delta, double mu, const double* __restrict__ fx,
+                 const double* __restrict__ gx, const double* __restrict__ fy, const double* __restrict__ gy,
+                 const double* __restrict__ x, const double* __restrict__ z, const double* __restrict__ y,
+                 const double* __restrict__ w, const double* __restrict__ D, const double* __restrict__ E,
+                 double* __restrict__ dx, double* __restrict__ dz, double* __restrict__ dy, double* __restrict__ dw,
+                 double* __restrict__ part) {
+    __shared__ double sh[4];
+    double th = 0.0;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
+        if (i < n) {
+            const double ddx = fx[i] - gx[i] * dphi;
+            const double ddz = delta * mu / x[i] - z[i] - D[i] * ddx;
+            dx[i] = ddx; dz[i] = ddz;
+            th = fmax(th, -ddx / x[i]);
+            th = fmax(th, -ddz / z[i]);
+        } else {
+            const int j = i - n;
+            const double ddy = fy[j] - gy[j] * dphi;
+            const double ddw = delta * mu / y[j] - w[j] - E[j] * ddy;
+            dy[j] = ddy; dw[j] = ddw;
+            th = fmax(th, -ddy / y[j]);
+            th = fmax(th, -ddw / w[j]);
+        }
+    }
+    th = block_max(th, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = th;
+}
+
+__global__ void __launch_bounds__(NT)
+k_step(int m, int n, double theta, double* __restrict__ x, const double* __restrict__ dx, double* __restrict__ z,
+       const double* __restrict__ dz, double* __restrict__ y, const double* __restrict__ dy, double* __restrict__ w,
+       const double* __restrict__ dw) {
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (i < n) { x[i] = x[i] + theta * dx[i]; z[i] = z[i] + theta * dz[i]; }
+    else if (i < n + m) { const int j = i - n; y[j] = y[j] + theta * dy[j]; w[j] = w[j] + theta * dw[j]; }
+}
+
+__global__ void __launch_bounds__(NT)
+k_unscale(int m, int n, double phi, double* __restrict__ x, double* __restrict__ z, double* __restrict__ y,
+          double* __restrict__ w) {
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (i < n) { x[i] /= phi; z[i] /= phi; }
+    else if (i < n + m) { const int j = i - n; y[j] /= phi; w[j] /= phi; }
+}
+
+// ---------------------------------------------------------------- intpt
+// rho = b - A x - w, sigma = c - A'y + z and their squared norms (intpt.c:139-149)
+__global__ void __launch_bounds__(NT)
+k_pf_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
+               const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
+               const double* __restrict__ b, const double* __restrict__ c, const double* __restrict__ x,
+               const double* __restrict__ y, const double* __restrict__ w, const double* __restrict__ z,
+               double* __restrict__ rho, double* __restrict__ sig, double* __restrict__ part) {
+    __shared__ double sh[4];
+    double sr = 0.0, ss = 0.0;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
+        if (i < m) {
+            double ax = 0.0;
+            for (int k = kAt[i]; k < kAt[i + 1]; k++) ax += At[k] * x[iAt[k]];
+            const double r = b[i] - ax - w[i];
+            rho[i] = r;
+            sr += r * r;
+        } else {
+            const int j = i - m;
+            double aty = 0.0;
+            for (int k = kA[j]; k < kA[j + 1]; k++) aty += A[k] * y[iA[k]];
+            const double s = c[j] - aty + z[j];
+            sig[j] = s;
+            ss += s * s;
+        }
+    }
+    sr = block_sum(sr, sh);
+    ss = block_sum(ss, sh);
+    if (threadIdx.x == 0) { part[blockIdx.x] = sr; part[kRedBlocks + blockIdx.x] = ss; }
+}
+
+// D, E and the right-hand side (intpt.c:194-200)
+__global__ void __launch_bounds__(NT)
+k_pf_rhs(int m, int n, double mu, const double* __restrict__ x, const double* __restrict__ z,
+         const double* __restrict__ y, const double* __restrict__ w, const double* __restrict__ rho,
+         const double* __restrict__ sig, double* __restrict__ D, double* __restrict__ E, double* __restrict__ dx,
+         double* __restrict__ dy) {
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (i < n) { D[i] = z[i] / x[i]; dx[i] = sig[i] - z[i] + mu / x[i]; }
+    else if (i < n + m) { const int j = i - n; E[j] = w[j] / y[j]; dy[j] = rho[j] + w[j] - mu / y[j]; }
+}
+
+// dz, dw and the ratio test (intpt.c:204-219)
+__global__ void __launch_bounds__(NT)
+k_pf_directions(int m, int n, double mu, const double* __restrict__ x, const double* __restrict__ z,
+                const double* __restrict__ y, const double* __restrict__ w, const double* __restrict__ D,
+                const double* __restrict__ E, const double* __restrict__ dx, const double* __restrict__ dy,
+                double* __restrict__ dz, double* __restrict__ dw, double* __restrict__ part) {
+    __shared__ double sh[4];
+    double th = 0.0;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
+        if (i < n) {
+            const double v = mu / x[i] - z[i] - D[i] * dx[i];
+            dz[i] = v;
+            th = fmax(th, -dx[i] / x[i]);
+            th = fmax(th, -v / z[i]);
+        } else {
+            const int j = i - n;
+            const double v = mu / y[j] - w[j] - E[j] * dy[j];
+            dw[j] = v;
+            th = fmax(th, -dy[j] / y[j]);
+            th = fmax(th, -v / w[j]);
+        }
+    }
+    th = block_max(th, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = th;
+}
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+const char* kHsdHeader =
+    "--------------------------------------------------------------------------\n"
+    "         |           Primal          |            Dual           |       |\n"
+    "  Iter   |  Obj Value       Infeas   |  Obj Value       Infeas   |  mu   |\n"
+    "- - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - \n";
+const char* kIntptHeader =
+    "------------------------------------------------------------------\n"
+    "         |           Primal          |            Dual           |\n"
+    "  Iter   |  Obj Value       Infeas   |  Obj Value       Infeas   |\n"
+    "- - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - \n";
+
+}  // namespace
+
+IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A, const double* b, const double* c,
+                     double f, hipStream_t stream)
+    : m_(m), n_(n), f_(f), stream_(stream) {
+    const double t0 = now_s();
+    if (!stream_) {
+        IPO_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        own_stream_ = true;
+    }
+    kkt_ = std::make_unique<KktDevice>(m, n, kA, iA, A, stream_);
+    const size_t mm = m > 0 ? m : 1, nn = n > 0 ? n : 1;
+    b_.upload(b, m, stream_);
+    c_.upload(c, n, stream_);
+    for (DevBuf<double>* v : {&x_, &z_, &sig_, &D_, &fx_, &gx_, &dx_, &dz_}) v->alloc(nn);
+    for (DevBuf<double>* v : {&y_, &w_, &rho_, &E_, &fy_, &gy_, &dy_, &dw_}) v->alloc(mm);
+    if (m == 0) b_.alloc(1);
+    if (n == 0) c_.alloc(1);
+    part_.alloc(8 * kRedBlocks);
+    scal_.alloc(16);
+    IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hs_), 16 * sizeof(double), hipHostMallocDefault));
+    IPO_HIP_CHECK(hipStreamSynchronize(stream_));
+    t_setup_ = now_s() - t0;
+}
+
+IpmSolver::~IpmSolver() {
+    if (hs_) (void)hipHostFree(hs_);
+    kkt_.reset();
+    if (own_stream_) (void)hipStreamDestroy(stream_);
+}
+
+void IpmSolver::reduce(const RedJobs& j, int nout) {
+    launch_reduce(j, part_.get(), scal_.get(), stream_);
+    IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), nout * sizeof(double), hipMemcpyDeviceToHost, stream_));
+    IPO_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void IpmSolver::download(double* x, double* y, double* w, double* z) const {
+    if (x) x_.download(x, n_, stream_);
+    if (y) y_.download(y, m_, stream_);
+    if (w) w_.download(w, m_, stream_);
+    if (z) z_.download(z, n_, stream_);
+    IPO_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+int IpmSolver::run(const IpmOptions& opt, IpmResult* res) {
+    IpmResult local;
+    if (!res) res = &local;
+    *res = IpmResult();
+    res->t_setup_s = t_setup_;
+    kkt_->enable_timing(opt.timing);
+    const double t0 = now_s();
+    const int st = opt.method == Method::Intpt ? run_intpt(opt, res) : run_hsd(opt, res);
+    res->t_solve_s = now_s() - t0;
+    res->status = st;
+    res->kkt = kkt_->timers();
+    return st;
+}
+
+int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
+    const int m = m_, n = n_;
+    hipStream_t s = stream_;
+    const int gv = ceil_div(m + n, NT);
+    FILE* tr = opt.trace;
+    hipLaunchKernelGGL(k_fill, dim3(ceil_div(n, NT)), dim3(NT), 0, s, n, 1.0, x_.get());
+    hipLaunchKernelGGL(k_fill, dim3(ceil_div(n, NT)), dim3(NT), 0, s, n, 1.0, z_.get());
+    hipLaunchKernelGGL(k_fill, dim3(ceil_div(m, NT)), dim3(NT), 0, s, m, 1.0, w_.get());
+    hipLaunchKernelGGL(k_fill, dim3(ceil_div(m, NT)), dim3(NT), 0, s, m, 1.0, y_.get());
+    double phi = 1.0, psi = 1.0;
+    if (tr) {
+        std::fprintf(tr, "m = %d,n = %d,nz = %d\n", m, n, kkt_->plan().amap.empty() ? 0 : (int)kkt_->plan().amap.size());
+        std::fputs(kHsdHeader, tr);
+        std::fflush(tr);
+    }
+    KktDevice& K = *kkt_;
+    int status = 5, iter;
+    for (iter = 0; iter < opt.max_iter; iter++) {
+        RedJobs j{};
+        j.nj = 4;
+        j.a[0] = z_.get(); j.b[0] = x_.get(); j.len[0] = n; j.op[0] = 0;
+        j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = m; j.op[1] = 0;
+        j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
+        j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = m; j.op[3] = 0;
+        reduce(j, 4);
+        const double mu = (hs_[0] + hs_[1] + phi * psi) / (n + m + 1);
+        const double delta = (iter % 2 == 0) ? 0.0 : 1.0;
+        const double pobj = hs_[2], dobj = hs_[3];
+        if (mu < 1.0e-12) {
+            if (phi > psi) status = 0;
+            else if (dobj < 0.0) status = 2;
+            else if (pobj > 0.0) status = 4;
+            else { if (tr) std::fprintf(tr, "Trouble in river city \n"); status = 4; }
+            break;
+        }
+        hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(NT), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
+                           K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), phi, delta, mu,
+                           E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get());
+        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get());
+        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        const double normr = std::sqrt(hs_[0]) / phi;
+        const double norms = std::sqrt(hs_[1]) / phi;
+        const double gamma = -(1 - delta) * (dobj - pobj + psi) + psi - delta * mu / phi;
+        if (tr) {
+            std::fprintf(tr, "%8d   %14.7e  %8.1e    %14.7e  %8.1e  %8.1e \n", iter, pobj / phi + f_, normr,
+                         dobj / phi + f_, norms, mu);
+            std::fflush(tr);
+        }
+        res->final_mu = mu; res->final_pobj = pobj / phi + f_; res->final_dobj = dobj / phi + f_;
+        res->final_pinf = normr; res->final_dinf = norms;
+
+        K.factor(E_.get(), D_.get());
+        K.solve(E_.get(), D_.get(), fy_.get(), fx_.get());
+        res->refine_passes += K.last_passes();
+        K.solve(E_.get(), D_.get(), gy_.get(), gx_.get());
+        res->refine_passes += K.last_passes();
+
+        RedJobs q{};
+        q.nj = 4;
+        q.a[0] = c_.get(); q.b[0] = fx_.get(); q.len[0] = n; q.op[0] = 0;
+        q.a[1] = b_.get(); q.b[1] = fy_.get(); q.len[1] = m; q.op[1] = 0;
+        q.a[2] = c_.get(); q.b[2] = gx_.get(); q.len[2] = n; q.op[2] = 0;
+        q.a[3] = b_.get(); q.b[3] = gy_.get(); q.len[3] = m; q.op[3] = 0;
+        reduce(q, 4);
+        const double dphi = (hs_[0] - hs_[1] + gamma) / (hs_[2] - hs_[3] - psi / phi);
+        const double dpsi = delta * mu / phi - psi - (psi / phi) * dphi;
+
+        hipLaunchKernelGGL(k_hsd_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dphi, delta, mu, fx_.get(),
+                           gx_.get(), fy_.get(), gy_.get(), x_.get(), z_.get(), y_.get(), w_.get(), D_.get(), E_.get(),
+                           dx_.get(), dz_.get(), dy_.get(), dw_.get(), part_.get());
+        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 1, 1u, scal_.get());
+        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        double theta = hs_[0];
+        if (theta < -dphi / phi) theta = -dphi / phi;
+        if (theta < -dpsi / psi) theta = -dpsi / psi;
+        theta = (0.95 / theta > 1.0) ? 1.0 : 0.95 / theta;
+
+        hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, theta, x_.get(), dx_.get(), z_.get(), dz_.get(),
+                           y_.get(), dy_.get(), w_.get(), dw_.get());
+        phi = phi + theta * dphi;
+        psi = psi + theta * dpsi;
+    }
+    hipLaunchKernelGGL(k_unscale, dim3(gv), dim3(NT), 0, s, m, n, phi, x_.get(), z_.get(), y_.get(), w_.get());
+    IPO_HIP_CHECK(hipGetLastError());
+    IPO_HIP_CHECK(hipStreamSynchronize(s));
+    res->iters = iter;
+    res->phi = phi;
+    res->psi = psi;
+    return status;
+}
+
+int IpmSolver::run_intpt(const IpmOptions& opt, IpmResult* res) {
+    const int m = m_, n = n_;
+    hipStream_t s = stream_;
+    const int gv = ceil_div(m + n, NT);
+    FILE* tr = opt.trace;
+    for (DevBuf<double>* v : {&x_, &z_}) hipLaunchKernelGGL(k_fill, dim3(ceil_div(n, NT)), dim3(NT), 0, s, n, 1000.0, v->get());
+    for (DevBuf<double>* v : {&y_, &w_}) hipLaunchKernelGGL(k_fill, dim3(ceil_div(m, NT)), dim3(NT), 0, s, m, 1000.0, v->get());
+    const double delta = 0.02, r = 0.9;
+    double normr0 = HUGE_VAL, norms0 = HUGE_VAL;
+    if (tr) {
+        std::fprintf(tr, "m = %d,n = %d,nz = %d\n", m, n, (int)kkt_->plan().amap.size());
+        std::fputs(kIntptHeader, tr);
+        std::fflush(tr);
+    }
+    KktDevice& K = *kkt_;
+    int status = 5, iter;
+    for (iter = 0; iter < opt.max_iter; iter++) {
+        hipLaunchKernelGGL(k_pf_residuals, dim3(kRedBlocks), dim3(NT), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
+                           K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), rho_.get(),
+                           sig_.get(), part_.get());
+        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get() + 8);
+        RedJobs j{};
+        j.nj = 4;
+        j.a[0] = z_.get(); j.b[0] = x_.get(); j.len[0] = n; j.op[0] = 0;
+        j.a[1] = y_.get(); j.b[1] = w_.get(); j.len[1] = m; j.op[1] = 0;
+        j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
+        j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = m; j.op[3] = 0;
+        launch_reduce(j, part_.get(), scal_.get(), s);
+        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 10 * sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        // intpt.c:47 keeps the printed quantities in single precision
+        const float normr = static_cast<float>(std::sqrt(hs_[8]));
+        const float norms = static_cast<float>(std::sqrt(hs_[9]));
+        const double gamma = hs_[0] + hs_[1];
+        const float pobj = static_cast<float>(hs_[2] + f_);
+        const float dobj = static_cast<float>(hs_[3] + f_);
+        if (tr) {
+            std::fprintf(tr, "%8d   %14.7e  %8.1e    %14.7e  %8.1e \n", iter, pobj, normr, dobj, norms);
+            std::fflush(tr);
+        }
+        res->final_mu = gamma; res->final_pobj = pobj; res->final_dobj = dobj;
+        res->final_pinf = normr; res->final_dinf = norms;
+        if (normr < 1.0e-6 && norms < 1.0e-6 && gamma < 1.0e-6) { status = 0; break; }
+        if (normr > 10 * normr0) { status = 2; break; }
+        if (norms > 10 * norms0) { status = 4; break; }
+        const double mu = delta * gamma / (n + m);
+        hipLaunchKernelGGL(k_pf_rhs, dim3(gv), dim3(NT), 0, s, m, n, mu, x_.get(), z_.get(), y_.get(), w_.get(),
+                           rho_.get(), sig_.get(), D_.get(), E_.get(), dx_.get(), dy_.get());
+        K.factor(E_.get(), D_.get());
+        K.solve(E_.get(), D_.get(), dy_.get(), dx_.get());
+        res->refine_passes += K.last_passes();
+        hipLaunchKernelGGL(k_pf_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, mu, x_.get(), z_.get(), y_.get(),
+                           w_.get(), D_.get(), E_.get(), dx_.get(), dy_.get(), dz_.get(), dw_.get(), part_.get());
+        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 1, 1u, scal_.get());
+        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        double theta = hs_[0];
+        theta = (r / theta > 1.0) ? 1.0 : r / theta;
+        hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, theta, x_.get(), dx_.get(), z_.get(), dz_.get(),
+                           y_.get(), dy_.get(), w_.get(), dw_.get());
+        normr0 = normr;
+        norms0 = norms;
+    }
+    IPO_HIP_CHECK(hipGetLastError());
+    IPO_HIP_CHECK(hipStreamSynchronize(s));
+    res->iters = iter;
+    return status;
+}
+
+int ipm_solve_host(int m, int n, int nz, const int* iA, const int* kA, const double* A, const double* b,
+                   const double* c, double f, double* x, double* y, double* w, double* z, const IpmOptions& opt,
+                   IpmResult* res) {
+    (void)nz;
+    IpmSolver S(m, n, kA, iA, A, b, c, f);
+    const int st = S.run(opt, res);
+    S.download(x, y, w, z);
+    return st;
+}
+
+}  // namespace ipo

@@ -1,0 +1,107 @@
+// kkt_device.h -- device-resident numeric LDL^T of the ipo KKT matrix.
+//
+// Replaces the numeric half of src/ipo/ldlt.c:
+//   factor()   <- inv_num  ldlt.c:164-309 (assembly, lltnum :517-636,
+//                 dependent-pivot rule :600-614, eps_diag growth :293-306)
+//   solve()    <- solve    ldlt.c:327-425 (iterative refinement) with
+//                 rawsolve ldlt.c:433-505 as supernodal level sweeps
+// Everything stays in HBM between calls; only a few scalars (refinement
+// residual, min |d|, dependent-pivot count) come back to the host.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "hip_util.h"
+#include "kkt_plan.h"
+
+namespace ipo {
+
+struct KktTimers {
+    double factor_ms = 0.0;   // accumulated device time of factor()
+    double solve_ms = 0.0;    // accumulated device time of solve()
+    double update_ms = 0.0;   // k_update launches only (timing mode)
+    double panel_ms = 0.0;    // k_factor launches only (timing mode)
+    double sweep_ms = 0.0;    // forward + backward substitution sweeps (timing mode)
+    long update_launches = 0, panel_launches = 0;
+    long factors = 0, solves = 0, rawsolves = 0;
+};
+
+class KktDevice {
+  public:
+    // A is the solver's m x n matrix (CSC).  The plan (ordering, supernodes)
+    // is computed here on the host.  kA/iA/A must outlive nothing: copied.
+    KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream);
+    ~KktDevice();
+    KktDevice(const KktDevice&) = delete;
+    KktDevice& operator=(const KktDevice&) = delete;
+
+    const KktPlan& plan() const { return plan_; }
+    int m() const { return m_; }
+    int n() const { return n_; }
+    hipStream_t stream() const { return stream_; }
+
+    // Device copies of the constraint matrix in both orientations.
+    const int* kA() const { return dkA_.get(); }
+    const int* iA() const { return diA_.get(); }
+    const double* A() const { return dA_.get(); }
+    const int* kAt() const { return dkAt_.get(); }
+    const int* iAt() const { return diAt_.get(); }
+    const double* At() const { return dAt_.get(); }
+
+    // Numeric factorisation of K(E, D); E (m), D (n) are device vectors.
+    void factor(const double* dE, const double* dD);
+    // In-place refined solve of  -E dy + A dx = fy,  A' dy + D dx = fx.
+    // Returns the rawsolve consistency flag of the last pass (1 = consistent).
+    int solve(const double* dE, const double* dD, double* dfy, double* dfx);
+
+    // One unrefined sweep L D L' z = rhs on a permuted device vector.
+    void rawsolve(double* dz);
+
+    double epsdiag() const { return epsdiag_; }
+    int ndep() const { return ndep_; }
+    int last_passes() const { return last_passes_; }
+    const KktTimers& timers() const { return tm_; }
+    void enable_timing(bool on) { timing_ = on; }
+
+    // Diagnostics: copy numeric factor to host (panels + D), for tests.
+    void download_factor(double* lx, double* d) const;
+    double* device_lx() const { return dLx_.get(); }
+    double* device_diag() const { return dDg_.get(); }
+
+  private:
+    void launch_reduce_maxabs2(const double* a, int na, const double* b, int nb, double* dst);
+
+    int m_, n_, T_;
+    hipStream_t stream_;
+    KktPlan plan_;
+    double epsdiag_ = 1.0e-14;     // ldlt.c:31, grows x10 (ldlt.c:301-305)
+    int ndep_ = 0;
+    int last_passes_ = 0;
+    bool timing_ = false;
+    KktTimers tm_;
+    hipEvent_t ev0_ = nullptr, ev1_ = nullptr, ev2_ = nullptr, ev3_ = nullptr;
+    std::vector<hipEvent_t> kev_;   // per-launch event pairs (timing mode)
+
+    // matrix
+    DevBuf<int> dkA_, diA_, dkAt_, diAt_;
+    DevBuf<double> dA_, dAt_;
+    // plan
+    DevBuf<int> dcol0_, drowptr_, drows_, dperm_, diperm_;
+    DevBuf<int64_t> doff_, damap_, ddslot_, drelptr_, dfrow_pos_;
+    DevBuf<int> dunit_sup_, dunit_tile_, dtask_ptr_, dtask_pair_, dtask_i0_, dtask_i1_;
+    DevBuf<int> dupd_src_, dupd_r0_, dupd_r1_, drel_, dlevel_sups_;
+    DevBuf<int> dfrow_ptr_, dfrow_col_;
+    // numeric
+    DevBuf<double> dLx_, dDg_;
+    DevBuf<int> dLive_;
+    DevBuf<int> dFlags_;           // [0] ndep, [1] inconsistent
+    DevBuf<double> dZ_, dDy_, dDx_, dRy_, dRx_;
+    DevBuf<double> dPart_, dScal_;
+    double* hScal_ = nullptr;      // pinned
+    int* hFlags_ = nullptr;        // pinned
+};
+
+}  // namespace ipo

@@ -1,0 +1,622 @@
+// kkt_device.hip -- supernodal LDL^T of the quasi-definite KKT matrix on
+// gfx950 (see kkt_device.h for the reference mapping).
+//
+// Data layout in HBM
+//   Lx    supernode panels, column-major, panel s = h_s x nc_s (ld = h_s):
+//         rows 0..nc-1 are the diagonal block (unit lower L11 after the
+//         factor, diagonal slots hold K's diagonal on input), rows nc..h-1
+//         are the rows R_s of L21.  One contiguous array, 8-B aligned.
+//   dg    D of L D L' (new index order), live = the reference's mark[].
+//
+// Factor = per elimination-tree level two kernels:
+//   k_update  one workgroup per (panel, 64-row tile): left-looking gather
+//             of every descendant panel's rank-nc_d update into an LDS tile
+//             (fixed task order -> bitwise reproducible), then subtract.
+//   k_factor  same units: dense LDL' of the diagonal block in LDS (redundant
+//             per tile, tiny), dependent-pivot rule of ldlt.c:600-614, then
+//             the triangular solve of the tile's L21 rows.
+// Solve = per level: forward row-gather + in-wave block substitution +
+// diagonal scaling (bottom-up), then column-gather + block back substitution
+// (top-down).  Refinement loop as ldlt.c:367-416.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+#include "dev_common.h"
+#include "kkt_device.h"
+#include "lp_io.h"
+
+namespace ipo {
+
+namespace {
+
+constexpr int TR = kTileRows;     // 64
+constexpr int PC = kPanelCols;    // 64
+constexpr int NT = 256;           // threads per workgroup
+
+struct PlanView {
+    const int* col0;
+    const int* rowptr;
+    const int* rows;
+    const int64_t* off;
+    const int* unit_sup;
+    const int* unit_tile;
+    const int* task_ptr;
+    const int* task_pair;
+    const int* task_i0;
+    const int* task_i1;
+    const int* upd_src;
+    const int* upd_r0;
+    const int* upd_r1;
+    const int64_t* relptr;
+    const int* rel;
+    double* Lx;
+    double* dg;
+    int* live;
+    int* flags;      // [0] dependent pivots, [1] inconsistent system
+    const int* sign; // node class per new index: -1 y-node, +1 x-node
+};
+
+// ---------------------------------------------------------------- assembly
+__global__ void __launch_bounds__(NT)
+k_assemble_A(int nz, const double* __restrict__ A, const int64_t* __restrict__ amap, double* __restrict__ Lx) {
+    const int k = blockIdx.x * NT + threadIdx.x;
+    if (k < nz) Lx[amap[k]] = A[k];
+}
+
+// K's diagonal: -max(E, eps) on y-nodes, +max(D, eps) on x-nodes (ldlt.c:235-236)
+__global__ void __launch_bounds__(NT)
+k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __restrict__ E,
+                const double* __restrict__ D, double eps, const int64_t* __restrict__ dslot,
+                double* __restrict__ Lx, int* __restrict__ live) {
+    const int v = blockIdx.x * NT + threadIdx.x;
+    if (v >= T) return;
+    const int old = perm[v];
+    Lx[dslot[v]] = old < m ? -ref_max(E[old], eps) : ref_max(D[old - m], eps);
+    live[v] = 1;
+}
+
+// ------------------------------------------------------- left-looking gather
+__global__ void __launch_bounds__(NT)
+k_update(PlanView p, int u0) {
+    __shared__ double acc[TR][PC + 1];
+    const int u = u0 + blockIdx.x;
+    const int s = p.unit_sup[u], t = p.unit_tile[u];
+    const int tb = p.task_ptr[u], te = p.task_ptr[u + 1];
+    if (tb == te) return;
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+    const int rbase = t * TR;
+    const int nrow = min(TR, h - rbase);
+    for (int i = threadIdx.x; i < TR * (PC + 1); i += NT) (&acc[0][0])[i] = 0.0;
+    __syncthreads();
+    for (int task = tb; task < te; task++) {
+        const int q = p.task_pair[task];
+        const int i0 = p.task_i0[task], i1 = p.task_i1[task];
+        const int d = p.upd_src[q];
+        const int cd0 = p.col0[d], ncd = p.col0[d + 1] - cd0;
+        const int hd = ncd + (p.rowptr[d + 1] - p.rowptr[d]);
+        const int r0 = p.upd_r0[q];
+        const int ncols = p.upd_r1[q] - r0;
+        const double* __restrict__ Ld = p.Lx + p.off[d] + ncd + r0;
+        const double* __restrict__ dd = p.dg + cd0;
+        const int* __restrict__ rl = p.rel + p.relptr[q];
+        const int nr = i1 - i0;
+        const int tot = nr * ncols;
+        for (int idx = threadIdx.x; idx < tot; idx += NT) {
+            const int ii = i0 + idx % nr;
+            const int jj = idx / nr;
+            const int prow = rl[ii], pcol = rl[jj];
+            if (prow < pcol) continue;
+            double sum = 0.0;
+            for (int k = 0; k < ncd; k++) sum += Ld[ii + (size_t)k * hd] * (dd[k] * Ld[jj + (size_t)k * hd]);
+            acc[prow - rbase][pcol] += sum;
+        }
+        __syncthreads();
+    }
+    double* panel = p.Lx + p.off[s];
+    for (int idx = threadIdx.x; idx < nrow * nc; idx += NT) {
+        const int r = idx % nrow, c = idx / nrow;
+        if (rbase + r >= c) panel[(rbase + r) + (size_t)c * h] -= acc[r][c];
+    }
+}
+
+// ------------------------------------------- diagonal block LDL' + L21 solve
+__global__ void __launch_bounds__(NT)
+k_factor(PlanView p, int u0) {
+    __shared__ double B[PC][PC + 1];      // diagonal block, B[row][col]
+    __shared__ double R[TR][PC + 1];      // this tile's L21 rows
+    __shared__ double dv[PC];
+    __shared__ int lv[PC];
+    __shared__ double red[4];
+    __shared__ int ndep_sh;
+    const int u = u0 + blockIdx.x;
+    const int s = p.unit_sup[u], t = p.unit_tile[u];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+    double* panel = p.Lx + p.off[s];
+    const int tid = threadIdx.x;
+
+    for (int idx = tid; idx < nc * nc; idx += NT) {
+        const int r = idx % nc, c = idx / nc;
+        B[r][c] = r >= c ? panel[r + (size_t)c * h] : 0.0;
+    }
+    if (tid == 0) ndep_sh = 0;
+    __syncthreads();
+
+    for (int k = 0; k < nc; k++) {
+        double dk = B[k][k];
+        int alive = 1;
+        if (fabs(dk) <= 0.0) {                    // epsnum = 0 (ldlt.c:29): exact zero pivot
+            // largest off-diagonal magnitude of column k after all updates
+            // from columns < k: block rows are in B, rows below are rebuilt
+            // here by a partial forward solve (rare path).
+            double mx = 0.0;
+            for (int r = k + 1 + tid; r < nc; r += NT) mx = ref_max(mx, ref_abs(B[r][k]));
+            for (int rr = nc + tid; rr < h; rr += NT) {
+                double w[PC];
+                for (int c = 0; c <= k; c++) w[c] = panel[rr + (size_t)c * h];
+                for (int j = 0; j < k; j++) {
+                    const double wj = lv[j] ? w[j] : 0.0;
+                    for (int c = j + 1; c <= k; c++) w[c] -= wj * B[c][j];
+                }
+                mx = ref_max(mx, ref_abs(w[k]));
+            }
+            mx = block_max(mx, red);
+            if (tid == 0) red[0] = mx;
+            __syncthreads();
+            mx = red[0];
+            if (mx < 1.0e+6 * 1.0e-8) alive = 0;              // column dropped, d stays 0
+            else dk = (p.sign[c0 + k] < 0 ? -1.0 : 1.0) * 1.0e-8;   // y-nodes -, x-nodes +
+            if (tid == 0) ndep_sh++;
+            __syncthreads();
+        }
+        if (tid == 0) { dv[k] = dk; lv[k] = alive; }
+        __syncthreads();
+        // right-looking update of the trailing block, then scale column k
+        if (alive) {
+            const double inv = 1.0 / dk;
+            for (int idx = tid; idx < (nc - k - 1) * (nc - k - 1); idx += NT) {
+                const int r = k + 1 + idx % (nc - k - 1);
+                const int c = k + 1 + idx / (nc - k - 1);
+                if (r >= c) B[r][c] -= B[r][k] * (B[c][k] * inv);
+            }
+        }
+        __syncthreads();
+        for (int r = k + 1 + tid; r < nc; r += NT) B[r][k] = alive ? B[r][k] / dk : 0.0;
+        __syncthreads();
+    }
+
+    if (t == 0) {
+        for (int idx = tid; idx < nc * nc; idx += NT) {
+            const int r = idx % nc, c = idx / nc;
+            if (r > c) panel[r + (size_t)c * h] = B[r][c];
+        }
+        for (int k = tid; k < nc; k += NT) { p.dg[c0 + k] = dv[k]; p.live[c0 + k] = lv[k]; }
+        if (tid == 0 && ndep_sh) atomicAdd(&p.flags[0], ndep_sh);
+    }
+
+    // L21 rows of this tile: w = a - sum_j w_j L11(k, j); l = w / d
+    const int rbase = t * TR;
+    const int rlo = max(rbase, nc), rhi = min(rbase + TR, h);
+    const int nrow = rhi - rlo;
+    if (nrow <= 0) return;
+    for (int idx = tid; idx < nrow * nc; idx += NT) {
+        const int r = idx % nrow, c = idx / nrow;
+        R[r][c] = panel[(rlo + r) + (size_t)c * h];
+    }
+    __syncthreads();
+    const int r = tid & 63, part = tid >> 6;
+    for (int k = 0; k < nc; k++) {
+        const double wk = r < nrow ? R[r][k] : 0.0;
+        __syncthreads();
+        if (r < nrow) {
+            for (int c = k + 1 + part; c < nc; c += 4) R[r][c] -= wk * B[c][k];
+            if (part == 0) R[r][k] = lv[k] ? wk / dv[k] : 0.0;
+        }
+        __syncthreads();
+    }
+    for (int idx = tid; idx < nrow * nc; idx += NT) {
+        const int rr = idx % nrow, c = idx / nrow;
+        panel[(rlo + rr) + (size_t)c * h] = R[rr][c];
+    }
+}
+
+// -------------------------------------------------------------- solves
+// z (permuted) -> L^{-1} z, then D^{-1}, one level of supernodes per launch.
+__global__ void __launch_bounds__(NT)
+k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ frow_ptr,
+          const int* __restrict__ frow_col, const int64_t* __restrict__ frow_pos, double* __restrict__ z,
+          const double* __restrict__ epsp) {
+    __shared__ double zl[PC];
+    const int s = level_sups[q0 + blockIdx.x];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+    const double* panel = p.Lx + p.off[s];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k = wv; k < nc; k += 4) {
+        const int v = c0 + k;
+        double acc = 0.0;
+        for (int e = frow_ptr[v] + lane; e < frow_ptr[v + 1]; e += 64) acc += p.Lx[frow_pos[e]] * z[frow_col[e]];
+        acc = wave_sum(acc);
+        if (lane == 0) zl[k] = z[v] - acc;
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    const double eps = *epsp;
+    double zr = lane < nc ? zl[lane] : 0.0;
+    int bad = 0;
+    for (int j = 0; j < nc; j++) {
+        const int alive = p.live[c0 + j];
+        if (lane == j && !alive) {
+            if (fabs(zr) > eps) bad = 1;
+            else zr = 0.0;
+        }
+        const double zj = __shfl(zr, j, 64);
+        if (alive && lane > j && lane < nc) zr -= panel[lane + (size_t)j * h] * zj;
+    }
+    if (lane < nc) {
+        const int v = c0 + lane;
+        if (p.live[v]) zr = zr / p.dg[v];
+        else if (fabs(zr) > eps) bad = 1;
+        else zr = 0.0;
+        z[v] = zr;
+    }
+    if (bad) atomicOr(&p.flags[1], 1);
+}
+
+// z -> L^{-T} z, top-down.
+__global__ void __launch_bounds__(NT)
+k_backward(PlanView p, const int* __restrict__ level_sups, int q0, double* __restrict__ z,
+           const double* __restrict__ epsp) {
+    __shared__ double zl[PC];
+    const int s = level_sups[q0 + blockIdx.x];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int hb = p.rowptr[s + 1] - p.rowptr[s];
+    const int h = nc + hb;
+    const double* panel = p.Lx + p.off[s];
+    const int* rows = p.rows + p.rowptr[s];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int k = wv; k < nc; k += 4) {
+        const double* col = panel + (size_t)k * h + nc;
+        double acc = 0.0;
+        for (int i = lane; i < hb; i += 64) acc += col[i] * z[rows[i]];
+        acc = wave_sum(acc);
+        if (lane == 0) zl[k] = z[c0 + k] - acc;
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    const double eps = *epsp;
+    double zr = lane < nc ? zl[lane] : 0.0;
+    int bad = 0;
+    for (int j = nc - 1; j >= 0; j--) {
+        const int alive = p.live[c0 + j];
+        if (lane == j && !alive) {
+            if (fabs(zr) > eps) bad = 1;
+            else zr = 0.0;
+        }
+        const double zj = __shfl(zr, j, 64);
+        if (alive && lane < j) zr -= panel[j + (size_t)lane * h] * zj;
+    }
+    if (lane < nc) z[c0 + lane] = zr;
+    if (bad) atomicOr(&p.flags[1], 1);
+}
+
+// -------------------------------------------------------- refinement glue
+// z[v] = rhs(perm[v]) with rhs = (fy | fx)
+__global__ void __launch_bounds__(NT)
+k_perm_in(int T, int m, const int* __restrict__ perm, const double* __restrict__ fy, const double* __restrict__ fx,
+          double* __restrict__ z) {
+    const int v = blockIdx.x * NT + threadIdx.x;
+    if (v >= T) return;
+    const int o = perm[v];
+    z[v] = o < m ? fy[o] : fx[o - m];
+}
+
+// dy/dx (=|+=|-=) z[iperm[.]]
+__global__ void __launch_bounds__(NT)
+k_perm_out(int T, int m, const int* __restrict__ iperm, const double* __restrict__ z, double* __restrict__ dy,
+           double* __restrict__ dx, int mode) {
+    const int o = blockIdx.x * NT + threadIdx.x;
+    if (o >= T) return;
+    const double v = z[iperm[o]];
+    double* dst = o < m ? dy + o : dx + (o - m);
+    if (mode == 0) *dst = v;
+    else if (mode == 1) *dst = *dst + v;
+    else *dst = *dst - v;
+}
+
+// KKT residual (ldlt.c:389-398):
+//   ry_j = fy_j - ((A dx)_j - E_j dy_j)        row gather over CSR
+//   rx_i = fx_i - ((A' dy)_i + D_i dx_i)       column gather over CSC
+// plus max-abs partials of both (ldlt.c:401).
+__global__ void __launch_bounds__(NT)
+k_kkt_residual(int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
+               const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
+               const double* __restrict__ E, const double* __restrict__ D, const double* __restrict__ fy,
+               const double* __restrict__ fx, const double* __restrict__ dy, const double* __restrict__ dx,
+               double* __restrict__ ry, double* __restrict__ rx, double* __restrict__ part) {
+    __shared__ double sh[4];
+    double mx = 0.0;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
+        if (i < m) {
+            double s = 0.0;
+            for (int k = kAt[i]; k < kAt[i + 1]; k++) s += At[k] * dx[iAt[k]];
+            const double r = fy[i] - (s - E[i] * dy[i]);
+            ry[i] = r;
+            mx = fmax(mx, ref_abs(r));
+        } else {
+            const int j = i - m;
+            double s = 0.0;
+            for (int k = kA[j]; k < kA[j + 1]; k++) s += A[k] * dy[iA[k]];
+            const double r = fx[j] - (s + D[j] * dx[j]);
+            rx[j] = r;
+            mx = fmax(mx, ref_abs(r));
+        }
+    }
+    mx = block_max(mx, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = mx;
+}
+
+// -min|d| partials, so that the max-finisher yields -min|d| (negated on host)
+__global__ void __launch_bounds__(NT)
+k_min_abs_partial(const double* __restrict__ d, int T, double* __restrict__ part) {
+    __shared__ double sh[4];
+    double mn = HUGE_VAL;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < T; i += kRedBlocks * NT) mn = fmin(mn, ref_abs(d[i]));
+    const double r = block_max(-mn, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+__global__ void k_scale_scalar(double* e, double f) { e[0] *= f; }
+
+}  // namespace
+
+// ======================================================================
+KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream)
+    : m_(m), n_(n), T_(m + n), stream_(stream) {
+    std::vector<int> kat, iat;
+    std::vector<double> at;
+    csc_transpose(m, n, kA, iA, A, kat, iat, at);
+    plan_ = build_kkt_plan(m, n, kA, iA, kat.data(), iat.data());
+    const int nz = kA[n];
+    hipStream_t s = stream_;
+    dkA_.upload(kA, n + 1, s);
+    diA_.upload(iA, nz, s);
+    dA_.upload(A, nz, s);
+    dkAt_.upload(kat, s);
+    diAt_.upload(iat, s);
+    dAt_.upload(at, s);
+
+    dcol0_.upload(plan_.col0, s);
+    drowptr_.upload(plan_.rowptr, s);
+    drows_.upload(plan_.rows, s);
+    dperm_.upload(plan_.perm, s);
+    diperm_.upload(plan_.iperm, s);
+    doff_.upload(plan_.off, s);
+    damap_.upload(plan_.amap, s);
+    ddslot_.upload(plan_.dslot, s);
+    drelptr_.upload(plan_.relptr, s);
+    dfrow_pos_.upload(plan_.frow_pos, s);
+    dunit_sup_.upload(plan_.unit_sup, s);
+    dunit_tile_.upload(plan_.unit_tile, s);
+    dtask_ptr_.upload(plan_.task_ptr, s);
+    dtask_pair_.upload(plan_.task_pair, s);
+    dtask_i0_.upload(plan_.task_i0, s);
+    dtask_i1_.upload(plan_.task_i1, s);
+    dupd_src_.upload(plan_.upd_src, s);
+    dupd_r0_.upload(plan_.upd_r0, s);
+    dupd_r1_.upload(plan_.upd_r1, s);
+    drel_.upload(plan_.rel, s);
+    dlevel_sups_.upload(plan_.level_sups, s);
+    dfrow_ptr_.upload(plan_.frow_ptr, s);
+    dfrow_col_.upload(plan_.frow_col, s);
+
+    dLx_.alloc(plan_.lx_size > 0 ? plan_.lx_size : 1);
+    dDg_.alloc(T_ > 0 ? T_ : 1);
+    dLive_.alloc(T_ > 0 ? T_ : 1);
+    // flags: [0] ndep, [1] inconsistent, [2..2+T) node class sign per new index
+    dFlags_.alloc(2 + T_);
+    {
+        std::vector<int> fl(2 + T_, 0);
+        for (int v = 0; v < T_; v++) fl[2 + v] = plan_.dsign[v];
+        dFlags_.upload(fl, s);
+    }
+    dZ_.alloc(T_ > 0 ? T_ : 1);
+    dDy_.alloc(m > 0 ? m : 1);
+    dRy_.alloc(m > 0 ? m : 1);
+    dDx_.alloc(n > 0 ? n : 1);
+    dRx_.alloc(n > 0 ? n : 1);
+    dPart_.alloc(8 * kRedBlocks);
+    dScal_.alloc(16);
+    IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hScal_), 16 * sizeof(double), hipHostMallocDefault));
+    IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hFlags_), 4 * sizeof(int), hipHostMallocDefault));
+    IPO_HIP_CHECK(hipEventCreate(&ev0_));
+    IPO_HIP_CHECK(hipEventCreate(&ev1_));
+    IPO_HIP_CHECK(hipEventCreate(&ev2_));
+    IPO_HIP_CHECK(hipEventCreate(&ev3_));
+    IPO_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+KktDevice::~KktDevice() {
+    if (hScal_) (void)hipHostFree(hScal_);
+    if (hFlags_) (void)hipHostFree(hFlags_);
+    if (ev0_) (void)hipEventDestroy(ev0_);
+    if (ev1_) (void)hipEventDestroy(ev1_);
+    if (ev2_) (void)hipEventDestroy(ev2_);
+    if (ev3_) (void)hipEventDestroy(ev3_);
+    for (hipEvent_t e : kev_) (void)hipEventDestroy(e);
+}
+
+static PlanView make_view(const KktPlan&, const DevBuf<int>& col0, const DevBuf<int>& rowptr, const DevBuf<int>& rows,
+                          const DevBuf<int64_t>& off, const DevBuf<int>& us, const DevBuf<int>& ut,
+                          const DevBuf<int>& tp, const DevBuf<int>& tq, const DevBuf<int>& t0, const DevBuf<int>& t1,
+                          const DevBuf<int>& src, const DevBuf<int>& r0, const DevBuf<int>& r1,
+                          const DevBuf<int64_t>& relptr, const DevBuf<int>& rel, const DevBuf<double>& lx,
+                          const DevBuf<double>& dg, const DevBuf<int>& live, const DevBuf<int>& flags) {
+    PlanView v;
+    v.col0 = col0.get(); v.rowptr = rowptr.get(); v.rows = rows.get(); v.off = off.get();
+    v.unit_sup = us.get(); v.unit_tile = ut.get(); v.task_ptr = tp.get(); v.task_pair = tq.get();
+    v.task_i0 = t0.get(); v.task_i1 = t1.get(); v.upd_src = src.get(); v.upd_r0 = r0.get(); v.upd_r1 = r1.get();
+    v.relptr = relptr.get(); v.rel = rel.get(); v.Lx = lx.get(); v.dg = dg.get(); v.live = live.get();
+    v.flags = flags.get();
+    v.sign = flags.get() + 2;
+    return v;
+}
+
+#define IPO_VIEW() make_view(plan_, dcol0_, drowptr_, drows_, doff_, dunit_sup_, dunit_tile_, dtask_ptr_, \
+                             dtask_pair_, dtask_i0_, dtask_i1_, dupd_src_, dupd_r0_, dupd_r1_, drelptr_, drel_, \
+                             dLx_, dDg_, dLive_, dFlags_)
+
+void KktDevice::factor(const double* dE, const double* dD) {
+    hipStream_t s = stream_;
+    if (timing_) IPO_HIP_CHECK(hipEventRecord(ev0_, s));
+    const PlanView pv = IPO_VIEW();
+    const int nz = static_cast<int>(plan_.amap.size());
+    IPO_HIP_CHECK(hipMemsetAsync(dLx_.get(), 0, dLx_.bytes(), s));
+    IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get(), 0, 2 * sizeof(int), s));
+    if (nz > 0) hipLaunchKernelGGL(k_assemble_A, dim3(ceil_div(nz, NT)), dim3(NT), 0, s, nz, dA_.get(), damap_.get(), dLx_.get());
+    hipLaunchKernelGGL(k_assemble_diag, dim3(ceil_div(T_, NT)), dim3(NT), 0, s, T_, m_, dperm_.get(), dE, dD, epsdiag_,
+                       ddslot_.get(), dLx_.get(), dLive_.get());
+    if (timing_ && kev_.size() < static_cast<size_t>(4 * plan_.nlevels)) {
+        for (hipEvent_t e : kev_) (void)hipEventDestroy(e);
+        kev_.assign(4 * plan_.nlevels, nullptr);
+        for (hipEvent_t& e : kev_) IPO_HIP_CHECK(hipEventCreate(&e));
+    }
+    std::vector<char> upd_used(timing_ ? plan_.nlevels : 0, 0);
+    for (int l = 0; l < plan_.nlevels; l++) {
+        const int u0 = plan_.unit_level_ptr[l], u1 = plan_.unit_level_ptr[l + 1];
+        if (u1 <= u0) continue;
+        if (l > 0) {
+            if (timing_) { IPO_HIP_CHECK(hipEventRecord(kev_[4 * l], s)); upd_used[l] = 1; }
+            hipLaunchKernelGGL(k_update, dim3(u1 - u0), dim3(NT), 0, s, pv, u0);
+            if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 1], s));
+        }
+        if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 2], s));
+        hipLaunchKernelGGL(k_factor, dim3(u1 - u0), dim3(NT), 0, s, pv, u0);
+        if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 3], s));
+    }
+    IPO_HIP_CHECK(hipGetLastError());
+    // min |d| over the factor (ldlt.c:293-306) and the dependent-pivot count
+    hipLaunchKernelGGL(k_min_abs_partial, dim3(kRedBlocks), dim3(NT), 0, s, dDg_.get(), T_, dPart_.get());
+    hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), 1, 1u, dScal_.get());
+    IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+    IPO_HIP_CHECK(hipMemcpyAsync(hFlags_, dFlags_.get(), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
+    IPO_HIP_CHECK(hipStreamSynchronize(s));
+    if (timing_) {
+        float ms = 0;
+        IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
+        tm_.factor_ms += ms;
+        for (int l = 0; l < plan_.nlevels; l++) {
+            if (plan_.unit_level_ptr[l + 1] <= plan_.unit_level_ptr[l]) continue;
+            if (upd_used[l]) {
+                IPO_HIP_CHECK(hipEventElapsedTime(&ms, kev_[4 * l], kev_[4 * l + 1]));
+                tm_.update_ms += ms;
+                tm_.update_launches++;
+            }
+            IPO_HIP_CHECK(hipEventElapsedTime(&ms, kev_[4 * l + 2], kev_[4 * l + 3]));
+            tm_.panel_ms += ms;
+            tm_.panel_launches++;
+        }
+    }
+    tm_.factors++;
+    ndep_ = hFlags_[0];
+    if (-hScal_[0] < 1.0e-14) epsdiag_ *= 10;
+}
+
+void KktDevice::rawsolve(double* dz) {
+    hipStream_t s = stream_;
+    const PlanView pv = IPO_VIEW();
+    double* epsp = dScal_.get() + 4;
+    if (ndep_ > 0) {
+        // eps = epssol * max|z[0..n)| (ldlt.c:446: first n entries of the permuted vector)
+        RedJobs j{};
+        j.nj = 1; j.a[0] = dz; j.b[0] = nullptr; j.len[0] = n_; j.op[0] = 1;
+        launch_reduce(j, dPart_.get(), epsp, s);
+        hipLaunchKernelGGL(k_scale_scalar, dim3(1), dim3(1), 0, s, epsp, 1.0e-6);
+    } else {
+        IPO_HIP_CHECK(hipMemsetAsync(epsp, 0, sizeof(double), s));
+    }
+    if (timing_) IPO_HIP_CHECK(hipEventRecord(ev2_, s));
+    for (int l = 0; l < plan_.nlevels; l++) {
+        const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
+        hipLaunchKernelGGL(k_forward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dfrow_ptr_.get(),
+                           dfrow_col_.get(), dfrow_pos_.get(), dz, epsp);
+    }
+    for (int l = plan_.nlevels - 1; l >= 0; l--) {
+        const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
+        hipLaunchKernelGGL(k_backward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dz, epsp);
+    }
+    IPO_HIP_CHECK(hipGetLastError());
+    if (timing_) {
+        IPO_HIP_CHECK(hipEventRecord(ev3_, s));
+        IPO_HIP_CHECK(hipEventSynchronize(ev3_));
+        float ms = 0;
+        IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev2_, ev3_));
+        tm_.sweep_ms += ms;
+    }
+    tm_.rawsolves++;
+}
+
+int KktDevice::solve(const double* dE, const double* dD, double* dfy, double* dfx) {
+    hipStream_t s = stream_;
+    if (timing_) IPO_HIP_CHECK(hipEventRecord(ev0_, s));
+    const int m = m_, n = n_, T = T_;
+    IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get() + 1, 0, sizeof(int), s));
+    // maxbc = MAX(maxv(fx), maxv(fy)) + 1   (ldlt.c:367)
+    {
+        RedJobs j{};
+        j.nj = 2;
+        j.a[0] = dfx; j.b[0] = nullptr; j.len[0] = n; j.op[0] = 1;
+        j.a[1] = dfy; j.b[1] = nullptr; j.len[1] = m; j.op[1] = 1;
+        launch_reduce(j, dPart_.get(), dScal_.get(), s);
+        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+    IPO_HIP_CHECK(hipStreamSynchronize(s));
+    const double maxbc = (hScal_[0] > hScal_[1] ? hScal_[0] : hScal_[1]) + 1;
+
+    double* z = dZ_.get();
+    double* dy = dDy_.get();
+    double* dx = dDx_.get();
+    double* ry = dRy_.get();
+    double* rx = dRx_.get();
+    int pass = 0;
+    double rs = HUGE_VAL, rs_old;
+    do {
+        hipLaunchKernelGGL(k_perm_in, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, dperm_.get(),
+                           pass == 0 ? dfy : ry, pass == 0 ? dfx : rx, z);
+        rawsolve(z);
+        hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), z, dy, dx,
+                           pass == 0 ? 0 : 1);
+        hipLaunchKernelGGL(k_kkt_residual, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dkAt_.get(), diAt_.get(), dAt_.get(),
+                           dkA_.get(), diA_.get(), dA_.get(), dE, dD, dfy, dfx, dy, dx, ry, rx, dPart_.get());
+        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), 1, 1u, dScal_.get());
+        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        rs_old = rs;
+        rs = hScal_[0];
+        pass++;
+    } while (rs > 1.0e-10 * maxbc && rs < rs_old / 2);
+    if (rs > rs_old && pass > 1)
+        hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), z, dy, dx, 2);
+    IPO_HIP_CHECK(hipMemcpyAsync(dfy, dy, sizeof(double) * m, hipMemcpyDeviceToDevice, s));
+    IPO_HIP_CHECK(hipMemcpyAsync(dfx, dx, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 1, dFlags_.get() + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
+    IPO_HIP_CHECK(hipStreamSynchronize(s));
+    if (timing_) { float ms = 0; IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_)); tm_.solve_ms += ms; }
+    tm_.solves++;
+    last_passes_ = pass;
+    return hFlags_[1] ? 0 : 1;
+}
+
+void KktDevice::download_factor(double* lx, double* d) const {
+    if (lx) dLx_.download(lx, plan_.lx_size, stream_);
+    if (d) dDg_.download(d, T_, stream_);
+    IPO_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+}  // namespace ipo

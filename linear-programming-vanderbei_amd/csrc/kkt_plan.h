@@ -1,0 +1,101 @@
+// kkt_plan.h -- host-side symbolic analysis of the quasi-definite KKT system
+//
+//        K = [ -E   A ]      E = w/y (m rows, "y-nodes")
+//            [  A'  D ]      D = z/x (n cols, "x-nodes")
+//
+// that ipo factors every interior-point iteration (src/ipo/ldlt.c:164-309,
+// called from hsd.c:218 / intpt.c:197).  Symbolic work stays on the host,
+// as the reference does it once per process (ldlt.c:211-223):
+//
+//   * ordering   -- the reference's tiered minimum-degree ordering
+//                   (ldlt.c:638-1262), re-implemented here so the GPU
+//                   factor has exactly the reference's fill pattern;
+//   * supernodes -- consecutive columns with nested structure, split into
+//                   panels of at most kPanelCols columns;
+//   * schedule   -- supernodal elimination tree levels, per-target update
+//                   lists with relative row positions, assembly maps from
+//                   A's nonzeros to panel slots.
+//
+// Node numbering before permutation: y-nodes 0..m-1, x-nodes m..m+n-1.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace ipo {
+
+constexpr int kPanelCols = 64;     // max columns per supernode panel
+constexpr int kTileRows = 64;      // rows per factor work unit
+
+struct KktOrdering {
+    int m = 0, n = 0, T = 0;
+    std::vector<int> perm, iperm;  // perm[new] = old
+    std::vector<int> Lp, Li;       // strict-lower pattern of L, new indices, sorted
+    int pdf = 0;                   // 1 = y-nodes tier 0 ("primal"), 2 = x-nodes tier 0
+    int denwin = 0;                // first column of the reference's dense window
+    double narth = 0.0;            // reference op count (ldlt.c:1243-1248)
+};
+
+// ldlt.c:638-858 (inv_sym) + ldlt.c:860-1262 (lltsym), method _MD, dense = 3
+KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
+                                    const int* kAt, const int* iAt);
+
+struct KktPlan {
+    int m = 0, n = 0, T = 0;
+    std::vector<int> perm, iperm;
+
+    // supernodal panels: supernode s owns columns [col0[s], col0[s+1]),
+    // its below-block rows are rows[rowptr[s] .. rowptr[s+1]) (sorted, new
+    // indices).  Panel = h x nc column-major, ld = h = nc + |R_s|; rows of
+    // the panel are the nc block rows followed by R_s.
+    int nsup = 0;
+    std::vector<int> col0;          // [nsup+1]
+    std::vector<int> rowptr;        // [nsup+1]
+    std::vector<int> rows;          // concatenated R_s
+    std::vector<int64_t> off;       // [nsup+1] offset of panel s in Lx
+    std::vector<int> parent;        // supernodal etree
+    std::vector<int> sup_of;        // [T] column -> supernode
+    std::vector<int> level;         // [nsup]
+    int nlevels = 0;
+    std::vector<int> level_ptr;     // [nlevels+1]
+    std::vector<int> level_sups;    // supernodes, grouped by level
+
+    // left-looking update pairs, grouped by target supernode:
+    //   for target s, pairs upd_ptr[s]..upd_ptr[s+1]; source d = upd_src[p];
+    //   rows R_d[upd_r0[p] .. |R_d|) land in s, the first upd_r1[p]-upd_r0[p]
+    //   of them inside s's columns; their panel rows are rel[relptr[p] + i].
+    std::vector<int> upd_ptr, upd_src, upd_r0, upd_r1;
+    std::vector<int64_t> relptr;
+    std::vector<int> rel;
+
+    // assembly: A nonzero k (CSC order) -> slot in Lx; node v (new) -> diagonal slot
+    std::vector<int64_t> amap;
+    std::vector<int64_t> dslot;     // [T]
+    std::vector<int> dsign;         // [T] -1 for y-nodes, +1 for x-nodes (new index)
+    int64_t lx_size = 0;
+
+    // GPU work decomposition (filled by build_kkt_plan)
+    //  factor units: one per (supernode, 64-row tile of its panel), grouped
+    //  by level; unit u gathers tasks task_ptr[u]..task_ptr[u+1], each a
+    //  slice [task_i0, task_i1) of one update pair's rows.
+    std::vector<int> unit_level_ptr;   // [nlevels+1]
+    std::vector<int> unit_sup, unit_tile;
+    std::vector<int> task_ptr, task_pair, task_i0, task_i1;
+    //  forward-solve row lists: for row v, the L entries (v, col) whose column
+    //  lies in another supernode: Lx slot and column.
+    std::vector<int> frow_ptr;         // [T+1]
+    std::vector<int> frow_col;
+    std::vector<int64_t> frow_pos;
+
+    // reference statistics
+    int64_t lnz = 0;                // nnz strict lower L (reference pattern)
+    double narth = 0.0;
+    int pdf = 0, denwin = 0;
+    int max_h = 0, max_nc = 0;
+    double flops_factor = 0.0;      // sum over updates of 2*ra*rc*nc (approx)
+    double flops_update = 0.0;      // exact flops of k_update per factorisation (2 per multiply-add, +1 d-scale)
+    double bytes_update = 0.0;      // algorithmic bytes of k_update per factorisation
+};
+
+KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt);
+
+}  // namespace ipo

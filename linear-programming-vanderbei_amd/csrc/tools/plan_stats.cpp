@@ -1,0 +1,40 @@
+// plan_stats: print the symbolic plan of an MPS problem (developer tool).
+#include <chrono>
+#include <cstdio>
+#include <string>
+#include "../kkt_plan.h"
+#include "../lp_io.h"
+
+int main(int argc, char** argv) {
+    if (argc < 2) { std::fprintf(stderr, "usage: plan_stats file.mps\n"); return 1; }
+    ipo::MpsProblem p; std::string err;
+    if (ipo::read_mps(argv[1], p, &err)) { std::fprintf(stderr, "read error: %s\n", err.c_str()); return 1; }
+    ipo::SolverForm s;
+    if (ipo::to_solver_form(p, s)) { std::printf("free variable -> status 3\n"); return 0; }
+    std::vector<int> kat, iat; std::vector<double> at;
+    ipo::csc_transpose(s.m, s.n, s.kA.data(), s.iA.data(), s.A.data(), kat, iat, at);
+    auto t0 = std::chrono::steady_clock::now();
+    ipo::KktPlan P = ipo::build_kkt_plan(s.m, s.n, s.kA.data(), s.iA.data(), kat.data(), iat.data());
+    double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("m=%d n=%d nz=%d T=%d pdf=%d lnz=%lld narth=%.4e denwin=%d\n", s.m, s.n, s.nz, P.T, P.pdf,
+                (long long)P.lnz, P.narth, P.denwin);
+    std::printf("nsup=%d nlevels=%d lx=%lld (%.1f MB) max_h=%d max_nc=%d pairs=%zu rel=%zu flops=%.4e symbolic=%.3fs\n",
+                P.nsup, P.nlevels, (long long)P.lx_size, P.lx_size * 8e-6, P.max_h, P.max_nc, P.upd_src.size(),
+                P.rel.size(), P.flops_factor, dt);
+    if (argc > 2) {
+        for (int l = 0; l < P.nlevels; l++) {
+            int cnt = P.level_ptr[l + 1] - P.level_ptr[l];
+            long work = 0; int maxh = 0;
+            for (int q = P.level_ptr[l]; q < P.level_ptr[l + 1]; q++) {
+                int s2 = P.level_sups[q]; int h = P.col0[s2+1]-P.col0[s2] + P.rowptr[s2+1]-P.rowptr[s2];
+                if (h > maxh) maxh = h; work += h;
+            }
+            std::printf("L%d: sups=%d rows=%ld maxh=%d\n", l, cnt, work, maxh);
+        }
+    }
+    // print perm hash for comparison
+    unsigned long long hsh = 1469598103934665603ull;
+    for (int v : P.perm) { hsh ^= (unsigned)v; hsh *= 1099511628211ull; }
+    std::printf("perm_hash=%016llx\n", hsh);
+    return 0;
+}

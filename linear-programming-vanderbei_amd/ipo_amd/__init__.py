@@ -1,0 +1,368 @@
+"""ipo_amd -- Python host mirror of the ipo-hip C ABI (include/ipo_hip.h).
+
+The product is the C-ABI shared library ``lib/libipo_hip.so`` (HIP kernels for
+gfx950 + native host code).  This module is a thin ctypes binding used by the
+tests and ``bench.py``; it mirrors the reference's operator interface:
+
+* :func:`solver`          -- ``solver()`` of src/common/solve.c:24-26 (hsd.c / intpt.c)
+* :class:`Ldlt`           -- ``ldltfac()`` / ``forwardbackward()`` of src/ipo/ldlt.h
+* :func:`run_mps`         -- the ``ipo file.mps`` driver (src/common/main.c:16-58)
+
+There is no CPU fallback: if the library is missing or no GPU is present the
+calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import tempfile
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libipo_hip.so")
+
+STATUS_TEXT = {
+    0: "optimal solution", 1: "primal unbounded", 2: "primal infeasible", 3: "dual unbounded",
+    4: "dual infeasible", 5: "iteration limit", 6: "infinite lower bounds - not implemented",
+    7: "suboptimal solution",
+}
+METHODS = {"hsd": 0, "intpt": 1}
+
+
+class IpoHipError(RuntimeError):
+    pass
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("iters", C.c_int), ("status", C.c_int),
+        ("t_setup_s", C.c_double), ("t_solve_s", C.c_double),
+        ("factor_ms", C.c_double), ("solve_ms", C.c_double),
+        ("factors", C.c_long), ("solves", C.c_long), ("rawsolves", C.c_long), ("refine_passes", C.c_long),
+        ("final_mu", C.c_double), ("final_pobj", C.c_double), ("final_dobj", C.c_double),
+        ("final_pinf", C.c_double), ("final_dinf", C.c_double),
+        ("lnz", C.c_long), ("narth", C.c_double), ("nsup", C.c_int), ("nlevels", C.c_int),
+        ("flops_factor", C.c_double), ("lx_bytes", C.c_double),
+        ("update_ms", C.c_double), ("panel_ms", C.c_double), ("sweep_ms", C.c_double),
+        ("update_launches", C.c_long), ("panel_launches", C.c_long),
+        ("flops_update", C.c_double), ("bytes_update", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+_libc = None
+
+EXPORTED = [
+    "solver", "ldltfac", "forwardbackward", "inv_clo",
+    "ipo_hip_solve", "ipo_hip_run_mps", "ipo_hip_mps_dims", "ipo_hip_mps_load",
+    "ipo_hip_kkt_create", "ipo_hip_kkt_destroy", "ipo_hip_kkt_factor", "ipo_hip_kkt_solve",
+    "ipo_hip_kkt_info", "ipo_hip_kkt_perm", "ipo_hip_symbolic",
+    "ipo_hip_device_count", "ipo_hip_last_error", "ipo_hip_version",
+    "ipo_hip_ctx_create", "ipo_hip_ctx_run", "ipo_hip_ctx_download", "ipo_hip_ctx_destroy",
+    "ipo_hip_ctx_setup_seconds",
+]
+
+_P = C.c_void_p
+_I = C.c_int
+_D = C.c_double
+
+
+def lib() -> C.CDLL:
+    """Load libipo_hip.so (raises if it was not built)."""
+    global _lib, _libc
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise IpoHipError(f"{LIB_PATH} missing: run `make -C linear-programming-vanderbei_amd` "
+                          "(or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    L.solver.argtypes = [_I, _I, _I, _P, _P, _P, _P, _P, _D, _P, _P, _P, _P]
+    L.solver.restype = _I
+    L.ldltfac.argtypes = [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I]
+    L.ldltfac.restype = None
+    L.forwardbackward.argtypes = [_P, _P, _P, _P]
+    L.forwardbackward.restype = None
+    L.inv_clo.argtypes = []
+    L.inv_clo.restype = None
+    L.ipo_hip_solve.argtypes = [_I, _I, _I, _I, _P, _P, _P, _P, _P, _D, _P, _P, _P, _P, _P, _I, _I, C.POINTER(Stats)]
+    L.ipo_hip_solve.restype = _I
+    L.ipo_hip_run_mps.argtypes = [C.c_char_p, _I, _P, _I, C.POINTER(Stats)]
+    L.ipo_hip_run_mps.restype = _I
+    L.ipo_hip_mps_dims.argtypes = [C.c_char_p] + [C.POINTER(_I)] * 6
+    L.ipo_hip_mps_dims.restype = _I
+    L.ipo_hip_mps_load.argtypes = [C.c_char_p, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), _P, _P, _P, _P, _P,
+                                   C.POINTER(_D)]
+    L.ipo_hip_mps_load.restype = _I
+    L.ipo_hip_kkt_create.argtypes = [_I, _I, _P, _P, _P]
+    L.ipo_hip_kkt_create.restype = _P
+    L.ipo_hip_kkt_destroy.argtypes = [_P]
+    L.ipo_hip_kkt_destroy.restype = None
+    L.ipo_hip_kkt_factor.argtypes = [_P, _P, _P]
+    L.ipo_hip_kkt_factor.restype = _I
+    L.ipo_hip_kkt_solve.argtypes = [_P, _P, _P, _P, _P]
+    L.ipo_hip_kkt_solve.restype = _I
+    L.ipo_hip_kkt_info.argtypes = [_P, C.POINTER(C.c_long), C.POINTER(_D), C.POINTER(_I), C.POINTER(_I),
+                                   C.POINTER(_I), C.POINTER(_I), C.POINTER(_D), C.POINTER(_I), C.POINTER(_I)]
+    L.ipo_hip_kkt_info.restype = _I
+    L.ipo_hip_kkt_perm.argtypes = [_P, _P]
+    L.ipo_hip_kkt_perm.restype = _I
+    L.ipo_hip_symbolic.argtypes = [_I, _I, _P, _P, _P, C.POINTER(C.c_long), C.POINTER(_D), C.POINTER(_I),
+                                   C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]
+    L.ipo_hip_symbolic.restype = _I
+    L.ipo_hip_ctx_create.argtypes = [_I, _I, _P, _P, _P, _P, _P, _D]
+    L.ipo_hip_ctx_create.restype = _P
+    L.ipo_hip_ctx_run.argtypes = [_P, _I, _I, _P, _I, C.POINTER(Stats)]
+    L.ipo_hip_ctx_run.restype = _I
+    L.ipo_hip_ctx_download.argtypes = [_P, _P, _P, _P, _P]
+    L.ipo_hip_ctx_download.restype = None
+    L.ipo_hip_ctx_destroy.argtypes = [_P]
+    L.ipo_hip_ctx_destroy.restype = None
+    L.ipo_hip_ctx_setup_seconds.argtypes = [_P]
+    L.ipo_hip_ctx_setup_seconds.restype = _D
+    L.ipo_hip_device_count.restype = _I
+    L.ipo_hip_last_error.restype = C.c_char_p
+    L.ipo_hip_version.restype = C.c_char_p
+    _lib = L
+    _libc = C.CDLL(None)
+    _libc.fopen.restype = _P
+    _libc.fopen.argtypes = [C.c_char_p, C.c_char_p]
+    _libc.fclose.argtypes = [_P]
+    _libc.fflush.argtypes = [_P]
+    return L
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def last_error() -> str:
+    return lib().ipo_hip_last_error().decode()
+
+
+def device_count() -> int:
+    return lib().ipo_hip_device_count()
+
+
+def require_gpu() -> None:
+    if device_count() < 1:
+        raise IpoHipError("no HIP device visible: ipo-hip has no CPU fallback")
+
+
+# ----------------------------------------------------------------- MPS front end
+@dataclass
+class SolverForm:
+    """Problem in the form solver() takes: max c'x + f, Ax <= b, x >= 0 (A CSC)."""
+    m: int
+    n: int
+    kA: np.ndarray
+    iA: np.ndarray
+    A: np.ndarray
+    b: np.ndarray
+    c: np.ndarray
+    f: float
+
+    @property
+    def nz(self) -> int:
+        return int(self.kA[-1])
+
+    def transpose(self):
+        """CSR of A (= CSC of A'), stable like linalg.c:75-103."""
+        counts = np.bincount(self.iA, minlength=self.m)
+        kAt = np.zeros(self.m + 1, np.int32)
+        np.cumsum(counts, out=kAt[1:])
+        cols = np.repeat(np.arange(self.n, dtype=np.int32), np.diff(self.kA))
+        order = np.argsort(self.iA, kind="stable")
+        return kAt, cols[order].astype(np.int32), self.A[order].copy()
+
+
+def mps_dims(path: str):
+    """(m0, n0, nz0, m, n, nz, status) of an MPS file (solve.c:62 and hsd.c:117 lines)."""
+    v = [C.c_int(0) for _ in range(6)]
+    st = lib().ipo_hip_mps_dims(path.encode(), *[C.byref(x) for x in v])
+    return tuple(x.value for x in v) + (st,)
+
+
+def load_mps(path: str) -> SolverForm:
+    """Read + normalise an MPS file with the native front end (lp_io.cpp)."""
+    L = lib()
+    m, n, nz = C.c_int(0), C.c_int(0), C.c_int(0)
+    st = L.ipo_hip_mps_load(path.encode(), C.byref(m), C.byref(n), C.byref(nz), None, None, None, None, None, None)
+    if st:
+        raise IpoHipError(f"mps load {path}: status {st} {last_error()}")
+    kA = np.zeros(n.value + 1, np.int32)
+    iA = np.zeros(nz.value, np.int32)
+    A = np.zeros(nz.value, np.float64)
+    b = np.zeros(m.value, np.float64)
+    c = np.zeros(n.value, np.float64)
+    f = C.c_double(0.0)
+    L.ipo_hip_mps_load(path.encode(), C.byref(m), C.byref(n), C.byref(nz), _ptr(kA), _ptr(iA), _ptr(A), _ptr(b),
+                       _ptr(c), C.byref(f))
+    return SolverForm(m.value, n.value, kA, iA, A, b, c, f.value)
+
+
+def _capture(fn):
+    """Run fn(FILE*) and return (result, text written)."""
+    lib()
+    fd, path = tempfile.mkstemp(prefix="ipo_hip_", suffix=".txt")
+    os.close(fd)
+    fp = _libc.fopen(path.encode(), b"w")
+    try:
+        r = fn(fp)
+    finally:
+        _libc.fflush(fp)
+        _libc.fclose(fp)
+    with open(path) as fh:
+        text = fh.read()
+    os.unlink(path)
+    return r, text
+
+
+def run_mps(path: str, method: str = "hsd", timing: bool = False):
+    """Equivalent of `ipo path` (main.c) on the GPU.  Returns (status, stdout text, stats dict)."""
+    require_gpu()
+    st = Stats()
+    status, text = _capture(lambda fp: lib().ipo_hip_run_mps(path.encode(), METHODS[method], fp, int(timing),
+                                                            C.byref(st)))
+    return status, text, st.as_dict()
+
+
+def solver(p: SolverForm, method: str = "hsd", trace: bool = False, max_iter: int = 200, timing: bool = False):
+    """solver() on host arrays.  Returns dict(status, x, y, w, z, stats, trace)."""
+    require_gpu()
+    x = np.zeros(p.n, np.float64)
+    z = np.zeros(p.n, np.float64)
+    y = np.zeros(p.m, np.float64)
+    w = np.zeros(p.m, np.float64)
+    st = Stats()
+    kA = np.ascontiguousarray(p.kA, np.int32)
+    iA = np.ascontiguousarray(p.iA, np.int32)
+    A = np.ascontiguousarray(p.A, np.float64)
+    b = np.ascontiguousarray(p.b, np.float64)
+    c = np.ascontiguousarray(p.c, np.float64)
+
+    def call(fp):
+        return lib().ipo_hip_solve(METHODS[method], p.m, p.n, p.nz, _ptr(iA), _ptr(kA), _ptr(A), _ptr(b), _ptr(c),
+                                   float(p.f), _ptr(x), _ptr(y), _ptr(w), _ptr(z), fp, max_iter, int(timing),
+                                   C.byref(st))
+    if trace:
+        status, text = _capture(call)
+    else:
+        status, text = call(None), ""
+    return {"status": status, "x": x, "y": y, "w": w, "z": z, "stats": st.as_dict(), "trace": text}
+
+
+# ----------------------------------------------------------------- KKT factor
+class KktFactor:
+    """Device LDL' of K = [-E A; A' D] for the solver's A (m x n CSC)."""
+
+    def __init__(self, m, n, kA, iA, A):
+        require_gpu()
+        self.m, self.n = m, n
+        self._keep = [np.ascontiguousarray(kA, np.int32), np.ascontiguousarray(iA, np.int32),
+                      np.ascontiguousarray(A, np.float64)]
+        self.h = lib().ipo_hip_kkt_create(m, n, *[_ptr(a) for a in self._keep])
+        if not self.h:
+            raise IpoHipError("kkt create: " + last_error())
+
+    def factor(self, E, D):
+        E = np.ascontiguousarray(E, np.float64)
+        D = np.ascontiguousarray(D, np.float64)
+        if lib().ipo_hip_kkt_factor(self.h, _ptr(E), _ptr(D)) != 0:
+            raise IpoHipError("kkt factor: " + last_error())
+
+    def solve(self, E, D, fy, fx):
+        E = np.ascontiguousarray(E, np.float64)
+        D = np.ascontiguousarray(D, np.float64)
+        fy = np.array(fy, np.float64, copy=True)
+        fx = np.array(fx, np.float64, copy=True)
+        ok = lib().ipo_hip_kkt_solve(self.h, _ptr(E), _ptr(D), _ptr(fy), _ptr(fx))
+        if ok < 0:
+            raise IpoHipError("kkt solve: " + last_error())
+        return fy, fx, ok
+
+    def info(self) -> dict:
+        lnz, narth, eps = C.c_long(), C.c_double(), C.c_double()
+        nsup, nlev, denwin, pdf, ndep, passes = (C.c_int() for _ in range(6))
+        lib().ipo_hip_kkt_info(self.h, C.byref(lnz), C.byref(narth), C.byref(nsup), C.byref(nlev), C.byref(denwin),
+                               C.byref(pdf), C.byref(eps), C.byref(ndep), C.byref(passes))
+        return dict(lnz=lnz.value, narth=narth.value, nsup=nsup.value, nlevels=nlev.value, denwin=denwin.value,
+                    pdf=pdf.value, epsdiag=eps.value, ndep=ndep.value, passes=passes.value)
+
+    def perm(self) -> np.ndarray:
+        p = np.zeros(self.m + self.n, np.int32)
+        lib().ipo_hip_kkt_perm(self.h, _ptr(p))
+        return p
+
+    def close(self):
+        if self.h:
+            lib().ipo_hip_kkt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """Device-resident problem (ipo_hip_ctx): setup once, run() many times."""
+
+    def __init__(self, p: SolverForm):
+        require_gpu()
+        self.p = p
+        self._keep = [np.ascontiguousarray(p.kA, np.int32), np.ascontiguousarray(p.iA, np.int32),
+                      np.ascontiguousarray(p.A, np.float64), np.ascontiguousarray(p.b, np.float64),
+                      np.ascontiguousarray(p.c, np.float64)]
+        self.h = lib().ipo_hip_ctx_create(p.m, p.n, *[_ptr(a) for a in self._keep], float(p.f))
+        if not self.h:
+            raise IpoHipError("ctx create: " + last_error())
+        self.setup_seconds = lib().ipo_hip_ctx_setup_seconds(self.h)
+
+    def run(self, method="hsd", max_iter=200, trace=False, timing=False):
+        st = Stats()
+
+        def call(fp):
+            return lib().ipo_hip_ctx_run(self.h, METHODS[method], max_iter, fp, int(timing), C.byref(st))
+        if trace:
+            status, text = _capture(call)
+        else:
+            status, text = call(None), ""
+        return status, st.as_dict(), text
+
+    def solution(self):
+        x = np.zeros(self.p.n); z = np.zeros(self.p.n); y = np.zeros(self.p.m); w = np.zeros(self.p.m)
+        lib().ipo_hip_ctx_download(self.h, _ptr(x), _ptr(y), _ptr(w), _ptr(z))
+        return x, y, w, z
+
+    def close(self):
+        if self.h:
+            lib().ipo_hip_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def symbolic(m, n, kA, iA) -> dict:
+    """Host-only symbolic analysis (reference ordering); no GPU needed."""
+    kA = np.ascontiguousarray(kA, np.int32)
+    iA = np.ascontiguousarray(iA, np.int32)
+    perm = np.zeros(m + n, np.int32)
+    lnz, narth = C.c_long(), C.c_double()
+    denwin, pdf, nsup, nlev = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    rc = lib().ipo_hip_symbolic(m, n, _ptr(kA), _ptr(iA), _ptr(perm), C.byref(lnz), C.byref(narth), C.byref(denwin),
+                                C.byref(pdf), C.byref(nsup), C.byref(nlev))
+    if rc:
+        raise IpoHipError("symbolic: " + last_error())
+    return dict(perm=perm, lnz=lnz.value, narth=narth.value, denwin=denwin.value, pdf=pdf.value, nsup=nsup.value,
+                nlevels=nlev.value)

@@ -1,0 +1,111 @@
+"""Test-side access to the CPU ORACLE (oracle/, test infrastructure only).
+
+Builds oracle/ with its Makefile on first use and exposes the CLI (full
+`ipo` stdout) and the KKT LDL' pieces through ctypes.  Never imported by
+the product (linear-programming-vanderbei_amd/)."""
+import ctypes as C
+import os
+import subprocess
+import threading
+
+import numpy as np
+
+from conftest import REPO
+
+ORACLE_DIR = os.path.join(REPO, "oracle")
+BUILD = os.path.join(ORACLE_DIR, "build")
+_lock = threading.Lock()
+_lib = None
+
+
+def build():
+    with _lock:
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def cli_path():
+    exe = os.path.join(BUILD, "ipo_oracle")
+    if not os.path.exists(exe):
+        build()
+    return exe
+
+
+def run_cli(mps: str, method: str = "hsd", timeout: float = 3600) -> str:
+    out = subprocess.run([cli_path(), mps, method], capture_output=True, text=True, timeout=timeout)
+    return out.stdout
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        so = os.path.join(BUILD, "liborc.so")
+        if not os.path.exists(so):
+            build()
+        L = C.CDLL(so)
+        P, I, D = C.c_void_p, C.c_int, C.c_double
+        L.orc_kkt_create.restype = P
+        L.orc_kkt_create.argtypes = [I, I, P, P, P, P, P, P]
+        L.orc_kkt_destroy.argtypes = [P]
+        L.orc_kkt_factor.argtypes = [P, P, P]
+        L.orc_kkt_solve.argtypes = [P, P, P, P, P]
+        L.orc_kkt_solve.restype = I
+        L.orc_kkt_lnz.restype = C.c_long
+        L.orc_kkt_lnz.argtypes = [P]
+        L.orc_kkt_narth.restype = D
+        L.orc_kkt_narth.argtypes = [P]
+        for f in ("orc_kkt_denwin", "orc_kkt_pdf", "orc_kkt_dim", "orc_kkt_ndep", "orc_kkt_last_passes"):
+            getattr(L, f).argtypes = [P]
+            getattr(L, f).restype = I
+        L.orc_kkt_epsdiag.restype = D
+        L.orc_kkt_epsdiag.argtypes = [P]
+        L.orc_kkt_perm.argtypes = [P, P]
+        L.orc_kkt_diag.argtypes = [P, P]
+        _lib = L
+    return _lib
+
+
+class OracleKkt:
+    """orc_kkt: the reference's tiered-MD ordering + left-looking LDL'."""
+
+    def __init__(self, form):
+        L = lib()
+        self.m, self.n = form.m, form.n
+        kAt, iAt, At = form.transpose()
+        self._keep = [np.ascontiguousarray(form.kA, np.int32), np.ascontiguousarray(form.iA, np.int32),
+                      np.ascontiguousarray(form.A, np.float64), kAt, iAt, At]
+        self.h = L.orc_kkt_create(self.m, self.n, *[a.ctypes.data for a in self._keep])
+
+    def factor(self, E, D):
+        E = np.ascontiguousarray(E, np.float64)
+        D = np.ascontiguousarray(D, np.float64)
+        lib().orc_kkt_factor(self.h, E.ctypes.data, D.ctypes.data)
+
+    def solve(self, E, D, fy, fx):
+        E = np.ascontiguousarray(E, np.float64)
+        D = np.ascontiguousarray(D, np.float64)
+        fy = np.array(fy, np.float64, copy=True)
+        fx = np.array(fx, np.float64, copy=True)
+        ok = lib().orc_kkt_solve(self.h, E.ctypes.data, D.ctypes.data, fy.ctypes.data, fx.ctypes.data)
+        return fy, fx, ok
+
+    def info(self):
+        L = lib()
+        return dict(lnz=L.orc_kkt_lnz(self.h), narth=L.orc_kkt_narth(self.h), denwin=L.orc_kkt_denwin(self.h),
+                    pdf=L.orc_kkt_pdf(self.h), ndep=L.orc_kkt_ndep(self.h), epsdiag=L.orc_kkt_epsdiag(self.h),
+                    passes=L.orc_kkt_last_passes(self.h))
+
+    def perm(self):
+        p = np.zeros(self.m + self.n, np.int32)
+        lib().orc_kkt_perm(self.h, p.ctypes.data)
+        return p
+
+    def diag(self):
+        d = np.zeros(self.m + self.n, np.float64)
+        lib().orc_kkt_diag(self.h, d.ctypes.data)
+        return d
+
+    def __del__(self):
+        try:
+            lib().orc_kkt_destroy(self.h)
+        except Exception:
+            pass
