@@ -122,7 +122,7 @@ def cpu_baseline(mps, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=117, help="IPM iterations timed (capped by convergence)")
+    ap.add_argument("--steps", type=int, default=200, help="IPM iterations timed (MAX_ITER; the solve stops at convergence, 117 for dfl001)")
     ap.add_argument("--warmup", type=int, default=2, help="untimed IPM iterations before the timed solve")
     ap.add_argument("--problem", default="dfl001")
     ap.add_argument("--cpu-iters", type=int, default=3, help="HSD iterations of the CPU oracle sample (0 = skip)")

@@ -107,6 +107,8 @@ int    ipo_hip_kkt_solve(ipo_hip_kkt *k, const double *E, const double *D, doubl
 int    ipo_hip_kkt_info(const ipo_hip_kkt *k, long *lnz, double *narth, int *nsup, int *nlevels, int *denwin,
                         int *pdf, double *epsdiag, int *ndep, int *passes);
 int    ipo_hip_kkt_perm(const ipo_hip_kkt *k, int *perm);
+/* start from a captured state: the reference's eps_diag floor (ldlt.c:31,301-305) */
+void   ipo_hip_kkt_set_epsdiag(ipo_hip_kkt *k, double epsdiag);
 
 /* Host-only symbolic analysis (no GPU needed): reference ordering stats. */
 int ipo_hip_symbolic(int m, int n, const int *kA, const int *iA, int *perm, long *lnz, double *narth,

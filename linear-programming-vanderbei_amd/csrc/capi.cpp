@@ -393,6 +393,8 @@ int ipo_hip_kkt_perm(const ipo_hip_kkt* k, int* perm) {
     return 0;
 }
 
+void ipo_hip_kkt_set_epsdiag(ipo_hip_kkt* k, double e) { k->kkt->set_epsdiag(e); }
+
 int ipo_hip_symbolic(int m, int n, const int* kA, const int* iA, int* perm, long* lnz, double* narth, int* denwin,
                      int* pdf, int* nsup, int* nlevels) {
     try {

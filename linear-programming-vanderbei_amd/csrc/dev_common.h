@@ -61,6 +61,9 @@ __global__ void __launch_bounds__(kRedThreads)
 k_reduce_jobs(RedJobs jobs, double* __restrict__ part);
 
 // Host helper: run jobs, finish into out[0..nj) (device), async on stream.
+// With g_ordered_reductions (default) dot jobs are summed in index order like
+// the reference's dotprod(); otherwise by a fixed-shape tree.
+extern bool g_ordered_reductions;
 void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st);
 
 }  // namespace ipo

@@ -34,7 +34,57 @@ k_finish_reduce(const double* __restrict__ part, int nq, unsigned maxmask, doubl
     }
 }
 
+// dotprod() of linalg.c:17-25 in its own order: one running sum, i = 0..n-1.
+// One block per job; the products are independent (prefetched), only the
+// adds form the sequential chain.  Max-type jobs are order-free.
+__global__ void __launch_bounds__(64)
+k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
+    const int j = blockIdx.x;
+    const double* a = jobs.a[j];
+    const double* b = jobs.b[j];
+    const int len = jobs.len[j];
+    const int op = jobs.op[j];
+    if (op != 0) {
+        __shared__ double sh[1];
+        double acc = 0.0;
+        for (int i = threadIdx.x; i < len; i += 64) {
+            if (op == 1) acc = fmax(acc, ref_abs(a[i]));
+            else acc = fmax(acc, -a[i] / b[i]);
+        }
+        acc = wave_max(acc);
+        if (threadIdx.x == 0) { sh[0] = acc; out[j] = acc; }
+        return;
+    }
+    // products in parallel into LDS, then one lane adds them in index order
+    constexpr int CH = 4096;
+    __shared__ double prod[CH];
+    double s = 0.0e0;
+    for (int base = 0; base < len; base += CH) {
+        const int cnt = min(CH, len - base);
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += 64) prod[i] = a[base + i] * b[base + i];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int i = 0;
+            for (; i + 8 <= cnt; i += 8) {
+                const double p0 = prod[i], p1 = prod[i + 1], p2 = prod[i + 2], p3 = prod[i + 3];
+                const double p4 = prod[i + 4], p5 = prod[i + 5], p6 = prod[i + 6], p7 = prod[i + 7];
+                s += p0; s += p1; s += p2; s += p3; s += p4; s += p5; s += p6; s += p7;
+            }
+            for (; i < cnt; i++) s += prod[i];
+        }
+    }
+    if (threadIdx.x == 0) out[j] = s;
+}
+
+bool g_ordered_reductions = true;
+
 void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st) {
+    if (g_ordered_reductions) {
+        hipLaunchKernelGGL(k_reduce_ordered, dim3(jobs.nj), dim3(64), 0, st, jobs, out);
+        IPO_HIP_CHECK(hipGetLastError());
+        return;
+    }
     unsigned mask = 0;
     for (int j = 0; j < jobs.nj; j++) if (jobs.op[j] != 0) mask |= 1u << j;
     hipLaunchKernelGGL(k_reduce_jobs, dim3(kRedBlocks), dim3(kRedThreads), 0, st, jobs, part);

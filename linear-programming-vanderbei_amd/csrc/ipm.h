@@ -65,6 +65,7 @@ class IpmSolver {
     DevBuf<double> rho_, sig_, D_, E_, fx_, fy_, gx_, gy_, dx_, dy_, dz_, dw_;
     DevBuf<double> part_, scal_;
     double* hs_ = nullptr;       // pinned scalars
+    bool full_trace_ = false;    // IPO_HIP_TRACE_FULL: full-precision scalars per iteration on stderr
 };
 
 // Whole-pipeline convenience used by the C ABI: host arrays in, host out.

@@ -7,6 +7,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 
 #include "dev_common.h"
 #include "ipm.h"
@@ -255,6 +256,7 @@ int IpmSolver::run(const IpmOptions& opt, IpmResult* res) {
 }
 
 int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
+    full_trace_ = std::getenv("IPO_HIP_TRACE_FULL") != nullptr;
     const int m = m_, n = n_;
     hipStream_t s = stream_;
     const int gv = ceil_div(m + n, NT);
@@ -305,8 +307,10 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
         }
         res->final_mu = mu; res->final_pobj = pobj / phi + f_; res->final_dobj = dobj / phi + f_;
         res->final_pinf = normr; res->final_dinf = norms;
+        if (full_trace_) std::fprintf(stderr, "FT %d %.17g %.17g %.17g %.17g %.17g %.17g\n", iter, pobj, dobj, mu, phi, psi, normr);
 
         K.factor(E_.get(), D_.get());
+        if (full_trace_) std::fprintf(stderr, "FT   ndep=%d eps=%.1e\n", K.ndep(), K.epsdiag());
         K.solve(E_.get(), D_.get(), fy_.get(), fx_.get());
         res->refine_passes += K.last_passes();
         K.solve(E_.get(), D_.get(), gy_.get(), gx_.get());

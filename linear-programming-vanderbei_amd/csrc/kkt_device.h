@@ -19,13 +19,23 @@
 
 namespace ipo {
 
+// Device view of the dense tail (see kkt_plan.h): S = nt x nt column-major.
+struct TailView {
+    double* S;
+    int nt, ntb, tc;
+    const int* task_ptr;
+    const TailTask* tasks;
+    double* W;        // nt x 64 workspace: L21 * D of the current block column
+};
+
 struct KktTimers {
     double factor_ms = 0.0;   // accumulated device time of factor()
     double solve_ms = 0.0;    // accumulated device time of solve()
     double update_ms = 0.0;   // k_update launches only (timing mode)
     double panel_ms = 0.0;    // k_factor launches only (timing mode)
     double sweep_ms = 0.0;    // forward + backward substitution sweeps (timing mode)
-    long update_launches = 0, panel_launches = 0;
+    double tail_update_ms = 0.0;  // k_tail_update (timing mode)
+    long update_launches = 0, panel_launches = 0, tail_update_launches = 0;
     long factors = 0, solves = 0, rawsolves = 0;
 };
 
@@ -61,6 +71,9 @@ class KktDevice {
     void rawsolve(double* dz);
 
     double epsdiag() const { return epsdiag_; }
+    void set_pivot_tolerance(double t) { pivot_tol_ = t; }
+    void set_epsdiag(double e) { epsdiag_ = e; }
+    double pivot_tolerance() const { return pivot_tol_; }
     int ndep() const { return ndep_; }
     int last_passes() const { return last_passes_; }
     const KktTimers& timers() const { return tm_; }
@@ -72,6 +85,7 @@ class KktDevice {
     double* device_diag() const { return dDg_.get(); }
 
   private:
+    TailView tail_view() const;
     void launch_reduce_maxabs2(const double* a, int na, const double* b, int nb, double* dst);
 
     int m_, n_, T_;
@@ -79,6 +93,10 @@ class KktDevice {
     KktPlan plan_;
     double epsdiag_ = 1.0e-14;     // ldlt.c:31, grows x10 (ldlt.c:301-305)
     int ndep_ = 0;
+    // Zero-pivot test |d| <= tol * sum|terms| (the reference tests d == 0,
+    // which in its own operation order catches exact cancellations; a
+    // different summation order leaves a few ulps instead).  2^-46.
+    double pivot_tol_ = 1.4210854715202004e-14;
     int last_passes_ = 0;
     bool timing_ = false;
     KktTimers tm_;
@@ -94,9 +112,13 @@ class KktDevice {
     DevBuf<int> dunit_sup_, dunit_tile_, dtask_ptr_, dtask_pair_, dtask_i0_, dtask_i1_;
     DevBuf<int> dupd_src_, dupd_r0_, dupd_r1_, drel_, dlevel_sups_;
     DevBuf<int> dfrow_ptr_, dfrow_col_;
+    DevBuf<int> dtail_task_ptr_;
+    DevBuf<uint64_t> dtail_tasks_, dutasks_;
+    DevBuf<double> dW_;
     // numeric
     DevBuf<double> dLx_, dDg_;
     DevBuf<int> dLive_;
+    DevBuf<double> dDscale_;
     DevBuf<int> dFlags_;           // [0] ndep, [1] inconsistent
     DevBuf<double> dZ_, dDy_, dDx_, dRy_, dRx_;
     DevBuf<double> dPart_, dScal_;

@@ -8,13 +8,14 @@
 //         are the rows R_s of L21.  One contiguous array, 8-B aligned.
 //   dg    D of L D L' (new index order), live = the reference's mark[].
 //
-// Factor = per elimination-tree level two kernels:
+// Factor = per elimination-tree level three kernels:
 //   k_update  one workgroup per (panel, 64-row tile): left-looking gather
 //             of every descendant panel's rank-nc_d update into an LDS tile
 //             (fixed task order -> bitwise reproducible), then subtract.
-//   k_factor  same units: dense LDL' of the diagonal block in LDS (redundant
-//             per tile, tiny), dependent-pivot rule of ldlt.c:600-614, then
-//             the triangular solve of the tile's L21 rows.
+//   k_diag    one workgroup per panel: dense LDL' of the diagonal block in
+//             LDS with the dependent-pivot rule of ldlt.c:600-614; L11' is
+//             stored in the block's unused upper triangle.
+//   k_trsm    one workgroup per 64-row tile: L21 = A21 L11^-T D^-1.
 // Solve = per level: forward row-gather + in-wave block substitution +
 // diagonal scaling (bottom-up), then column-gather + block back substitution
 // (top-down).  Refinement loop as ldlt.c:367-416.
@@ -22,6 +23,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "dev_common.h"
@@ -57,6 +59,8 @@ struct PlanView {
     int* live;
     int* flags;      // [0] dependent pivots, [1] inconsistent system
     const int* sign; // node class per new index: -1 y-node, +1 x-node
+    double* dscale;  // sum of |terms| that formed each pivot (zero-pivot test)
+    double tau;      // pivot d is "zero" when |d| <= tau * dscale
 };
 
 // ---------------------------------------------------------------- assembly
@@ -70,97 +74,127 @@ k_assemble_A(int nz, const double* __restrict__ A, const int64_t* __restrict__ a
 __global__ void __launch_bounds__(NT)
 k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __restrict__ E,
                 const double* __restrict__ D, double eps, const int64_t* __restrict__ dslot,
-                double* __restrict__ Lx, int* __restrict__ live) {
+                double* __restrict__ Lx, int* __restrict__ live, double* __restrict__ dscale) {
     const int v = blockIdx.x * NT + threadIdx.x;
     if (v >= T) return;
     const int old = perm[v];
-    Lx[dslot[v]] = old < m ? -ref_max(E[old], eps) : ref_max(D[old - m], eps);
+    const double a = old < m ? -ref_max(E[old], eps) : ref_max(D[old - m], eps);
+    Lx[dslot[v]] = a;
+    dscale[v] = fabs(a);
     live[v] = 1;
 }
 
 // ------------------------------------------------------- left-looking gather
+// Accumulate gather tasks into one 64-row x (<= 64)-column output tile.
+// Thread (row r = tid & 63, column group g = tid >> 6) owns 16 entries of
+// the tile and sums its terms in registers in task order: no LDS, no
+// barriers, bitwise reproducible.  Each task names a source panel and, by
+// bit masks, which tile rows / columns its rows land in (TailTask).
+//   out(r, c) -= sum_tasks sum_k L(row, k) * (d_k * L(col, k))      (ldlt.c:572,583)
+// Entries with (row0 + r) < (col0 + c) are skipped (upper triangle); on the
+// diagonal the |terms| are added to dscale for the zero-pivot test.
+__device__ void gather_tile(const PlanView& p, const TailTask* __restrict__ tasks, int tb, int te, double* out,
+                            size_t ld, int nrow, int ncol, int row0, int col0, double* dscale_col) {
+    const int tid = threadIdx.x;
+    const int r = tid & 63, g = tid >> 6;
+    double acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) acc[q] = 0.0;
+    double dabs = 0.0;
+    const int prow = row0 + r;
+    for (int task = tb; task < te; task++) {
+        const TailTask tk = tasks[task];
+        if (!((tk.rmask >> r) & 1ull)) continue;
+        const uint64_t cm = (tk.cmask >> (g * 16)) & 0xFFFFull;
+        if (!cm) continue;
+        const int d = tk.src;
+        const int cd0 = p.col0[d], ncd = p.col0[d + 1] - cd0;
+        const int hd = ncd + (p.rowptr[d + 1] - p.rowptr[d]);
+        const double* __restrict__ Ld = p.Lx + p.off[d] + ncd;      // row i of R_d at Ld[i + k*hd]
+        const double* __restrict__ dd = p.dg + cd0;
+        const int ri = tk.rbase + __popcll(tk.rmask & ((1ull << r) - 1ull));
+        int cj = tk.cbase + __popcll(tk.cmask & ((1ull << (g * 16)) - 1ull));
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            if (!((cm >> q) & 1ull)) continue;
+            const int pcol = col0 + g * 16 + q;
+            if (prow >= pcol) {
+                double sum = 0.0;
+                if (prow != pcol) {
+                    for (int k = 0; k < ncd; k++) sum += Ld[ri + (size_t)k * hd] * (dd[k] * Ld[cj + (size_t)k * hd]);
+                } else {
+                    double as = 0.0;
+                    for (int k = 0; k < ncd; k++) {
+                        const double t = Ld[ri + (size_t)k * hd] * (dd[k] * Ld[cj + (size_t)k * hd]);
+                        sum += t;
+                        as += fabs(t);
+                    }
+                    dabs += as;
+                }
+                acc[q] += sum;
+            }
+            cj++;
+        }
+    }
+    if (r >= nrow) return;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int c = g * 16 + q;
+        if (c >= ncol || prow < col0 + c) continue;
+        out[r + (size_t)c * ld] -= acc[q];
+    }
+    if (dscale_col && prow >= col0 && prow < col0 + ncol && (prow - col0) / 16 == g) dscale_col[prow - col0] += dabs;
+}
+
 __global__ void __launch_bounds__(NT)
-k_update(PlanView p, int u0) {
-    __shared__ double acc[TR][PC + 1];
+k_update(PlanView p, const TailTask* __restrict__ tasks, int u0) {
     const int u = u0 + blockIdx.x;
-    const int s = p.unit_sup[u], t = p.unit_tile[u];
     const int tb = p.task_ptr[u], te = p.task_ptr[u + 1];
     if (tb == te) return;
+    const int s = p.unit_sup[u], t = p.unit_tile[u];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
     const int rbase = t * TR;
-    const int nrow = min(TR, h - rbase);
-    for (int i = threadIdx.x; i < TR * (PC + 1); i += NT) (&acc[0][0])[i] = 0.0;
-    __syncthreads();
-    for (int task = tb; task < te; task++) {
-        const int q = p.task_pair[task];
-        const int i0 = p.task_i0[task], i1 = p.task_i1[task];
-        const int d = p.upd_src[q];
-        const int cd0 = p.col0[d], ncd = p.col0[d + 1] - cd0;
-        const int hd = ncd + (p.rowptr[d + 1] - p.rowptr[d]);
-        const int r0 = p.upd_r0[q];
-        const int ncols = p.upd_r1[q] - r0;
-        const double* __restrict__ Ld = p.Lx + p.off[d] + ncd + r0;
-        const double* __restrict__ dd = p.dg + cd0;
-        const int* __restrict__ rl = p.rel + p.relptr[q];
-        const int nr = i1 - i0;
-        const int tot = nr * ncols;
-        for (int idx = threadIdx.x; idx < tot; idx += NT) {
-            const int ii = i0 + idx % nr;
-            const int jj = idx / nr;
-            const int prow = rl[ii], pcol = rl[jj];
-            if (prow < pcol) continue;
-            double sum = 0.0;
-            for (int k = 0; k < ncd; k++) sum += Ld[ii + (size_t)k * hd] * (dd[k] * Ld[jj + (size_t)k * hd]);
-            acc[prow - rbase][pcol] += sum;
-        }
-        __syncthreads();
-    }
-    double* panel = p.Lx + p.off[s];
-    for (int idx = threadIdx.x; idx < nrow * nc; idx += NT) {
-        const int r = idx % nrow, c = idx / nrow;
-        if (rbase + r >= c) panel[(rbase + r) + (size_t)c * h] -= acc[r][c];
-    }
+    gather_tile(p, tasks, tb, te, p.Lx + p.off[s] + rbase, h, min(TR, h - rbase), nc, rbase, 0,
+                t == 0 ? p.dscale + c0 : nullptr);
 }
 
-// ------------------------------------------- diagonal block LDL' + L21 solve
-__global__ void __launch_bounds__(NT)
-k_factor(PlanView p, int u0) {
-    __shared__ double B[PC][PC + 1];      // diagonal block, B[row][col]
-    __shared__ double R[TR][PC + 1];      // this tile's L21 rows
+// ------------------------------------------------- diagonal block LDL'
+// Dense LDL' of an nc x nc diagonal block (nc <= 64) of a panel with leading
+// dimension ld and h rows (rows nc..h-1 lie below the block); c0 is the
+// block's first global column.  Reads the block's lower triangle, factors it
+// right-looking in LDS with the dependent-pivot rule of ldlt.c:600-614 and
+// the reference's update form l_r * (l_c * d), and stores L11' in the
+// block's UPPER triangle (the lower one keeps the input), D in dg, mark in
+// live.  One 256-thread workgroup.
+__device__ void factor_diag_block(const PlanView& p, double* panel, int ld, int nc, int h, int c0) {
+    __shared__ double B[PC][PC + 1];
     __shared__ double dv[PC];
     __shared__ int lv[PC];
+    __shared__ double dsc[PC];
     __shared__ double red[4];
     __shared__ int ndep_sh;
-    const int u = u0 + blockIdx.x;
-    const int s = p.unit_sup[u], t = p.unit_tile[u];
-    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
-    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
-    double* panel = p.Lx + p.off[s];
     const int tid = threadIdx.x;
-
-    for (int idx = tid; idx < nc * nc; idx += NT) {
-        const int r = idx % nc, c = idx / nc;
-        B[r][c] = r >= c ? panel[r + (size_t)c * h] : 0.0;
-    }
+    const int tr = tid & 63, tp = tid >> 6;     // row, part (4 parts stride the columns)
+    for (int c = tp; c < nc; c += 4) B[tr][c] = (tr < nc && tr >= c) ? panel[tr + (size_t)c * ld] : 0.0;
+    for (int k = tid; k < nc; k += NT) dsc[k] = p.dscale[c0 + k];
     if (tid == 0) ndep_sh = 0;
     __syncthreads();
-
     for (int k = 0; k < nc; k++) {
         double dk = B[k][k];
         int alive = 1;
-        if (fabs(dk) <= 0.0) {                    // epsnum = 0 (ldlt.c:29): exact zero pivot
-            // largest off-diagonal magnitude of column k after all updates
-            // from columns < k: block rows are in B, rows below are rebuilt
-            // here by a partial forward solve (rare path).
+        if (fabs(dk) <= p.tau * dsc[k]) {         // ldlt.c:600 with a rounding-aware zero test
+            // largest off-diagonal magnitude of column k after every update
+            // from columns < k; rows below the block are rebuilt from the
+            // (not yet solved) panel by a partial forward substitution
             double mx = 0.0;
             for (int r = k + 1 + tid; r < nc; r += NT) mx = ref_max(mx, ref_abs(B[r][k]));
             for (int rr = nc + tid; rr < h; rr += NT) {
                 double w[PC];
-                for (int c = 0; c <= k; c++) w[c] = panel[rr + (size_t)c * h];
+                for (int c = 0; c <= k; c++) w[c] = panel[rr + (size_t)c * ld];
                 for (int j = 0; j < k; j++) {
-                    const double wj = lv[j] ? w[j] : 0.0;
-                    for (int c = j + 1; c <= k; c++) w[c] -= wj * B[c][j];
+                    const double lj = lv[j] ? w[j] / dv[j] : 0.0;
+                    for (int c = j + 1; c <= k; c++) w[c] -= lj * (B[c][j] * dv[j]);
                 }
                 mx = ref_max(mx, ref_abs(w[k]));
             }
@@ -168,59 +202,187 @@ k_factor(PlanView p, int u0) {
             if (tid == 0) red[0] = mx;
             __syncthreads();
             mx = red[0];
-            if (mx < 1.0e+6 * 1.0e-8) alive = 0;              // column dropped, d stays 0
+            if (mx < 1.0e+6 * 1.0e-8) alive = 0;                    // column dropped, d keeps its value
             else dk = (p.sign[c0 + k] < 0 ? -1.0 : 1.0) * 1.0e-8;   // y-nodes -, x-nodes +
             if (tid == 0) ndep_sh++;
             __syncthreads();
         }
         if (tid == 0) { dv[k] = dk; lv[k] = alive; }
+        // scale column k first (lij = a / d), then update with lij * (ljk * d)
+        for (int r = k + 1 + tid; r < nc; r += NT) B[r][k] = alive ? B[r][k] / dk : 0.0;
         __syncthreads();
-        // right-looking update of the trailing block, then scale column k
-        if (alive) {
-            const double inv = 1.0 / dk;
-            for (int idx = tid; idx < (nc - k - 1) * (nc - k - 1); idx += NT) {
-                const int r = k + 1 + idx % (nc - k - 1);
-                const int c = k + 1 + idx / (nc - k - 1);
-                if (r >= c) B[r][c] -= B[r][k] * (B[c][k] * inv);
+        if (alive && tr > k && tr < nc) {
+            const double lr = B[tr][k];
+            for (int c = k + 1 + tp; c <= tr; c += 4) {
+                const double tk = lr * (B[c][k] * dk);
+                B[tr][c] -= tk;
+                if (tr == c) dsc[c] += fabs(tk);
             }
         }
         __syncthreads();
-        for (int r = k + 1 + tid; r < nc; r += NT) B[r][k] = alive ? B[r][k] / dk : 0.0;
-        __syncthreads();
     }
+    // L11(r, c) -> upper slot (c, r): thread tr writes row c = tr of the slot image
+    for (int r = tp; r < nc; r += 4)
+        if (tr < r) panel[tr + (size_t)r * ld] = B[r][tr];
+    for (int k = tid; k < nc; k += NT) { p.dg[c0 + k] = dv[k]; p.live[c0 + k] = lv[k]; }
+    if (tid == 0 && ndep_sh) atomicAdd(&p.flags[0], ndep_sh);
+}
 
-    if (t == 0) {
-        for (int idx = tid; idx < nc * nc; idx += NT) {
-            const int r = idx % nc, c = idx / nc;
-            if (r > c) panel[r + (size_t)c * h] = B[r][c];
-        }
-        for (int k = tid; k < nc; k += NT) { p.dg[c0 + k] = dv[k]; p.live[c0 + k] = lv[k]; }
-        if (tid == 0 && ndep_sh) atomicAdd(&p.flags[0], ndep_sh);
-    }
+__global__ void __launch_bounds__(NT)
+k_diag(PlanView p, const int* __restrict__ level_sups, int q0) {
+    const int s = level_sups[q0 + blockIdx.x];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+    factor_diag_block(p, p.Lx + p.off[s], h, nc, h, c0);
+}
 
-    // L21 rows of this tile: w = a - sum_j w_j L11(k, j); l = w / d
-    const int rbase = t * TR;
-    const int rlo = max(rbase, nc), rhi = min(rbase + TR, h);
+// ------------------------------------------------------- L21 = A21 L11^-T D^-1
+// Rows [rlo, rhi) of a panel (ld, nc columns starting at global column c0),
+// against the factored diagonal block (L11' in its upper triangle).  With
+// wbuf != nullptr also writes W = L21 * D (row-major-by-column, ldw) for the
+// dense tail's trailing update.  Reference form: l = w / d, w -= l * (l11 * d).
+__device__ void solve_rows(const PlanView& p, double* panel, int ld, int nc, int c0, int rlo, int rhi,
+                           double* wbuf, int ldw, int wrow0) {
+    __shared__ double B[PC][PC + 1];      // L11(c, k) * d_k
+    __shared__ double R[TR][PC + 1];
+    __shared__ double dv[PC];
+    __shared__ int lv[PC];
     const int nrow = rhi - rlo;
-    if (nrow <= 0) return;
+    const int tid = threadIdx.x;
+    for (int k = tid; k < nc; k += NT) { dv[k] = p.dg[c0 + k]; lv[k] = p.live[c0 + k]; }
+    __syncthreads();
+    {
+        const int cc = tid & 63, rp = tid >> 6;    // slot (cc, r) holds L11(r, cc)
+        for (int r = rp; r < nc; r += 4) B[r][cc] = (cc < r) ? panel[cc + (size_t)r * ld] * dv[cc] : 0.0;
+    }
     for (int idx = tid; idx < nrow * nc; idx += NT) {
         const int r = idx % nrow, c = idx / nrow;
-        R[r][c] = panel[(rlo + r) + (size_t)c * h];
+        R[r][c] = panel[(rlo + r) + (size_t)c * ld];
     }
     __syncthreads();
     const int r = tid & 63, part = tid >> 6;
     for (int k = 0; k < nc; k++) {
-        const double wk = r < nrow ? R[r][k] : 0.0;
+        const double lk = (r < nrow && lv[k]) ? R[r][k] / dv[k] : 0.0;
         __syncthreads();
         if (r < nrow) {
-            for (int c = k + 1 + part; c < nc; c += 4) R[r][c] -= wk * B[c][k];
-            if (part == 0) R[r][k] = lv[k] ? wk / dv[k] : 0.0;
+            for (int c = k + 1 + part; c < nc; c += 4) R[r][c] -= lk * B[c][k];
+            if (part == 0) R[r][k] = lk;
         }
         __syncthreads();
     }
     for (int idx = tid; idx < nrow * nc; idx += NT) {
         const int rr = idx % nrow, c = idx / nrow;
-        panel[(rlo + rr) + (size_t)c * h] = R[rr][c];
+        const double l = R[rr][c];
+        panel[(rlo + rr) + (size_t)c * ld] = l;
+        if (wbuf) wbuf[(wrow0 + rr) + (size_t)c * ldw] = l * dv[c];
+    }
+}
+
+__global__ void __launch_bounds__(NT)
+k_trsm(PlanView p, int u0) {
+    const int u = u0 + blockIdx.x;
+    const int s = p.unit_sup[u], t = p.unit_tile[u];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+    const int rbase = t * TR;
+    const int rlo = max(rbase, nc), rhi = min(rbase + TR, h);
+    if (rhi <= rlo) return;
+    solve_rows(p, p.Lx + p.off[s], h, nc, c0, rlo, rhi, nullptr, 0, 0);
+}
+
+// ======================================================== dense tail
+// S = Lx + off_tail, nt x nt column-major (ld = nt), columns tail_c0.. .
+// (TailView is declared in kkt_device.h)
+
+// Gather of all sparse panels' contributions into one 64x64 tile of S.
+__global__ void __launch_bounds__(NT)
+k_tail_update(PlanView p, TailView tv) {
+    const int tile = blockIdx.x;
+    int bi = 0;
+    while ((bi + 1) * (bi + 2) / 2 <= tile) bi++;
+    const int bj = tile - bi * (bi + 1) / 2;
+    const int tb = tv.task_ptr[tile], te = tv.task_ptr[tile + 1];
+    if (tb == te) return;
+    const int nrow = min(TR, tv.nt - bi * TR), ncol = min(TR, tv.nt - bj * TR);
+    gather_tile(p, tv.tasks, tb, te, tv.S + bi * TR + (size_t)(bj * TR) * tv.nt, tv.nt, nrow, ncol, bi * TR, bj * TR,
+                bi == bj ? p.dscale + tv.tc + bj * TR : nullptr);
+}
+
+__global__ void __launch_bounds__(NT)
+k_tail_diag(PlanView p, TailView tv, int kb) {
+    const int k0 = kb * PC;
+    const int nc = min(PC, tv.nt - k0);
+    factor_diag_block(p, tv.S + k0 + (size_t)k0 * tv.nt, tv.nt, nc, tv.nt - k0, tv.tc + k0);
+}
+
+__global__ void __launch_bounds__(NT)
+k_tail_trsm(PlanView p, TailView tv, int kb) {
+    const int k0 = kb * PC;
+    const int nc = min(PC, tv.nt - k0);
+    const int rlo = nc + blockIdx.x * TR;            // rows relative to the block column
+    const int rhi = min(rlo + TR, tv.nt - k0);
+    if (rhi <= rlo) return;
+    solve_rows(p, tv.S + k0 + (size_t)k0 * tv.nt, tv.nt, nc, tv.tc + k0, rlo, rhi, tv.W, tv.nt, rlo);
+}
+
+// Trailing update S(bi, bj) -= L(bi, kb) * W(bj, kb)'  for bi >= bj > kb,
+// with v_mfma_f64_16x16x4_f64: 4 waves, each a 32x32 quarter (2x2 MFMA tiles).
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(NT)
+k_tail_syrk(PlanView p, TailView tv, int kb) {
+    __shared__ double As[TR][PC + 1];    // L rows of block bi   [row][k]
+    __shared__ double Bs[TR][PC + 1];    // W rows of block bj   [row][k]
+    const int nb = tv.ntb - kb - 1;      // trailing blocks
+    const int tile = blockIdx.x;
+    int ti = 0;
+    while ((ti + 1) * (ti + 2) / 2 <= tile) ti++;
+    const int tj = tile - ti * (ti + 1) / 2;
+    if (ti >= nb) return;
+    const int bi = kb + 1 + ti, bj = kb + 1 + tj;
+    const int k0 = kb * PC;
+    const int nc = min(PC, tv.nt - k0);
+    const int nt = tv.nt;
+    const int tid = threadIdx.x;
+    const double* Lcol = tv.S + (size_t)k0 * nt;      // column k0 of S
+    // W rows are stored relative to the block column: W[(row - k0) + k * nt]
+    for (int idx = tid; idx < TR * PC; idx += NT) {
+        const int rr = idx % TR, k = idx / TR;
+        const int ra = bi * TR + rr, rb = bj * TR + rr;
+        As[rr][k] = (k < nc && ra < nt) ? Lcol[ra + (size_t)k * nt] : 0.0;
+        Bs[rr][k] = (k < nc && rb < nt) ? tv.W[(rb - k0) + (size_t)k * nt] : 0.0;
+    }
+    __syncthreads();
+    const int wv = tid >> 6, lane = tid & 63;
+    const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
+    double4_t acc[2][2];
+    for (int a = 0; a < 2; a++)
+        for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    const int li = lane & 15, lk = lane >> 4;
+    for (int kk = 0; kk < PC; kk += 4) {
+        double av[2], bv[2];
+        for (int a = 0; a < 2; a++) av[a] = As[wr + a * 16 + li][kk + lk];
+        for (int b = 0; b < 2; b++) bv[b] = Bs[wc + b * 16 + li][kk + lk];
+        for (int a = 0; a < 2; a++)
+            for (int b = 0; b < 2; b++) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+    const bool diag_tile = bi == bj;
+    for (int a = 0; a < 2; a++)
+        for (int b = 0; b < 2; b++)
+            for (int i = 0; i < 4; i++) {
+                const int rr = wr + a * 16 + (lane >> 4) + 4 * i;
+                const int cc = wc + b * 16 + (lane & 15);
+                const int rg = bi * TR + rr, cg = bj * TR + cc;
+                if (rg >= nt || cg >= nt || (diag_tile && cc > rr)) continue;
+                tv.S[rg + (size_t)cg * nt] -= acc[a][b][i];
+            }
+    if (diag_tile && tid < TR) {           // |terms| of the diagonal for the zero-pivot test
+        const int rg = bi * TR + tid;
+        if (rg < nt) {
+            double as = 0.0;
+            for (int k = 0; k < nc; k++) as += fabs(As[tid][k] * Bs[tid][k]);
+            p.dscale[tv.tc + rg] += as;
+        }
     }
 }
 
@@ -231,11 +393,15 @@ k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __r
           const int* __restrict__ frow_col, const int64_t* __restrict__ frow_pos, double* __restrict__ z,
           const double* __restrict__ epsp) {
     __shared__ double zl[PC];
+    __shared__ double Ls[PC][PC + 1];     // Ls[r][j] = L11(r, j)
+    __shared__ int lv[PC];
     const int s = level_sups[q0 + blockIdx.x];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
     const double* panel = p.Lx + p.off[s];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int r = wv; r < nc; r += 4) Ls[r][lane] = lane < r ? panel[lane + (size_t)r * h] : 0.0;
+    if (threadIdx.x < nc) lv[threadIdx.x] = p.live[c0 + threadIdx.x];
     for (int k = wv; k < nc; k += 4) {
         const int v = c0 + k;
         double acc = 0.0;
@@ -249,21 +415,15 @@ k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __r
     double zr = lane < nc ? zl[lane] : 0.0;
     int bad = 0;
     for (int j = 0; j < nc; j++) {
-        const int alive = p.live[c0 + j];
+        const int alive = lv[j];
         if (lane == j && !alive) {
             if (fabs(zr) > eps) bad = 1;
             else zr = 0.0;
         }
         const double zj = __shfl(zr, j, 64);
-        if (alive && lane > j && lane < nc) zr -= panel[lane + (size_t)j * h] * zj;
+        if (alive && lane > j && lane < nc) zr -= Ls[lane][j] * zj;
     }
-    if (lane < nc) {
-        const int v = c0 + lane;
-        if (p.live[v]) zr = zr / p.dg[v];
-        else if (fabs(zr) > eps) bad = 1;
-        else zr = 0.0;
-        z[v] = zr;
-    }
+    if (lane < nc) z[c0 + lane] = zr;
     if (bad) atomicOr(&p.flags[1], 1);
 }
 
@@ -272,6 +432,8 @@ __global__ void __launch_bounds__(NT)
 k_backward(PlanView p, const int* __restrict__ level_sups, int q0, double* __restrict__ z,
            const double* __restrict__ epsp) {
     __shared__ double zl[PC];
+    __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L11(j, r)
+    __shared__ int lv[PC];
     const int s = level_sups[q0 + blockIdx.x];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int hb = p.rowptr[s + 1] - p.rowptr[s];
@@ -279,28 +441,146 @@ k_backward(PlanView p, const int* __restrict__ level_sups, int q0, double* __res
     const double* panel = p.Lx + p.off[s];
     const int* rows = p.rows + p.rowptr[s];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int j = wv; j < nc; j += 4) Ls[j][lane] = lane < j ? panel[lane + (size_t)j * h] : 0.0;
+    if (threadIdx.x < nc) lv[threadIdx.x] = p.live[c0 + threadIdx.x];
+    const double eps = *epsp;
+    int bad = 0;
     for (int k = wv; k < nc; k += 4) {
         const double* col = panel + (size_t)k * h + nc;
         double acc = 0.0;
         for (int i = lane; i < hb; i += 64) acc += col[i] * z[rows[i]];
         acc = wave_sum(acc);
-        if (lane == 0) zl[k] = z[c0 + k] - acc;
+        if (lane == 0) {
+            const int v = c0 + k;
+            double zv = z[v];
+            if (p.live[v]) zv = zv / p.dg[v];
+            else if (fabs(zv) > eps) bad = 1;
+            else zv = 0.0;
+            zl[k] = zv - acc;
+        }
     }
+    if (bad) atomicOr(&p.flags[1], 1);
+    bad = 0;
     __syncthreads();
     if (wv != 0) return;
-    const double eps = *epsp;
     double zr = lane < nc ? zl[lane] : 0.0;
-    int bad = 0;
     for (int j = nc - 1; j >= 0; j--) {
-        const int alive = p.live[c0 + j];
+        const int alive = lv[j];
         if (lane == j && !alive) {
             if (fabs(zr) > eps) bad = 1;
             else zr = 0.0;
         }
         const double zj = __shfl(zr, j, 64);
-        if (alive && lane < j) zr -= panel[j + (size_t)lane * h] * zj;
+        if (alive && lane < j) zr -= Ls[j][lane] * zj;
     }
     if (lane < nc) z[c0 + lane] = zr;
+    if (bad) atomicOr(&p.flags[1], 1);
+}
+
+// ---------------------------------------------------- dense-tail solves
+// forward, part 1: tail rows gather the sparse panels' contributions
+__global__ void __launch_bounds__(NT)
+k_tail_gather(PlanView p, TailView tv, const int* __restrict__ frow_ptr, const int* __restrict__ frow_col,
+              const int64_t* __restrict__ frow_pos, double* __restrict__ z) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int i = blockIdx.x * 4 + wv;
+    if (i >= tv.nt) return;
+    const int v = tv.tc + i;
+    double acc = 0.0;
+    for (int e = frow_ptr[v] + lane; e < frow_ptr[v + 1]; e += 64) acc += p.Lx[frow_pos[e]] * z[frow_col[e]];
+    acc = wave_sum(acc);
+    if (lane == 0) z[v] = z[v] - acc;
+}
+
+constexpr int NTB = 1024;   // one workgroup sweeps the dense tail
+
+// forward, part 2: blocked unit-lower solve of the dense tail (one workgroup)
+__global__ void __launch_bounds__(NTB)
+k_tail_fwd(PlanView p, TailView tv, double* __restrict__ z, const double* __restrict__ epsp) {
+    __shared__ double Ls[PC][PC + 1];     // Ls[r][j] = L11(r, j) of the current block
+    __shared__ double zb[PC];
+    __shared__ int lv[PC];
+    const int nt = tv.nt, tc = tv.tc;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const double eps = *epsp;
+    int bad = 0;
+    for (int kb = 0; kb < tv.ntb; kb++) {
+        const int k0 = kb * PC, nc = min(PC, nt - k0);
+        for (int r = wv; r < nc; r += NTB / 64)
+            Ls[r][lane] = lane < r ? tv.S[(k0 + lane) + (size_t)(k0 + r) * nt] : 0.0;
+        if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
+        __syncthreads();
+        if (wv == 0) {
+            double zr = lane < nc ? z[tc + k0 + lane] : 0.0;
+            for (int j = 0; j < nc; j++) {
+                const int alive = lv[j];
+                if (lane == j && !alive) {
+                    if (fabs(zr) > eps) bad = 1;
+                    else zr = 0.0;
+                }
+                const double zj = __shfl(zr, j, 64);
+                if (alive && lane > j && lane < nc) zr -= Ls[lane][j] * zj;
+            }
+            if (lane < nc) { z[tc + k0 + lane] = zr; zb[lane] = zr; }
+        }
+        __syncthreads();
+        for (int r = k0 + nc + tid; r < nt; r += NTB) {
+            double acc = 0.0;
+            for (int k = 0; k < nc; k++) acc += tv.S[r + (size_t)(k0 + k) * nt] * zb[k];
+            z[tc + r] = z[tc + r] - acc;
+        }
+        __syncthreads();
+    }
+    if (bad) atomicOr(&p.flags[1], 1);
+}
+
+// backward: D^{-1} on the tail, then blocked L^{-T} (one workgroup)
+__global__ void __launch_bounds__(NTB)
+k_tail_bwd(PlanView p, TailView tv, double* __restrict__ z, const double* __restrict__ epsp) {
+    __shared__ double zl[PC];
+    __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L11(j, r) of the current block
+    __shared__ int lv[PC];
+    const int nt = tv.nt, tc = tv.tc;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const double eps = *epsp;
+    int bad = 0;
+    for (int i = tid; i < nt; i += NTB) {
+        const int v = tc + i;
+        double zv = z[v];
+        if (p.live[v]) zv = zv / p.dg[v];
+        else if (fabs(zv) > eps) bad = 1;
+        else zv = 0.0;
+        z[v] = zv;
+    }
+    __syncthreads();
+    for (int kb = tv.ntb - 1; kb >= 0; kb--) {
+        const int k0 = kb * PC, nc = min(PC, nt - k0);
+        for (int j = wv; j < nc; j += NTB / 64)
+            Ls[j][lane] = lane < j ? tv.S[(k0 + lane) + (size_t)(k0 + j) * nt] : 0.0;
+        if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
+        for (int k = wv; k < nc; k += NTB / 64) {
+            const double* col = tv.S + (size_t)(k0 + k) * nt;
+            double acc = 0.0;
+            for (int r = k0 + nc + lane; r < nt; r += 64) acc += col[r] * z[tc + r];
+            acc = wave_sum(acc);
+            if (lane == 0) zl[k] = z[tc + k0 + k] - acc;
+        }
+        __syncthreads();
+        if (wv == 0) {
+            double zr = lane < nc ? zl[lane] : 0.0;
+            for (int j = nc - 1; j >= 0; j--) {
+                const int alive = lv[j];
+                if (lane == j && !alive) {
+                    if (fabs(zr) > eps) bad = 1;
+                    else zr = 0.0;
+                }
+                const double zj = __shfl(zr, j, 64);
+                if (alive && lane < j) zr -= Ls[j][lane] * zj;
+            }
+            if (lane < nc) z[tc + k0 + lane] = zr;
+        }
+        __syncthreads();
+    }
     if (bad) atomicOr(&p.flags[1], 1);
 }
 
@@ -413,10 +693,19 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dlevel_sups_.upload(plan_.level_sups, s);
     dfrow_ptr_.upload(plan_.frow_ptr, s);
     dfrow_col_.upload(plan_.frow_col, s);
+    dutasks_.upload(reinterpret_cast<const uint64_t*>(plan_.utasks.data()), plan_.utasks.size() * 4, s);
+    if (plan_.nt > 0) {
+        dtail_task_ptr_.upload(plan_.tail_task_ptr, s);
+        static_assert(sizeof(TailTask) == 32, "TailTask layout");
+        dtail_tasks_.upload(reinterpret_cast<const uint64_t*>(plan_.tail_tasks.data()), plan_.tail_tasks.size() * 4, s);
+        dW_.alloc(static_cast<size_t>(plan_.nt) * kPanelCols);
+    }
 
     dLx_.alloc(plan_.lx_size > 0 ? plan_.lx_size : 1);
     dDg_.alloc(T_ > 0 ? T_ : 1);
     dLive_.alloc(T_ > 0 ? T_ : 1);
+    dDscale_.alloc(T_ > 0 ? T_ : 1);
+    if (const char* e = std::getenv("IPO_HIP_PIVTOL")) pivot_tol_ = std::atof(e);
     // flags: [0] ndep, [1] inconsistent, [2..2+T) node class sign per new index
     dFlags_.alloc(2 + T_);
     {
@@ -466,9 +755,27 @@ static PlanView make_view(const KktPlan&, const DevBuf<int>& col0, const DevBuf<
     return v;
 }
 
-#define IPO_VIEW() make_view(plan_, dcol0_, drowptr_, drows_, doff_, dunit_sup_, dunit_tile_, dtask_ptr_, \
+#define IPO_VIEW() with_scale(make_view(plan_, dcol0_, drowptr_, drows_, doff_, dunit_sup_, dunit_tile_, dtask_ptr_, \
                              dtask_pair_, dtask_i0_, dtask_i1_, dupd_src_, dupd_r0_, dupd_r1_, drelptr_, drel_, \
-                             dLx_, dDg_, dLive_, dFlags_)
+                             dLx_, dDg_, dLive_, dFlags_), dDscale_.get(), pivot_tol_)
+
+static PlanView with_scale(PlanView v, double* dscale, double tau) {
+    v.dscale = dscale;
+    v.tau = tau;
+    return v;
+}
+
+TailView KktDevice::tail_view() const {
+    TailView t;
+    t.S = dLx_.get() + plan_.off_tail;
+    t.nt = plan_.nt;
+    t.ntb = plan_.ntb;
+    t.tc = plan_.tail_c0;
+    t.task_ptr = dtail_task_ptr_.get();
+    t.tasks = reinterpret_cast<const TailTask*>(dtail_tasks_.get());
+    t.W = dW_.get();
+    return t;
+}
 
 void KktDevice::factor(const double* dE, const double* dD) {
     hipStream_t s = stream_;
@@ -479,24 +786,44 @@ void KktDevice::factor(const double* dE, const double* dD) {
     IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get(), 0, 2 * sizeof(int), s));
     if (nz > 0) hipLaunchKernelGGL(k_assemble_A, dim3(ceil_div(nz, NT)), dim3(NT), 0, s, nz, dA_.get(), damap_.get(), dLx_.get());
     hipLaunchKernelGGL(k_assemble_diag, dim3(ceil_div(T_, NT)), dim3(NT), 0, s, T_, m_, dperm_.get(), dE, dD, epsdiag_,
-                       ddslot_.get(), dLx_.get(), dLive_.get());
+                       ddslot_.get(), dLx_.get(), dLive_.get(), dDscale_.get());
     if (timing_ && kev_.size() < static_cast<size_t>(4 * plan_.nlevels)) {
         for (hipEvent_t e : kev_) (void)hipEventDestroy(e);
         kev_.assign(4 * plan_.nlevels, nullptr);
         for (hipEvent_t& e : kev_) IPO_HIP_CHECK(hipEventCreate(&e));
     }
     std::vector<char> upd_used(timing_ ? plan_.nlevels : 0, 0);
+    const TailView tv = tail_view();
     for (int l = 0; l < plan_.nlevels; l++) {
         const int u0 = plan_.unit_level_ptr[l], u1 = plan_.unit_level_ptr[l + 1];
         if (u1 <= u0) continue;
         if (l > 0) {
             if (timing_) { IPO_HIP_CHECK(hipEventRecord(kev_[4 * l], s)); upd_used[l] = 1; }
-            hipLaunchKernelGGL(k_update, dim3(u1 - u0), dim3(NT), 0, s, pv, u0);
+            hipLaunchKernelGGL(k_update, dim3(u1 - u0), dim3(NT), 0, s, pv,
+                               reinterpret_cast<const TailTask*>(dutasks_.get()), u0);
             if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 1], s));
         }
+        const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 2], s));
-        hipLaunchKernelGGL(k_factor, dim3(u1 - u0), dim3(NT), 0, s, pv, u0);
+        hipLaunchKernelGGL(k_diag, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0);
+        hipLaunchKernelGGL(k_trsm, dim3(u1 - u0), dim3(NT), 0, s, pv, u0);
         if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 3], s));
+    }
+    if (plan_.nt > 0) {
+        const int ntiles = plan_.ntb * (plan_.ntb + 1) / 2;
+        if (timing_) IPO_HIP_CHECK(hipEventRecord(ev2_, s));
+        hipLaunchKernelGGL(k_tail_update, dim3(ntiles), dim3(NT), 0, s, pv, tv);
+        if (timing_) IPO_HIP_CHECK(hipEventRecord(ev3_, s));
+        for (int kb = 0; kb < plan_.ntb; kb++) {
+            const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
+            hipLaunchKernelGGL(k_tail_diag, dim3(1), dim3(NT), 0, s, pv, tv, kb);
+            const int below = plan_.nt - k0 - nc;
+            if (below > 0) {
+                hipLaunchKernelGGL(k_tail_trsm, dim3(ceil_div(below, kTileRows)), dim3(NT), 0, s, pv, tv, kb);
+                const int nb = plan_.ntb - kb - 1;
+                hipLaunchKernelGGL(k_tail_syrk, dim3(nb * (nb + 1) / 2), dim3(NT), 0, s, pv, tv, kb);
+            }
+        }
     }
     IPO_HIP_CHECK(hipGetLastError());
     // min |d| over the factor (ldlt.c:293-306) and the dependent-pivot count
@@ -520,6 +847,11 @@ void KktDevice::factor(const double* dE, const double* dD) {
             IPO_HIP_CHECK(hipEventElapsedTime(&ms, kev_[4 * l + 2], kev_[4 * l + 3]));
             tm_.panel_ms += ms;
             tm_.panel_launches++;
+        }
+        if (plan_.nt > 0) {
+            IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev2_, ev3_));
+            tm_.tail_update_ms += ms;
+            tm_.tail_update_launches++;
         }
     }
     tm_.factors++;
@@ -545,6 +877,13 @@ void KktDevice::rawsolve(double* dz) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         hipLaunchKernelGGL(k_forward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dfrow_ptr_.get(),
                            dfrow_col_.get(), dfrow_pos_.get(), dz, epsp);
+    }
+    if (plan_.nt > 0) {
+        const TailView tv = tail_view();
+        hipLaunchKernelGGL(k_tail_gather, dim3(ceil_div(plan_.nt, 4)), dim3(NT), 0, s, pv, tv, dfrow_ptr_.get(),
+                           dfrow_col_.get(), dfrow_pos_.get(), dz);
+        hipLaunchKernelGGL(k_tail_fwd, dim3(1), dim3(NTB), 0, s, pv, tv, dz, epsp);
+        hipLaunchKernelGGL(k_tail_bwd, dim3(1), dim3(NTB), 0, s, pv, tv, dz, epsp);
     }
     for (int l = plan_.nlevels - 1; l >= 0; l--) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];

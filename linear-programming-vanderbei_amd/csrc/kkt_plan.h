@@ -25,6 +25,7 @@ namespace ipo {
 
 constexpr int kPanelCols = 64;     // max columns per supernode panel
 constexpr int kTileRows = 64;      // rows per factor work unit
+constexpr int kTailMin = 128;      // smallest dense tail handled as a dense block
 
 struct KktOrdering {
     int m = 0, n = 0, T = 0;
@@ -38,6 +39,15 @@ struct KktOrdering {
 // ldlt.c:638-858 (inv_sym) + ldlt.c:860-1262 (lltsym), method _MD, dense = 3
 KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
                                     const int* kAt, const int* iAt);
+
+// One gather task into a 64x64 tile of the dense tail: the tail rows of
+// source panel `src` whose positions inside the tile's row block (rmask)
+// and column block (cmask) are given as bit masks; R_src indices start at
+// rbase / cbase and follow the mask bit order.
+struct TailTask {
+    uint64_t rmask, cmask;
+    int src, rbase, cbase, pad;
+};
 
 struct KktPlan {
     int m = 0, n = 0, T = 0;
@@ -73,6 +83,16 @@ struct KktPlan {
     std::vector<int> dsign;         // [T] -1 for y-nodes, +1 for x-nodes (new index)
     int64_t lx_size = 0;
 
+    // dense tail: columns [tail_c0, T) form a full lower triangle (the
+    // reference's dense window); stored as an nt x nt column-major block at
+    // Lx + off_tail and factored right-looking in 64-column blocks.
+    int tail_c0 = 0, nt = 0, ntb = 0;
+    int64_t off_tail = 0;
+    std::vector<int> tail_r0;          // per sparse panel: first R_s index inside the tail
+    std::vector<int> tail_task_ptr;    // per tile (bi*(bi+1)/2 + bj)
+    std::vector<TailTask> tail_tasks;
+    double flops_tail_update = 0.0, bytes_tail_update = 0.0, flops_tail_factor = 0.0;
+
     // GPU work decomposition (filled by build_kkt_plan)
     //  factor units: one per (supernode, 64-row tile of its panel), grouped
     //  by level; unit u gathers tasks task_ptr[u]..task_ptr[u+1], each a
@@ -80,6 +100,7 @@ struct KktPlan {
     std::vector<int> unit_level_ptr;   // [nlevels+1]
     std::vector<int> unit_sup, unit_tile;
     std::vector<int> task_ptr, task_pair, task_i0, task_i1;
+    std::vector<TailTask> utasks;      // the same tasks as row/column bit masks
     //  forward-solve row lists: for row v, the L entries (v, col) whose column
     //  lies in another supernode: Lx slot and column.
     std::vector<int> frow_ptr;         // [T+1]

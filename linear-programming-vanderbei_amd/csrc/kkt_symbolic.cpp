@@ -205,30 +205,40 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
     P.pdf = o.pdf;
     P.denwin = o.denwin;
 
-    // ---- supernodes: column j+1 joins j's panel when struct(L_j+1) = struct(L_j) \ {j+1}
     std::vector<int> cnt(T);
     for (int j = 0; j < T; j++) cnt[j] = o.Lp[j + 1] - o.Lp[j];
+
+    // ---- dense tail: the maximal suffix of columns whose L column is full
+    //      (the reference's dense window, ldlt.c:1027 / :587-590)
+    int tc = T;
+    while (tc > 0 && cnt[tc - 1] == T - tc) tc--;
+    if (T - tc < kTailMin) tc = T;
+    P.tail_c0 = tc;
+    P.nt = T - tc;
+    P.ntb = (P.nt + kTileRows - 1) / kTileRows;
+
+    // ---- sparse supernodes on [0, tc): column j+1 joins j's panel when
+    //      struct(L_j+1) = struct(L_j) \ {j+1}; panels hold <= kPanelCols columns
     P.col0.clear();
-    P.col0.push_back(0);
-    for (int j = 0; j + 1 < T; j++) {
-        const int width = j + 1 - P.col0.back();
-        const bool nested = cnt[j] > 0 && o.Li[o.Lp[j]] == j + 1 && cnt[j + 1] == cnt[j] - 1;
-        if (!nested || width >= kPanelCols) P.col0.push_back(j + 1);
+    if (tc > 0) {
+        P.col0.push_back(0);
+        for (int j = 0; j + 1 < tc; j++) {
+            const int width = j + 1 - P.col0.back();
+            const bool nested = cnt[j] > 0 && o.Li[o.Lp[j]] == j + 1 && cnt[j + 1] == cnt[j] - 1;
+            if (!nested || width >= kPanelCols) P.col0.push_back(j + 1);
+        }
+        P.col0.push_back(tc);
+    } else {
+        P.col0.push_back(0);
     }
-    P.col0.push_back(T);
     P.nsup = static_cast<int>(P.col0.size()) - 1;
     const int ns = P.nsup;
-
-    P.sup_of.assign(T, 0);
+    P.sup_of.assign(T, -1);
     for (int s = 0; s < ns; s++)
         for (int j = P.col0[s]; j < P.col0[s + 1]; j++) P.sup_of[j] = s;
 
-    // below-block rows of each panel = rows of its last column
     P.rowptr.assign(ns + 1, 0);
-    for (int s = 0; s < ns; s++) {
-        const int last = P.col0[s + 1] - 1;
-        P.rowptr[s + 1] = P.rowptr[s] + cnt[last];
-    }
+    for (int s = 0; s < ns; s++) P.rowptr[s + 1] = P.rowptr[s] + cnt[P.col0[s + 1] - 1];
     P.rows.resize(P.rowptr[ns]);
     P.off.assign(ns + 1, 0);
     for (int s = 0; s < ns; s++) {
@@ -240,13 +250,19 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
         P.max_h = std::max(P.max_h, h);
         P.max_nc = std::max(P.max_nc, nc);
     }
-    P.lx_size = P.off[ns];
+    P.off_tail = P.off[ns];
+    P.lx_size = P.off_tail + static_cast<int64_t>(P.nt) * P.nt;
 
-    // ---- supernodal tree + levels (children have smaller indices)
+    auto panel_h = [&](int s) { return P.col0[s + 1] - P.col0[s] + (P.rowptr[s + 1] - P.rowptr[s]); };
+
+    // ---- sparse supernodal tree + levels (children have smaller indices)
     P.parent.assign(ns, -1);
     P.level.assign(ns, 0);
     for (int s = 0; s < ns; s++) {
-        if (P.rowptr[s + 1] > P.rowptr[s]) P.parent[s] = P.sup_of[P.rows[P.rowptr[s]]];
+        if (P.rowptr[s + 1] > P.rowptr[s]) {
+            const int r = P.rows[P.rowptr[s]];
+            P.parent[s] = r < tc ? P.sup_of[r] : -1;
+        }
     }
     for (int s = 0; s < ns; s++)
         if (P.parent[s] >= 0) P.level[P.parent[s]] = std::max(P.level[P.parent[s]], P.level[s] + 1);
@@ -261,56 +277,45 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
         for (int s = 0; s < ns; s++) P.level_sups[fill[P.level[s]]++] = s;
     }
 
-    // position of a global row inside panel s
-    auto panel_pos = [&](int s, int row) -> int {
-        const int c0 = P.col0[s], c1 = P.col0[s + 1];
-        if (row < c1) return row - c0;
-        auto b = P.rows.begin() + P.rowptr[s], e = P.rows.begin() + P.rowptr[s + 1];
-        auto it = std::lower_bound(b, e, row);
-        if (it == e || *it != row) throw std::logic_error("kkt plan: row not in target panel");
-        return (c1 - c0) + static_cast<int>(it - b);
-    };
-
-    // ---- update pairs: source d touches every supernode owning one of its rows
+    // ---- sparse update pairs (targets below the tail)
     struct Pair { int tgt, src, r0, r1; };
     std::vector<Pair> pairs;
+    P.tail_r0.assign(ns, 0);
     for (int d = 0; d < ns; d++) {
         const int b = P.rowptr[d], e = P.rowptr[d + 1];
         int i = b;
-        while (i < e) {
+        while (i < e && P.rows[i] < tc) {
             const int t = P.sup_of[P.rows[i]];
             int j = i;
-            while (j < e && P.sup_of[P.rows[j]] == t) j++;
+            while (j < e && P.rows[j] < tc && P.sup_of[P.rows[j]] == t) j++;
             pairs.push_back({t, d, i - b, j - b});
             i = j;
         }
+        P.tail_r0[d] = i - b;       // R_d[tail_r0 ..] are tail rows
     }
     std::stable_sort(pairs.begin(), pairs.end(), [](const Pair& a, const Pair& b) { return a.tgt < b.tgt; });
     P.upd_ptr.assign(ns + 1, 0);
-    for (const Pair& p : pairs) P.upd_ptr[p.tgt + 1]++;
+    for (const Pair& q : pairs) P.upd_ptr[q.tgt + 1]++;
     for (int s = 0; s < ns; s++) P.upd_ptr[s + 1] += P.upd_ptr[s];
     const size_t np = pairs.size();
     P.upd_src.resize(np); P.upd_r0.resize(np); P.upd_r1.resize(np); P.relptr.assign(np + 1, 0);
     for (size_t q = 0; q < np; q++) {
-        const Pair& p = pairs[q];
-        const int hd = P.rowptr[p.src + 1] - P.rowptr[p.src];
-        P.upd_src[q] = p.src; P.upd_r0[q] = p.r0; P.upd_r1[q] = p.r1;
-        P.relptr[q + 1] = P.relptr[q] + (hd - p.r0);
-        const double ra = hd - p.r0, rc = p.r1 - p.r0, nc = P.col0[p.src + 1] - P.col0[p.src];
-        P.flops_factor += 2.0 * nc * rc * (ra - 0.5 * rc);
+        const Pair& pr = pairs[q];
+        const int hd = P.rowptr[pr.src + 1] - P.rowptr[pr.src];
+        P.upd_src[q] = pr.src; P.upd_r0[q] = pr.r0; P.upd_r1[q] = pr.r1;
+        P.relptr[q + 1] = P.relptr[q] + (hd - pr.r0);
     }
     P.rel.resize(P.relptr[np]);
     for (size_t q = 0; q < np; q++) {
-        const Pair& p = pairs[q];
-        const int* rd = P.rows.data() + P.rowptr[p.src];
-        const int hd = P.rowptr[p.src + 1] - P.rowptr[p.src];
+        const Pair& pr = pairs[q];
+        const int* rd = P.rows.data() + P.rowptr[pr.src];
+        const int hd = P.rowptr[pr.src + 1] - P.rowptr[pr.src];
         int64_t o2 = P.relptr[q];
-        // rows are sorted in both lists: merge instead of searching
-        const int c0 = P.col0[p.tgt], c1 = P.col0[p.tgt + 1];
-        const int* rt = P.rows.data() + P.rowptr[p.tgt];
-        const int ht = P.rowptr[p.tgt + 1] - P.rowptr[p.tgt];
+        const int c0 = P.col0[pr.tgt], c1 = P.col0[pr.tgt + 1];
+        const int* rt = P.rows.data() + P.rowptr[pr.tgt];
+        const int ht = P.rowptr[pr.tgt + 1] - P.rowptr[pr.tgt];
         int it = 0;
-        for (int i = p.r0; i < hd; i++) {
+        for (int i = pr.r0; i < hd; i++) {
             const int row = rd[i];
             if (row < c1) { P.rel[o2++] = row - c0; continue; }
             while (it < ht && rt[it] < row) it++;
@@ -318,27 +323,22 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
             P.rel[o2++] = (c1 - c0) + it;
         }
     }
-    for (int s = 0; s < ns; s++) {      // dense factor + trsm of each panel
-        const double nc = P.col0[s + 1] - P.col0[s], h = nc + (P.rowptr[s + 1] - P.rowptr[s]);
-        P.flops_factor += nc * nc * nc / 3.0 + (h - nc) * nc * nc;
-    }
 
-    // ---- GPU work units: (supernode, row tile), level by level
+    // ---- sparse GPU work units: (supernode, row tile), level by level
     {
-        std::vector<int> unit_first(ns + 1, 0);      // first unit of supernode s
+        std::vector<int> unit_first(ns + 1, 0);
         P.unit_level_ptr.assign(P.nlevels + 1, 0);
         for (int l = 0; l < P.nlevels; l++) {
             for (int q = P.level_ptr[l]; q < P.level_ptr[l + 1]; q++) {
                 const int s = P.level_sups[q];
-                const int h = P.col0[s + 1] - P.col0[s] + (P.rowptr[s + 1] - P.rowptr[s]);
-                const int nt = (h + kTileRows - 1) / kTileRows;
+                const int nt = (panel_h(s) + kTileRows - 1) / kTileRows;
                 unit_first[s] = static_cast<int>(P.unit_sup.size());
                 for (int t = 0; t < nt; t++) { P.unit_sup.push_back(s); P.unit_tile.push_back(t); }
             }
             P.unit_level_ptr[l + 1] = static_cast<int>(P.unit_sup.size());
         }
         const int nu = static_cast<int>(P.unit_sup.size());
-        std::vector<std::vector<int>> tk(nu);          // flattened (pair, i0, i1)
+        std::vector<std::vector<int>> tk(nu);
         for (int s = 0; s < ns; s++) {
             for (int q = P.upd_ptr[s]; q < P.upd_ptr[s + 1]; q++) {
                 const int len = static_cast<int>(P.relptr[q + 1] - P.relptr[q]);
@@ -354,47 +354,90 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
                 }
             }
         }
-        // exact work of the gather kernel: every (i, j) pair with panel row >= panel col
-        for (int u = 0; u < nu; u++) {
-            const int s = P.unit_sup[u];
-            for (size_t e = 0; e < tk[u].size() / 3; e++) {
-                const int q = tk[u][3 * e], i0 = tk[u][3 * e + 1], i1 = tk[u][3 * e + 2];
-                const int* rl = P.rel.data() + P.relptr[q];
-                const int d = P.upd_src[q];
-                const double ncd = P.col0[d + 1] - P.col0[d];
-                const int ncols = P.upd_r1[q] - P.upd_r0[q];
-                long pairs = 0;
-                for (int jj = 0; jj < ncols; jj++) {
-                    // rows i in [i0, i1) with rl[i] >= rl[jj]; rl ascending
-                    const int* lo = std::lower_bound(rl + i0, rl + i1, rl[jj]);
-                    pairs += (rl + i1) - lo;
-                }
-                P.flops_update += pairs * ncd * 3.0;
-                P.bytes_update += 8.0 * ncd * ((i1 - i0) + ncols);   // L_d rows read once per task
-                (void)s;
-            }
-        }
-        for (int u = 0; u < nu; u++) {   // panel tile read-modify-write
-            const int s = P.unit_sup[u];
-            if (P.task_ptr.empty() && tk[u].empty()) continue;
-            if (tk[u].empty()) continue;
-            const int nc = P.col0[s + 1] - P.col0[s];
-            const int h = nc + (P.rowptr[s + 1] - P.rowptr[s]);
-            const int rows = std::min(kTileRows, h - P.unit_tile[u] * kTileRows);
-            P.bytes_update += 16.0 * rows * nc;
-        }
         P.task_ptr.assign(nu + 1, 0);
         for (int u = 0; u < nu; u++) P.task_ptr[u + 1] = P.task_ptr[u] + static_cast<int>(tk[u].size() / 3);
         P.task_pair.resize(P.task_ptr[nu]); P.task_i0.resize(P.task_ptr[nu]); P.task_i1.resize(P.task_ptr[nu]);
+        P.utasks.resize(P.task_ptr[nu]);
         for (int u = 0; u < nu; u++) {
+            const int s = P.unit_sup[u];
+            const int nc = P.col0[s + 1] - P.col0[s];
             for (size_t e = 0; e < tk[u].size() / 3; e++) {
-                P.task_pair[P.task_ptr[u] + e] = tk[u][3 * e];
-                P.task_i0[P.task_ptr[u] + e] = tk[u][3 * e + 1];
-                P.task_i1[P.task_ptr[u] + e] = tk[u][3 * e + 2];
+                const int q = tk[u][3 * e], i0 = tk[u][3 * e + 1], i1 = tk[u][3 * e + 2];
+                P.task_pair[P.task_ptr[u] + e] = q;
+                P.task_i0[P.task_ptr[u] + e] = i0;
+                P.task_i1[P.task_ptr[u] + e] = i1;
+                const int* rl = P.rel.data() + P.relptr[q];
+                {
+                    TailTask tt{};
+                    tt.src = P.upd_src[q];
+                    tt.rbase = P.upd_r0[q] + i0;
+                    tt.cbase = P.upd_r0[q];
+                    const int rb = P.unit_tile[u] * kTileRows;
+                    for (int i = i0; i < i1; i++) tt.rmask |= 1ull << (rl[i] - rb);
+                    for (int jj = 0; jj < P.upd_r1[q] - P.upd_r0[q]; jj++) tt.cmask |= 1ull << rl[jj];
+                    P.utasks[P.task_ptr[u] + e] = tt;
+                }
+                const double ncd = P.col0[P.upd_src[q] + 1] - P.col0[P.upd_src[q]];
+                const int ncols = P.upd_r1[q] - P.upd_r0[q];
+                long prs = 0;
+                for (int jj = 0; jj < ncols; jj++) {
+                    const int* lo = std::lower_bound(rl + i0, rl + i1, rl[jj]);
+                    prs += (rl + i1) - lo;
+                }
+                P.flops_update += 3.0 * ncd * prs;
+                P.bytes_update += 8.0 * ncd * ((i1 - i0) + ncols);
+            }
+            if (!tk[u].empty()) {
+                const int rows = std::min(kTileRows, panel_h(s) - P.unit_tile[u] * kTileRows);
+                P.bytes_update += 16.0 * rows * nc;
             }
         }
     }
-    // ---- forward-solve row lists (entries outside the row's own panel)
+
+    // ---- dense-tail gather tasks: every sparse supernode with tail rows
+    //      touches the 64x64 tiles (bi >= bj) its tail rows span
+    if (P.nt > 0) {
+        const int nb = P.ntb;
+        const int ntiles = nb * (nb + 1) / 2;
+        std::vector<std::vector<TailTask>> tt(ntiles);
+        for (int d = 0; d < ns; d++) {
+            const int b = P.rowptr[d], e = P.rowptr[d + 1];
+            const int q0 = b + P.tail_r0[d];
+            if (q0 >= e) continue;
+            // segments of tail rows per 64-row block
+            std::vector<int> sb, ss, se;
+            std::vector<uint64_t> sm;
+            int i = q0;
+            while (i < e) {
+                const int blk = (P.rows[i] - tc) / kTileRows;
+                int j = i;
+                uint64_t mask = 0;
+                while (j < e && (P.rows[j] - tc) / kTileRows == blk) { mask |= 1ull << ((P.rows[j] - tc) % kTileRows); j++; }
+                sb.push_back(blk); ss.push_back(i - b); se.push_back(j - b); sm.push_back(mask);
+                i = j;
+            }
+            const double ncd = P.col0[d + 1] - P.col0[d];
+            for (size_t x = 0; x < sb.size(); x++)
+                for (size_t y = 0; y <= x; y++) {
+                    TailTask t{};
+                    t.src = d;
+                    t.rbase = ss[x]; t.cbase = ss[y];
+                    t.rmask = sm[x]; t.cmask = sm[y];
+                    tt[sb[x] * (sb[x] + 1) / 2 + sb[y]].push_back(t);
+                    const double ra = se[x] - ss[x], rc = se[y] - ss[y];
+                    P.flops_tail_update += 3.0 * ncd * ra * rc;
+                    P.bytes_tail_update += 8.0 * ncd * (ra + rc);
+                }
+        }
+        P.tail_task_ptr.assign(ntiles + 1, 0);
+        for (int t = 0; t < ntiles; t++) P.tail_task_ptr[t + 1] = P.tail_task_ptr[t] + static_cast<int>(tt[t].size());
+        P.tail_tasks.reserve(P.tail_task_ptr[ntiles]);
+        for (int t = 0; t < ntiles; t++) P.tail_tasks.insert(P.tail_tasks.end(), tt[t].begin(), tt[t].end());
+        const double N = P.nt;
+        P.flops_tail_factor = N * N * N / 3.0 * 2.0;
+    }
+
+    // ---- forward-solve row lists (entries of sparse panels, by row)
     {
         P.frow_ptr.assign(T + 1, 0);
         for (int d = 0; d < ns; d++) {
@@ -419,26 +462,40 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
         }
     }
 
+    for (int s = 0; s < ns; s++) {
+        const double nc = P.col0[s + 1] - P.col0[s], h = panel_h(s);
+        P.flops_factor += nc * nc * nc / 3.0 + (h - nc) * nc * nc;
+    }
+    P.flops_factor += P.flops_update * 2.0 / 3.0 + P.flops_tail_update * 2.0 / 3.0 + P.flops_tail_factor;
+
     // ---- assembly maps
+    auto slot_of = [&](int row, int col) -> int64_t {   // row >= col, new indices
+        if (col >= tc) return P.off_tail + static_cast<int64_t>(col - tc) * P.nt + (row - tc);
+        const int s = P.sup_of[col];
+        const int c0 = P.col0[s], c1 = P.col0[s + 1];
+        const int h = panel_h(s);
+        int pos;
+        if (row < c1) pos = row - c0;
+        else {
+            auto bgn = P.rows.begin() + P.rowptr[s], end = P.rows.begin() + P.rowptr[s + 1];
+            auto it = std::lower_bound(bgn, end, row);
+            if (it == end || *it != row) throw std::logic_error("kkt plan: A entry outside the pattern");
+            pos = (c1 - c0) + static_cast<int>(it - bgn);
+        }
+        return P.off[s] + static_cast<int64_t>(col - c0) * h + pos;
+    };
     P.dslot.resize(T);
     P.dsign.resize(T);
     for (int v = 0; v < T; v++) {
-        const int s = P.sup_of[v];
-        const int h = P.col0[s + 1] - P.col0[s] + (P.rowptr[s + 1] - P.rowptr[s]);
-        const int lc = v - P.col0[s];
-        P.dslot[v] = P.off[s] + static_cast<int64_t>(lc) * h + lc;
+        P.dslot[v] = slot_of(v, v);
         P.dsign[v] = P.perm[v] < m ? -1 : 1;
     }
     P.amap.resize(kA[n]);
-    for (int c = 0; c < n; c++) {
+    for (int c = 0; c < n; c++)
         for (int k = kA[c]; k < kA[c + 1]; k++) {
             const int a = P.iperm[iA[k]], b = P.iperm[m + c];
-            const int col = std::min(a, b), row = std::max(a, b);
-            const int s = P.sup_of[col];
-            const int h = P.col0[s + 1] - P.col0[s] + (P.rowptr[s + 1] - P.rowptr[s]);
-            P.amap[k] = P.off[s] + static_cast<int64_t>(col - P.col0[s]) * h + panel_pos(s, row);
+            P.amap[k] = slot_of(std::max(a, b), std::min(a, b));
         }
-    }
     return P;
 }
 

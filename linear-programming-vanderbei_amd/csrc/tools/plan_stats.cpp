@@ -21,6 +21,8 @@ int main(int argc, char** argv) {
     std::printf("nsup=%d nlevels=%d lx=%lld (%.1f MB) max_h=%d max_nc=%d pairs=%zu rel=%zu flops=%.4e symbolic=%.3fs\n",
                 P.nsup, P.nlevels, (long long)P.lx_size, P.lx_size * 8e-6, P.max_h, P.max_nc, P.upd_src.size(),
                 P.rel.size(), P.flops_factor, dt);
+    std::printf("tail: c0=%d nt=%d blocks=%d tasks=%zu flops_tail_update=%.3e flops_tail_factor=%.3e flops_update=%.3e\n",
+                P.tail_c0, P.nt, P.ntb, P.tail_tasks.size(), P.flops_tail_update, P.flops_tail_factor, P.flops_update);
     if (argc > 2) {
         for (int l = 0; l < P.nlevels; l++) {
             int cnt = P.level_ptr[l + 1] - P.level_ptr[l];

@@ -65,7 +65,7 @@ EXPORTED = [
     "ipo_hip_kkt_info", "ipo_hip_kkt_perm", "ipo_hip_symbolic",
     "ipo_hip_device_count", "ipo_hip_last_error", "ipo_hip_version",
     "ipo_hip_ctx_create", "ipo_hip_ctx_run", "ipo_hip_ctx_download", "ipo_hip_ctx_destroy",
-    "ipo_hip_ctx_setup_seconds",
+    "ipo_hip_ctx_setup_seconds", "ipo_hip_kkt_set_epsdiag",
 ]
 
 _P = C.c_void_p
@@ -112,6 +112,8 @@ def lib() -> C.CDLL:
     L.ipo_hip_kkt_info.restype = _I
     L.ipo_hip_kkt_perm.argtypes = [_P, _P]
     L.ipo_hip_kkt_perm.restype = _I
+    L.ipo_hip_kkt_set_epsdiag.argtypes = [_P, _D]
+    L.ipo_hip_kkt_set_epsdiag.restype = None
     L.ipo_hip_symbolic.argtypes = [_I, _I, _P, _P, _P, C.POINTER(C.c_long), C.POINTER(_D), C.POINTER(_I),
                                    C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]
     L.ipo_hip_symbolic.restype = _I
@@ -293,6 +295,9 @@ class KktFactor:
                                C.byref(pdf), C.byref(eps), C.byref(ndep), C.byref(passes))
         return dict(lnz=lnz.value, narth=narth.value, nsup=nsup.value, nlevels=nlev.value, denwin=denwin.value,
                     pdf=pdf.value, epsdiag=eps.value, ndep=ndep.value, passes=passes.value)
+
+    def set_epsdiag(self, eps: float):
+        lib().ipo_hip_kkt_set_epsdiag(self.h, float(eps))
 
     def perm(self) -> np.ndarray:
         p = np.zeros(self.m + self.n, np.int32)

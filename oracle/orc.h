@@ -101,6 +101,7 @@ void orc_kkt_rowind(const orc_kkt *k, int *rowind); /* [lnz] (new indices, sorte
 void orc_kkt_lvals(const orc_kkt *k, double *lvals);/* [lnz] numeric L after factor */
 void orc_kkt_diag(const orc_kkt *k, double *d);     /* [N]   numeric D after factor */
 double orc_kkt_epsdiag(const orc_kkt *k);
+void   orc_kkt_set_epsdiag(orc_kkt *k, double e);   /* tests: start from a captured state */
 int  orc_kkt_ndep(const orc_kkt *k);
 int  orc_kkt_last_passes(const orc_kkt *k);
 

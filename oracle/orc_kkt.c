@@ -25,6 +25,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 #include "orc.h"
 
 #define EPS_PIVOT   1.0e-8   /* ldlt.c:27  */
@@ -349,6 +350,17 @@ static void numeric_ldlt(orc_kkt *K)
 
 void orc_kkt_factor(orc_kkt *K, const double *E, const double *D)
 {
+    static int fcount = 0;
+    if (getenv("ORC_DUMP_ED")) {   /* debug: capture (E, D) of factorisation #N */
+        if (fcount == atoi(getenv("ORC_DUMP_ED"))) {
+            FILE *f = fopen("/tmp/orc_ed.bin", "wb");
+            fwrite(&K->m, sizeof(int), 1, f); fwrite(&K->n, sizeof(int), 1, f);
+            fwrite(E, sizeof(double), (size_t)K->m, f); fwrite(D, sizeof(double), (size_t)K->n, f);
+            fwrite(&K->epsdiag, sizeof(double), 1, f);
+            fclose(f);
+        }
+        fcount++;
+    }
     int m = K->m, n = K->n, T = K->T;
     int *iperm = K->iperm, *Lp = K->Lp, *Li = K->Li, *pos = K->pos;
     double *Lx = K->Lx, *d = K->d;
@@ -377,6 +389,11 @@ void orc_kkt_factor(orc_kkt *K, const double *E, const double *D)
     double mind = HUGE_VAL;
     for (int v = 0; v < T; v++) if (dabs(d[v]) < mind) mind = dabs(d[v]);
     if (mind < 1.0e-14) K->epsdiag *= 10;
+    if (getenv("ORC_DEBUG_NDEP")) {
+        int dropped = 0;
+        for (int v = 0; v < T; v++) dropped += !K->live[v];
+        fprintf(stderr, "factor: ndep=%d dropped=%d mind=%.3e epsdiag=%.1e\n", K->ndep, dropped, mind, K->epsdiag);
+    }
 }
 
 /* forward / diagonal / backward substitution (rawsolve, ldlt.c:433-505) */
@@ -467,5 +484,6 @@ void orc_kkt_rowind(const orc_kkt *K, int *p) { memcpy(p, K->Li, sizeof(int) * (
 void orc_kkt_lvals(const orc_kkt *K, double *p) { memcpy(p, K->Lx, sizeof(double) * (size_t)K->lnz); }
 void orc_kkt_diag(const orc_kkt *K, double *p) { memcpy(p, K->d, sizeof(double) * (size_t)K->T); }
 double orc_kkt_epsdiag(const orc_kkt *K) { return K->epsdiag; }
+void orc_kkt_set_epsdiag(orc_kkt *K, double e) { K->epsdiag = e; }
 int  orc_kkt_ndep(const orc_kkt *K) { return K->ndep; }
 int  orc_kkt_last_passes(const orc_kkt *K) { return K->passes; }

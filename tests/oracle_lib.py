@@ -60,6 +60,7 @@ def lib():
         L.orc_kkt_epsdiag.argtypes = [P]
         L.orc_kkt_perm.argtypes = [P, P]
         L.orc_kkt_diag.argtypes = [P, P]
+        L.orc_kkt_set_epsdiag.argtypes = [P, D]
         _lib = L
     return _lib
 
@@ -93,6 +94,9 @@ class OracleKkt:
         return dict(lnz=L.orc_kkt_lnz(self.h), narth=L.orc_kkt_narth(self.h), denwin=L.orc_kkt_denwin(self.h),
                     pdf=L.orc_kkt_pdf(self.h), ndep=L.orc_kkt_ndep(self.h), epsdiag=L.orc_kkt_epsdiag(self.h),
                     passes=L.orc_kkt_last_passes(self.h))
+
+    def set_epsdiag(self, eps):
+        lib().orc_kkt_set_epsdiag(self.h, float(eps))
 
     def perm(self):
         p = np.zeros(self.m + self.n, np.int32)
