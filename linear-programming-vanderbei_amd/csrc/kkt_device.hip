@@ -85,77 +85,127 @@ k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __rest
 }
 
 // ------------------------------------------------------- left-looking gather
-// Accumulate gather tasks into one 64-row x (<= 64)-column output tile.
-// Thread (row r = tid & 63, column group g = tid >> 6) owns 16 entries of
-// the tile and sums its terms in registers in task order: no LDS, no
-// barriers, bitwise reproducible.  Each task names a source panel and, by
-// bit masks, which tile rows / columns its rows land in (TailTask).
-//   out(r, c) -= sum_tasks sum_k L(row, k) * (d_k * L(col, k))      (ldlt.c:572,583)
-// Entries with (row0 + r) < (col0 + c) are skipped (upper triangle); on the
-// diagonal the |terms| are added to dscale for the zero-pivot test.
-__device__ void gather_tile(const PlanView& p, const TailTask* __restrict__ tasks, int tb, int te, double* out,
-                            size_t ld, int nrow, int ncol, int row0, int col0, double* dscale_col) {
-    const int tid = threadIdx.x;
-    const int r = tid & 63, g = tid >> 6;
-    double acc[16];
+// out(r, c) -= sum_tasks sum_k L(row, k) * (d_k * L(col, k))     (ldlt.c:572,583)
+// for one 64-row x (<= 64)-column output tile.  The inner dimension is the
+// concatenation of every task's source columns (the plan's k-slot list);
+// kSlab slots at a time are staged in LDS as A(r, k) = L(row(r), k) and
+// B(c, k) = d_k L(col(c), k) -- zero where a task's row / column masks
+// (TailTask) leave the tile entry untouched -- and multiplied with
+// v_mfma_f64_16x16x4_f64, each of the 4 waves owning a 32x32 quarter.
+// Slabs are double-buffered: the global loads of slab s+1 are in flight
+// while slab s is multiplied.  The fixed slot order makes the sum bitwise
+// reproducible.  Entries above the diagonal ((row0 + r) < (col0 + c)) are
+// not written; on the diagonal the |terms| are added to dscale.
+typedef double double4_t __attribute__((ext_vector_type(4)));
+constexpr int KS = kSlab;
+
+__device__ __forceinline__ void stage_slab(const PlanView& p, const TailTask* __restrict__ tasks,
+                                           const int* __restrict__ kslot, int base, int wv, int lane,
+                                           double (&ra)[KS / 4], double (&rb)[KS / 4]) {
+    const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int q = 0; q < 16; q++) acc[q] = 0.0;
-    double dabs = 0.0;
-    const int prow = row0 + r;
-    for (int task = tb; task < te; task++) {
-        const TailTask tk = tasks[task];
-        if (!((tk.rmask >> r) & 1ull)) continue;
-        const uint64_t cm = (tk.cmask >> (g * 16)) & 0xFFFFull;
-        if (!cm) continue;
+    for (int j = 0; j < KS / 4; j++) {
+        const int sl = __builtin_amdgcn_readfirstlane(kslot[base + wv * (KS / 4) + j]);
+        ra[j] = 0.0;
+        rb[j] = 0.0;
+        if (sl < 0) continue;
+        const TailTask tk = tasks[sl >> 6];
+        const int kl = sl & 63;
         const int d = tk.src;
         const int cd0 = p.col0[d], ncd = p.col0[d + 1] - cd0;
         const int hd = ncd + (p.rowptr[d + 1] - p.rowptr[d]);
-        const double* __restrict__ Ld = p.Lx + p.off[d] + ncd;      // row i of R_d at Ld[i + k*hd]
-        const double* __restrict__ dd = p.dg + cd0;
-        const int ri = tk.rbase + __popcll(tk.rmask & ((1ull << r) - 1ull));
-        int cj = tk.cbase + __popcll(tk.cmask & ((1ull << (g * 16)) - 1ull));
+        const double* __restrict__ col = p.Lx + p.off[d] + ncd + (size_t)kl * hd;
+        if ((tk.rmask >> lane) & 1ull) ra[j] = col[tk.rbase + __popcll(tk.rmask & below)];
+        if ((tk.cmask >> lane) & 1ull) rb[j] = p.dg[cd0 + kl] * col[tk.cbase + __popcll(tk.cmask & below)];
+    }
+}
+
+__device__ void gather_tile(const PlanView& p, const TailTask* __restrict__ tasks, const int* __restrict__ kslot,
+                            int kb, int ke, double* out, size_t ld, int nrow, int ncol, int row0, int col0,
+                            double* dscale_col) {
+    __shared__ double As[2][TR][KS + 1];
+    __shared__ double Bs[2][TR][KS + 1];
+    __shared__ double dred[4][TR];
+    const int tid = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
+    const int li = lane & 15, lk = lane >> 4;
+    // diagonal entries of this tile: row r meets column c = row0 + r - col0
+    const int dcol = row0 + lane - col0;
+    const bool has_diag = dscale_col && dcol >= 0 && dcol < ncol && lane < nrow;
+    double4_t acc[2][2];
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            if (!((cm >> q) & 1ull)) continue;
-            const int pcol = col0 + g * 16 + q;
-            if (prow >= pcol) {
-                double sum = 0.0;
-                if (prow != pcol) {
-                    for (int k = 0; k < ncd; k++) sum += Ld[ri + (size_t)k * hd] * (dd[k] * Ld[cj + (size_t)k * hd]);
-                } else {
-                    double as = 0.0;
-                    for (int k = 0; k < ncd; k++) {
-                        const double t = Ld[ri + (size_t)k * hd] * (dd[k] * Ld[cj + (size_t)k * hd]);
-                        sum += t;
-                        as += fabs(t);
-                    }
-                    dabs += as;
-                }
-                acc[q] += sum;
-            }
-            cj++;
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    double dabs = 0.0;
+    double ra[KS / 4], rb[KS / 4];
+    const int nslab = (ke - kb) / KS;
+    stage_slab(p, tasks, kslot, kb, wv, lane, ra, rb);
+#pragma unroll
+    for (int j = 0; j < KS / 4; j++) { As[0][lane][wv * (KS / 4) + j] = ra[j]; Bs[0][lane][wv * (KS / 4) + j] = rb[j]; }
+    __syncthreads();
+    for (int sb = 0; sb < nslab; sb++) {
+        const int cur = sb & 1;
+        if (sb + 1 < nslab) stage_slab(p, tasks, kslot, kb + (sb + 1) * KS, wv, lane, ra, rb);
+#pragma unroll
+        for (int kk = 0; kk < KS; kk += 4) {
+            double av[2], bv[2];
+#pragma unroll
+            for (int a = 0; a < 2; a++) av[a] = As[cur][wr + a * 16 + li][kk + lk];
+#pragma unroll
+            for (int b = 0; b < 2; b++) bv[b] = Bs[cur][wc + b * 16 + li][kk + lk];
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
         }
-    }
-    if (r >= nrow) return;
+        if (has_diag) {
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const int c = g * 16 + q;
-        if (c >= ncol || prow < col0 + c) continue;
-        out[r + (size_t)c * ld] -= acc[q];
+            for (int j = 0; j < KS / 4; j++) {
+                const int k = wv * (KS / 4) + j;
+                dabs += fabs(As[cur][lane][k] * Bs[cur][dcol][k]);
+            }
+        }
+        if (sb + 1 < nslab) {
+#pragma unroll
+            for (int j = 0; j < KS / 4; j++) {
+                As[cur ^ 1][lane][wv * (KS / 4) + j] = ra[j];
+                Bs[cur ^ 1][lane][wv * (KS / 4) + j] = rb[j];
+            }
+        }
+        __syncthreads();
     }
-    if (dscale_col && prow >= col0 && prow < col0 + ncol && (prow - col0) / 16 == g) dscale_col[prow - col0] += dabs;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int rr = wr + a * 16 + (lane >> 4) + 4 * i;
+                const int cc = wc + b * 16 + (lane & 15);
+                if (rr >= nrow || cc >= ncol || row0 + rr < col0 + cc) continue;
+                out[rr + (size_t)cc * ld] -= acc[a][b][i];
+            }
+    if (dscale_col) {
+        dred[wv][lane] = dabs;
+        __syncthreads();
+        if (wv == 0 && has_diag) dscale_col[dcol] += ((dred[0][lane] + dred[1][lane]) + dred[2][lane]) + dred[3][lane];
+    }
 }
 
 __global__ void __launch_bounds__(NT)
-k_update(PlanView p, const TailTask* __restrict__ tasks, int u0) {
+k_update(PlanView p, const TailTask* __restrict__ tasks, const int* __restrict__ kslot,
+         const int* __restrict__ kslot_ptr, int u0) {
     const int u = u0 + blockIdx.x;
-    const int tb = p.task_ptr[u], te = p.task_ptr[u + 1];
-    if (tb == te) return;
+    const int kb = kslot_ptr[u], ke = kslot_ptr[u + 1];
+    if (kb == ke) return;
     const int s = p.unit_sup[u], t = p.unit_tile[u];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
     const int rbase = t * TR;
-    gather_tile(p, tasks, tb, te, p.Lx + p.off[s] + rbase, h, min(TR, h - rbase), nc, rbase, 0,
+    gather_tile(p, tasks, kslot, kb, ke, p.Lx + p.off[s] + rbase, h, min(TR, h - rbase), nc, rbase, 0,
                 t == 0 ? p.dscale + c0 : nullptr);
 }
 
@@ -296,15 +346,15 @@ k_trsm(PlanView p, int u0) {
 
 // Gather of all sparse panels' contributions into one 64x64 tile of S.
 __global__ void __launch_bounds__(NT)
-k_tail_update(PlanView p, TailView tv) {
+k_tail_update(PlanView p, TailView tv, const int* __restrict__ kslot, const int* __restrict__ kslot_ptr) {
     const int tile = blockIdx.x;
     int bi = 0;
     while ((bi + 1) * (bi + 2) / 2 <= tile) bi++;
     const int bj = tile - bi * (bi + 1) / 2;
-    const int tb = tv.task_ptr[tile], te = tv.task_ptr[tile + 1];
-    if (tb == te) return;
+    const int kb = kslot_ptr[tile], ke = kslot_ptr[tile + 1];
+    if (kb == ke) return;
     const int nrow = min(TR, tv.nt - bi * TR), ncol = min(TR, tv.nt - bj * TR);
-    gather_tile(p, tv.tasks, tb, te, tv.S + bi * TR + (size_t)(bj * TR) * tv.nt, tv.nt, nrow, ncol, bi * TR, bj * TR,
+    gather_tile(p, tv.tasks, kslot, kb, ke, tv.S + bi * TR + (size_t)(bj * TR) * tv.nt, tv.nt, nrow, ncol, bi * TR, bj * TR,
                 bi == bj ? p.dscale + tv.tc + bj * TR : nullptr);
 }
 
@@ -327,7 +377,6 @@ k_tail_trsm(PlanView p, TailView tv, int kb) {
 
 // Trailing update S(bi, bj) -= L(bi, kb) * W(bj, kb)'  for bi >= bj > kb,
 // with v_mfma_f64_16x16x4_f64: 4 waves, each a 32x32 quarter (2x2 MFMA tiles).
-typedef double double4_t __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(NT)
 k_tail_syrk(PlanView p, TailView tv, int kb) {
@@ -693,9 +742,13 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dlevel_sups_.upload(plan_.level_sups, s);
     dfrow_ptr_.upload(plan_.frow_ptr, s);
     dfrow_col_.upload(plan_.frow_col, s);
+    dkslot_.upload(plan_.kslot, s);
+    dkslot_ptr_.upload(plan_.kslot_ptr, s);
     dutasks_.upload(reinterpret_cast<const uint64_t*>(plan_.utasks.data()), plan_.utasks.size() * 4, s);
     if (plan_.nt > 0) {
         dtail_task_ptr_.upload(plan_.tail_task_ptr, s);
+        dtail_kslot_.upload(plan_.tail_kslot, s);
+        dtail_kslot_ptr_.upload(plan_.tail_kslot_ptr, s);
         static_assert(sizeof(TailTask) == 32, "TailTask layout");
         dtail_tasks_.upload(reinterpret_cast<const uint64_t*>(plan_.tail_tasks.data()), plan_.tail_tasks.size() * 4, s);
         dW_.alloc(static_cast<size_t>(plan_.nt) * kPanelCols);
@@ -800,7 +853,7 @@ void KktDevice::factor(const double* dE, const double* dD) {
         if (l > 0) {
             if (timing_) { IPO_HIP_CHECK(hipEventRecord(kev_[4 * l], s)); upd_used[l] = 1; }
             hipLaunchKernelGGL(k_update, dim3(u1 - u0), dim3(NT), 0, s, pv,
-                               reinterpret_cast<const TailTask*>(dutasks_.get()), u0);
+                               reinterpret_cast<const TailTask*>(dutasks_.get()), dkslot_.get(), dkslot_ptr_.get(), u0);
             if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 1], s));
         }
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
@@ -812,7 +865,8 @@ void KktDevice::factor(const double* dE, const double* dD) {
     if (plan_.nt > 0) {
         const int ntiles = plan_.ntb * (plan_.ntb + 1) / 2;
         if (timing_) IPO_HIP_CHECK(hipEventRecord(ev2_, s));
-        hipLaunchKernelGGL(k_tail_update, dim3(ntiles), dim3(NT), 0, s, pv, tv);
+        hipLaunchKernelGGL(k_tail_update, dim3(ntiles), dim3(NT), 0, s, pv, tv, dtail_kslot_.get(),
+                           dtail_kslot_ptr_.get());
         if (timing_) IPO_HIP_CHECK(hipEventRecord(ev3_, s));
         for (int kb = 0; kb < plan_.ntb; kb++) {
             const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);

@@ -25,6 +25,7 @@ namespace ipo {
 
 constexpr int kPanelCols = 64;     // max columns per supernode panel
 constexpr int kTileRows = 64;      // rows per factor work unit
+constexpr int kSlab = 16;         // k-columns staged per MFMA gather step
 constexpr int kTailMin = 128;      // smallest dense tail handled as a dense block
 
 struct KktOrdering {
@@ -101,6 +102,12 @@ struct KktPlan {
     std::vector<int> unit_sup, unit_tile;
     std::vector<int> task_ptr, task_pair, task_i0, task_i1;
     std::vector<TailTask> utasks;      // the same tasks as row/column bit masks
+    //  k-slot lists for the MFMA gather: the inner dimension of a unit's
+    //  (or tail tile's) update is the concatenation of its tasks' source
+    //  columns; slot = (task << 6) | column-in-source, -1 = padding, each
+    //  list padded to a multiple of kSlab.
+    std::vector<int> kslot, kslot_ptr;            // per factor unit
+    std::vector<int> tail_kslot, tail_kslot_ptr;  // per tail tile
     //  forward-solve row lists: for row v, the L entries (v, col) whose column
     //  lies in another supernode: Lx slot and column.
     std::vector<int> frow_ptr;         // [T+1]

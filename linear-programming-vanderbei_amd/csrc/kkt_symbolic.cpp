@@ -437,6 +437,28 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
         P.flops_tail_factor = N * N * N / 3.0 * 2.0;
     }
 
+    // ---- k-slot lists (inner dimension of the MFMA gather)
+    {
+        auto build = [&](const std::vector<int>& tptr, const std::vector<TailTask>& tasks, std::vector<int>& ks,
+                         std::vector<int>& kp) {
+            const int nu = static_cast<int>(tptr.size()) - 1;
+            if (static_cast<int64_t>(tasks.size()) >= (int64_t(1) << 25))
+                throw std::length_error("kkt plan: too many gather tasks for 25-bit slot ids");
+            kp.assign(nu + 1, 0);
+            ks.clear();
+            for (int u = 0; u < nu; u++) {
+                for (int t = tptr[u]; t < tptr[u + 1]; t++) {
+                    const int d = tasks[t].src, ncd = P.col0[d + 1] - P.col0[d];
+                    for (int k = 0; k < ncd; k++) ks.push_back((t << 6) | k);
+                }
+                while (ks.size() % kSlab) ks.push_back(-1);
+                kp[u + 1] = static_cast<int>(ks.size());
+            }
+        };
+        build(P.task_ptr, P.utasks, P.kslot, P.kslot_ptr);
+        if (P.nt > 0) build(P.tail_task_ptr, P.tail_tasks, P.tail_kslot, P.tail_kslot_ptr);
+    }
+
     // ---- forward-solve row lists (entries of sparse panels, by row)
     {
         P.frow_ptr.assign(T + 1, 0);

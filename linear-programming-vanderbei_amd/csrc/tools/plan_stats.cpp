@@ -2,6 +2,7 @@
 #include <chrono>
 #include <cstdio>
 #include <string>
+#include <algorithm>
 #include "../kkt_plan.h"
 #include "../lp_io.h"
 
@@ -33,6 +34,45 @@ int main(int argc, char** argv) {
             }
             std::printf("L%d: sups=%d rows=%ld maxh=%d\n", l, cnt, work, maxh);
         }
+    }
+    if (argc > 2 && std::string(argv[2]) == "units") {
+        // per level: units, tasks, useful flops, and the critical path of the
+        // mask gather = max over units of max over threads of sum ncd*cols
+        double tot_crit = 0;
+        for (int l = 0; l < P.nlevels; l++) {
+            int u0 = P.unit_level_ptr[l], u1 = P.unit_level_ptr[l + 1];
+            long ntask = 0, maxtask = 0; double flops = 0, crit = 0, sumcrit = 0;
+            for (int u = u0; u < u1; u++) {
+                long nt = P.task_ptr[u + 1] - P.task_ptr[u];
+                ntask += nt; if (nt > maxtask) maxtask = nt;
+                double thr[256] = {0};
+                for (int t = P.task_ptr[u]; t < P.task_ptr[u + 1]; t++) {
+                    const ipo::TailTask& tk = P.utasks[t];
+                    int d = tk.src; int ncd = P.col0[d + 1] - P.col0[d];
+                    int nr = __builtin_popcountll(tk.rmask), ncl = __builtin_popcountll(tk.cmask);
+                    flops += 2.0 * nr * ncl * ncd;
+                    for (int r = 0; r < 64; r++) if ((tk.rmask >> r) & 1)
+                        for (int g = 0; g < 4; g++) thr[r + 64 * g] += ncd * __builtin_popcountll((tk.cmask >> (16 * g)) & 0xFFFF);
+                }
+                double mx = 0; for (int i = 0; i < 256; i++) mx = std::max(mx, thr[i]);
+                crit = std::max(crit, mx); sumcrit += mx;
+            }
+            tot_crit += crit;
+            std::printf("L%2d units=%6d tasks=%8ld maxtasks=%6ld flops=%.3e crit=%.0f mean=%.0f\n", l, u1 - u0, ntask, maxtask, flops, crit, (u1 > u0) ? sumcrit / (u1 - u0) : 0.0);
+        }
+        std::printf("sum of per-level critical paths = %.0f fma steps\n", tot_crit);
+        double dense = 0, tot_maxk = 0; long totk = 0;
+        for (int l = 0; l < P.nlevels; l++) {
+            long mk = 0, sk = 0;
+            for (int u = P.unit_level_ptr[l]; u < P.unit_level_ptr[l + 1]; u++) {
+                long k = 0;
+                for (int t = P.task_ptr[u]; t < P.task_ptr[u + 1]; t++) { int d = P.utasks[t].src; k += P.col0[d + 1] - P.col0[d]; }
+                mk = std::max(mk, k); sk += k;
+            }
+            dense += 8192.0 * sk; tot_maxk += mk; totk += sk;
+            std::printf("L%2d sumK=%ld maxK=%ld\n", l, sk, mk);
+        }
+        std::printf("dense-equivalent flops %.3e, sum K %ld, sum of per-level max K %.0f\n", dense, totk, tot_maxk);
     }
     // print perm hash for comparison
     unsigned long long hsh = 1469598103934665603ull;
