@@ -112,10 +112,14 @@ class KktDevice {
     DevBuf<double> dA_, dAt_;
     // plan
     DevBuf<int> dcol0_, drowptr_, drows_, dperm_, diperm_;
-    DevBuf<int64_t> doff_, damap_, ddslot_, drelptr_, dfrow_pos_;
+    DevBuf<int64_t> doff_, damap_, ddslot_, drelptr_;
     DevBuf<int> dunit_sup_, dunit_tile_, dtask_ptr_, dtask_pair_, dtask_i0_, dtask_i1_;
     DevBuf<int> dupd_src_, dupd_r0_, dupd_r1_, drel_, dlevel_sups_;
-    DevBuf<int> dfrow_ptr_, dfrow_col_;
+    DevBuf<int> dyrow_ptr_, dyrow_idx_;
+    DevBuf<double> dYbuf_;
+    std::vector<int> chunk_ptr_;          // per level: solve chunks [chunk_ptr_[l], chunk_ptr_[l+1])
+    DevBuf<int> dchunk_sup_, dchunk_r0_, dsup_chunk0_;
+    DevBuf<double> dPartial_;    // backward partial sums, one 64-vector per chunk      // forward-sweep update values, one per row of every R_s
     DevBuf<int> dtail_task_ptr_, dkslot_, dkslot_ptr_, dtail_kslot_, dtail_kslot_ptr_;
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;

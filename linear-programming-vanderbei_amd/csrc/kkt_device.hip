@@ -436,201 +436,359 @@ k_tail_syrk(PlanView p, TailView tv, int kb) {
 }
 
 // -------------------------------------------------------------- solves
-// z (permuted) -> L^{-1} z, then D^{-1}, one level of supernodes per launch.
-__global__ void __launch_bounds__(NT)
-k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ frow_ptr,
-          const int* __restrict__ frow_col, const int64_t* __restrict__ frow_pos, double* __restrict__ z,
-          const double* __restrict__ epsp) {
-    __shared__ double zl[PC];
-    __shared__ double Ls[PC][PC + 1];     // Ls[r][j] = L11(r, j)
-    __shared__ int lv[PC];
-    const int s = level_sups[q0 + blockIdx.x];
-    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
-    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
-    const double* panel = p.Lx + p.off[s];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int r = wv; r < nc; r += 4) Ls[r][lane] = lane < r ? panel[lane + (size_t)r * h] : 0.0;
-    if (threadIdx.x < nc) lv[threadIdx.x] = p.live[c0 + threadIdx.x];
-    for (int k = wv; k < nc; k += 4) {
-        const int v = c0 + k;
-        double acc = 0.0;
-        for (int e = frow_ptr[v] + lane; e < frow_ptr[v + 1]; e += 64) acc += p.Lx[frow_pos[e]] * z[frow_col[e]];
-        acc = wave_sum(acc);
-        if (lane == 0) zl[k] = z[v] - acc;
-    }
-    __syncthreads();
-    if (wv != 0) return;
-    const double eps = *epsp;
-    double zr = lane < nc ? zl[lane] : 0.0;
-    int bad = 0;
+// value of v in lane j (j wave-uniform), via two v_readlane_b32
+__device__ __forceinline__ double lane_bcast(double v, int j) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(b), j);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), j);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
+// One wave solves a unit-lower nc x nc block in place: lane r holds z_r on
+// entry and on exit; Ls[r][j] = L(r, j).  A dropped column j (mark false)
+// keeps z_j when |z_j| > eps (and the system is flagged inconsistent), else
+// z_j = 0 -- ldlt.c:446-470.
+__device__ __forceinline__ double tri_lower(double zr, const double (*Ls)[PC + 1], const int* lv, int nc, double eps,
+                                            int& bad) {
+    const int lane = threadIdx.x & 63;
     for (int j = 0; j < nc; j++) {
         const int alive = lv[j];
         if (lane == j && !alive) {
             if (fabs(zr) > eps) bad = 1;
             else zr = 0.0;
         }
-        const double zj = __shfl(zr, j, 64);
+        const double zj = lane_bcast(zr, j);
         if (alive && lane > j && lane < nc) zr -= Ls[lane][j] * zj;
     }
-    if (lane < nc) z[c0 + lane] = zr;
-    if (bad) atomicOr(&p.flags[1], 1);
+    return zr;
 }
 
-// z -> L^{-T} z, top-down.
-__global__ void __launch_bounds__(NT)
-k_backward(PlanView p, const int* __restrict__ level_sups, int q0, double* __restrict__ z,
-           const double* __restrict__ epsp) {
-    __shared__ double zl[PC];
-    __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L11(j, r)
-    __shared__ int lv[PC];
-    const int s = level_sups[q0 + blockIdx.x];
-    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
-    const int hb = p.rowptr[s + 1] - p.rowptr[s];
-    const int h = nc + hb;
-    const double* panel = p.Lx + p.off[s];
-    const int* rows = p.rows + p.rowptr[s];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int j = wv; j < nc; j += 4) Ls[j][lane] = lane < j ? panel[lane + (size_t)j * h] : 0.0;
-    if (threadIdx.x < nc) lv[threadIdx.x] = p.live[c0 + threadIdx.x];
-    const double eps = *epsp;
-    int bad = 0;
-    for (int k = wv; k < nc; k += 4) {
-        const double* col = panel + (size_t)k * h + nc;
-        double acc = 0.0;
-        for (int i = lane; i < hb; i += 64) acc += col[i] * z[rows[i]];
-        acc = wave_sum(acc);
-        if (lane == 0) {
-            const int v = c0 + k;
-            double zv = z[v];
-            if (p.live[v]) zv = zv / p.dg[v];
-            else if (fabs(zv) > eps) bad = 1;
-            else zv = 0.0;
-            zl[k] = zv - acc;
-        }
-    }
-    if (bad) atomicOr(&p.flags[1], 1);
-    bad = 0;
-    __syncthreads();
-    if (wv != 0) return;
-    double zr = lane < nc ? zl[lane] : 0.0;
+// unit-upper (L11') counterpart; Ls[j][r] = L(j, r)
+__device__ __forceinline__ double tri_upper(double zr, const double (*Ls)[PC + 1], const int* lv, int nc, double eps,
+                                            int& bad) {
+    const int lane = threadIdx.x & 63;
     for (int j = nc - 1; j >= 0; j--) {
         const int alive = lv[j];
         if (lane == j && !alive) {
             if (fabs(zr) > eps) bad = 1;
             else zr = 0.0;
         }
-        const double zj = __shfl(zr, j, 64);
+        const double zj = lane_bcast(zr, j);
         if (alive && lane < j) zr -= Ls[j][lane] * zj;
     }
+    return zr;
+}
+
+// D^{-1} with the dropped-column rule (ldlt.c:473-480)
+__device__ __forceinline__ double dscale_rule(const PlanView& p, int v, double zv, double eps, int& bad) {
+    if (p.live[v]) return zv / p.dg[v];
+    if (fabs(zv) > eps) bad = 1;
+    else zv = 0.0;
+    return zv;
+}
+
+// Stage L11 of a panel (ld = h): rowform -> Ls[r][j] = L(r, j), else
+// Ls[j][r] = L(j, r); both read the upper-triangle slot image (j, r).
+__device__ __forceinline__ void stage_l11(const double* panel, size_t ld, int nc, double (*Ls)[PC + 1]) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int r = wv; r < nc; r += nw) Ls[r][lane] = lane < r ? panel[lane + (size_t)r * ld] : 0.0;
+}
+
+// Forward, diagonal part of supernode s: subtract the y values of solved
+// descendants from its rows, solve L11.  Leaves z_s in zl and in z.
+// 4 threads per row; partial sums combined as (p0 + p1) + (p2 + p3).
+__device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
+                         const double* __restrict__ ybuf, double* __restrict__ z, double eps, double* zl,
+                         double (*Ls)[PC + 1], int* lv) {
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    stage_l11(p.Lx + p.off[s], h, nc, Ls);
+    if (tid < nc) lv[tid] = p.live[c0 + tid];
+    for (int base = 0; base < nc; base += blockDim.x >> 2) {
+        const int k = base + (tid >> 2), part = tid & 3;
+        double acc = 0.0;
+        if (k < nc) {
+            const int v = c0 + k;
+            for (int e = yrow_ptr[v] + part; e < yrow_ptr[v + 1]; e += 4) acc += ybuf[yrow_idx[e]];
+        }
+        const double o1 = __shfl_xor(acc, 1, 64);
+        const double pr = (part & 1) ? o1 + acc : acc + o1;
+        const double o2 = __shfl_xor(pr, 2, 64);
+        const double tot = (part & 2) ? o2 + pr : pr + o2;
+        if (part == 0 && k < nc) zl[k] = z[c0 + k] - tot;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        int bad = 0;
+        const double zr = tri_lower(lane < nc ? zl[lane] : 0.0, Ls, lv, nc, eps, bad);
+        if (lane < nc) { z[c0 + lane] = zr; zl[lane] = zr; }
+        if (bad) atomicOr(&p.flags[1], 1);
+    }
+    __syncthreads();
+}
+
+// Forward, one level of small supernodes per launch, one workgroup each:
+// diagonal part, then y_s = L21 z_s for the ancestors (one row per thread).
+// D^{-1} is applied at the start of the backward sweep.
+__global__ void __launch_bounds__(NT)
+k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ yrow_ptr,
+          const int* __restrict__ yrow_idx, double* __restrict__ ybuf, double* __restrict__ z,
+          const double* __restrict__ epsp) {
+    __shared__ double zl[PC];
+    __shared__ double Ls[PC][PC + 1];
+    __shared__ int lv[PC];
+    const int s = level_sups[q0 + blockIdx.x];
+    fwd_diag(p, s, yrow_ptr, yrow_idx, ybuf, z, *epsp, zl, Ls, lv);
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
+    const double* panel = p.Lx + p.off[s];
+    double* __restrict__ y = ybuf + p.rowptr[s];
+    for (int i = threadIdx.x; i < hb; i += NT) {
+        const double* __restrict__ row = panel + nc + i;
+        double acc = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < nc; k++) acc += row[(size_t)k * h] * zl[k];
+        y[i] = acc;
+    }
+}
+
+// Forward for levels with large panels, part 1: diagonal parts only.
+__global__ void __launch_bounds__(NT)
+k_fwd_diag(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ yrow_ptr,
+           const int* __restrict__ yrow_idx, const double* __restrict__ ybuf, double* __restrict__ z,
+           const double* __restrict__ epsp) {
+    __shared__ double zl[PC];
+    __shared__ double Ls[PC][PC + 1];
+    __shared__ int lv[PC];
+    fwd_diag(p, level_sups[q0 + blockIdx.x], yrow_ptr, yrow_idx, ybuf, z, *epsp, zl, Ls, lv);
+}
+
+// part 2: y = L21 z_s over one 64-row chunk of R_s; wave w takes columns
+// 16w..16w+15, the four partial sums are added in wave order.
+__global__ void __launch_bounds__(NT)
+k_fwd_gemv(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict__ chunk_r0, int cb,
+           double* __restrict__ ybuf, const double* __restrict__ z) {
+    __shared__ double zs[PC];
+    __shared__ double red[4][64];
+    const int c = cb + blockIdx.x;
+    const int s = chunk_sup[c], r0 = chunk_r0[c];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid < nc) zs[tid] = z[c0 + tid];
+    __syncthreads();
+    const int i = r0 + lane, kq = wv * 16, nq = min(16, nc - kq);
+    double acc = 0.0;
+    if (i < hb && nq > 0) {
+        const double* __restrict__ row = p.Lx + p.off[s] + nc + i + (size_t)kq * h;
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+            if (q < nq) acc += row[(size_t)q * h] * zs[kq + q];
+    }
+    red[wv][lane] = acc;
+    __syncthreads();
+    if (wv == 0 && i < hb) ybuf[p.rowptr[s] + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+// Backward, one level of small supernodes per launch, one workgroup each:
+// z_s = D^{-1} z_s - L21' z_R, then L11'.  Wave w owns columns 16w..16w+15,
+// lanes stride the rows (coalesced column reads).
+__global__ void __launch_bounds__(NT)
+k_backward(PlanView p, const int* __restrict__ level_sups, int q0, double* __restrict__ z,
+           const double* __restrict__ epsp) {
+    __shared__ double xs[PC];
+    __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L(j, r)
+    __shared__ int lv[PC];
+    const int s = level_sups[q0 + blockIdx.x];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int hb = p.rowptr[s + 1] - p.rowptr[s];
+    const int h = nc + hb;
+    const double* panel = p.Lx + p.off[s];
+    const int* __restrict__ rows = p.rows + p.rowptr[s];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    stage_l11(panel, h, nc, Ls);
+    if (tid < nc) lv[tid] = p.live[c0 + tid];
+    const int kq = wv * 16, nq = min(16, nc - kq);
+    if (nq > 0) {
+        double acc[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc[q] = 0.0;
+        for (int i = lane; i < hb; i += 64) {
+            const double zi = z[rows[i]];
+            const double* __restrict__ col = panel + nc + i + (size_t)kq * h;
+#pragma unroll
+            for (int q = 0; q < 16; q++)
+                if (q < nq) acc[q] += col[(size_t)q * h] * zi;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const double t = wave_sum(acc[q]);
+            if (lane == 0 && q < nq) xs[kq + q] = t;
+        }
+    }
+    __syncthreads();
+    if (wv != 0) return;
+    const double eps = *epsp;
+    int bad = 0;
+    double zr = 0.0;
+    if (lane < nc) zr = dscale_rule(p, c0 + lane, z[c0 + lane], eps, bad) - xs[lane];
+    zr = tri_upper(zr, Ls, lv, nc, eps, bad);
+    if (lane < nc) z[c0 + lane] = zr;
+    if (bad) atomicOr(&p.flags[1], 1);
+}
+
+// Backward for levels with large panels, part 1: per 64-row chunk of R_s,
+// part[c][k] = sum over the chunk's rows of L(row, k) z_row.
+__global__ void __launch_bounds__(NT)
+k_bwd_partial(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict__ chunk_r0, int cb,
+              const double* __restrict__ z, double* __restrict__ part) {
+    const int c = cb + blockIdx.x;
+    const int s = chunk_sup[c], r0 = chunk_r0[c];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int kq = wv * 16, nq = min(16, nc - kq);
+    if (nq <= 0) return;
+    const int i = r0 + lane;
+    const double zi = i < hb ? z[p.rows[p.rowptr[s] + i]] : 0.0;
+    const double* __restrict__ col = p.Lx + p.off[s] + nc + i + (size_t)kq * h;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const double t = wave_sum((i < hb && q < nq) ? col[(size_t)q * h] * zi : 0.0);
+        if (lane == 0 && q < nq) part[(size_t)c * PC + kq + q] = t;
+    }
+}
+
+// part 2: one wave per supernode sums its chunks in order, then D^{-1} and L11'.
+__global__ void __launch_bounds__(64)
+k_bwd_finish(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ sup_chunk0,
+             const double* __restrict__ part, double* __restrict__ z, const double* __restrict__ epsp) {
+    __shared__ double Ls[PC][PC + 1];
+    __shared__ int lv[PC];
+    const int s = level_sups[q0 + blockIdx.x];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
+    const int lane = threadIdx.x;
+    stage_l11(p.Lx + p.off[s], h, nc, Ls);
+    if (lane < nc) lv[lane] = p.live[c0 + lane];
+    __syncthreads();
+    const double eps = *epsp;
+    int bad = 0;
+    double zr = 0.0;
+    if (lane < nc) {
+        const int cf = sup_chunk0[s], nch = (hb + 63) / 64;
+        double x = 0.0;
+        for (int c = 0; c < nch; c++) x += part[(size_t)(cf + c) * PC + lane];
+        zr = dscale_rule(p, c0 + lane, z[c0 + lane], eps, bad) - x;
+    }
+    zr = tri_upper(zr, Ls, lv, nc, eps, bad);
     if (lane < nc) z[c0 + lane] = zr;
     if (bad) atomicOr(&p.flags[1], 1);
 }
 
 // ---------------------------------------------------- dense-tail solves
-// forward, part 1: tail rows gather the sparse panels' contributions
+// forward, part 1: tail rows subtract the y values the sparse panels left
 __global__ void __launch_bounds__(NT)
-k_tail_gather(PlanView p, TailView tv, const int* __restrict__ frow_ptr, const int* __restrict__ frow_col,
-              const int64_t* __restrict__ frow_pos, double* __restrict__ z) {
+k_tail_gather(TailView tv, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
+              const double* __restrict__ ybuf, double* __restrict__ z) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int i = blockIdx.x * 4 + wv;
     if (i >= tv.nt) return;
     const int v = tv.tc + i;
     double acc = 0.0;
-    for (int e = frow_ptr[v] + lane; e < frow_ptr[v + 1]; e += 64) acc += p.Lx[frow_pos[e]] * z[frow_col[e]];
+    for (int e = yrow_ptr[v] + lane; e < yrow_ptr[v + 1]; e += 64) acc += ybuf[yrow_idx[e]];
     acc = wave_sum(acc);
     if (lane == 0) z[v] = z[v] - acc;
 }
 
-constexpr int NTB = 1024;   // one workgroup sweeps the dense tail
-
-// forward, part 2: blocked unit-lower solve of the dense tail (one workgroup)
-__global__ void __launch_bounds__(NTB)
-k_tail_fwd(PlanView p, TailView tv, double* __restrict__ z, const double* __restrict__ epsp) {
-    __shared__ double Ls[PC][PC + 1];     // Ls[r][j] = L11(r, j) of the current block
+// forward, part 2, block kb of the dense tail: every workgroup solves the
+// block's L11 in wave 0 (identical arithmetic, identical results; workgroup
+// 0 stores it), then updates 64 rows below it, z_r -= L(r, block) zb: lane
+// = row, wave w takes columns 16w..16w+15, partials added in wave order.
+__global__ void __launch_bounds__(NT)
+k_tail_fwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double* __restrict__ epsp) {
+    __shared__ double Ls[PC][PC + 1];
     __shared__ double zb[PC];
     __shared__ int lv[PC];
-    const int nt = tv.nt, tc = tv.tc;
+    __shared__ double red[4][64];
+    const int nt = tv.nt, tc = tv.tc, k0 = kb * PC, nc = min(PC, nt - k0);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const double eps = *epsp;
-    int bad = 0;
-    for (int kb = 0; kb < tv.ntb; kb++) {
-        const int k0 = kb * PC, nc = min(PC, nt - k0);
-        for (int r = wv; r < nc; r += NTB / 64)
-            Ls[r][lane] = lane < r ? tv.S[(k0 + lane) + (size_t)(k0 + r) * nt] : 0.0;
-        if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
-        __syncthreads();
-        if (wv == 0) {
-            double zr = lane < nc ? z[tc + k0 + lane] : 0.0;
-            for (int j = 0; j < nc; j++) {
-                const int alive = lv[j];
-                if (lane == j && !alive) {
-                    if (fabs(zr) > eps) bad = 1;
-                    else zr = 0.0;
-                }
-                const double zj = __shfl(zr, j, 64);
-                if (alive && lane > j && lane < nc) zr -= Ls[lane][j] * zj;
-            }
-            if (lane < nc) { z[tc + k0 + lane] = zr; zb[lane] = zr; }
+    const double* blk = tv.S + k0 + (size_t)k0 * nt;
+    stage_l11(blk, nt, nc, Ls);
+    if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
+    __syncthreads();
+    if (wv == 0) {
+        int bad = 0;
+        const double zr = tri_lower(lane < nc ? z[tc + k0 + lane] : 0.0, Ls, lv, nc, *epsp, bad);
+        if (lane < nc) zb[lane] = zr;
+        if (blockIdx.x == 0) {
+            if (lane < nc) z[tc + k0 + lane] = zr;
+            if (bad) atomicOr(&p.flags[1], 1);
         }
-        __syncthreads();
-        for (int r = k0 + nc + tid; r < nt; r += NTB) {
-            double acc = 0.0;
-            for (int k = 0; k < nc; k++) acc += tv.S[r + (size_t)(k0 + k) * nt] * zb[k];
-            z[tc + r] = z[tc + r] - acc;
-        }
-        __syncthreads();
     }
+    __syncthreads();
+    const int r = k0 + nc + blockIdx.x * 64 + lane;
+    const int kq = wv * 16, nq = min(16, nc - kq);
+    double acc = 0.0;
+    if (r < nt && nq > 0) {
+        const double* __restrict__ row = tv.S + r + (size_t)(k0 + kq) * nt;
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+            if (q < nq) acc += row[(size_t)q * nt] * zb[kq + q];
+    }
+    red[wv][lane] = acc;
+    __syncthreads();
+    if (wv == 0 && r < nt) z[tc + r] = z[tc + r] - (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+}
+
+// backward, part 1: D^{-1} on the tail with the dropped-column rule
+__global__ void __launch_bounds__(NT)
+k_tail_dscale(PlanView p, TailView tv, double* __restrict__ z, const double* __restrict__ epsp) {
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (i >= tv.nt) return;
+    const int v = tv.tc + i;
+    int bad = 0;
+    z[v] = dscale_rule(p, v, z[v], *epsp, bad);
     if (bad) atomicOr(&p.flags[1], 1);
 }
 
-// backward: D^{-1} on the tail, then blocked L^{-T} (one workgroup)
-__global__ void __launch_bounds__(NTB)
-k_tail_bwd(PlanView p, TailView tv, double* __restrict__ z, const double* __restrict__ epsp) {
-    __shared__ double zl[PC];
-    __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L11(j, r) of the current block
+// backward, part 2, block kb: L11' solve (every workgroup, workgroup 0
+// stores), then 64 columns j < k0 left of it: z_j -= sum_k L(k0 + k, j) zb_k;
+// lane = column, wave w takes k = 16w..16w+15, partials added in wave order.
+__global__ void __launch_bounds__(NT)
+k_tail_bwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double* __restrict__ epsp) {
+    __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L(j, r)
+    __shared__ double zb[PC];
     __shared__ int lv[PC];
-    const int nt = tv.nt, tc = tv.tc;
+    __shared__ double red[4][64];
+    const int nt = tv.nt, tc = tv.tc, k0 = kb * PC, nc = min(PC, nt - k0);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const double eps = *epsp;
-    int bad = 0;
-    for (int i = tid; i < nt; i += NTB) {
-        const int v = tc + i;
-        double zv = z[v];
-        if (p.live[v]) zv = zv / p.dg[v];
-        else if (fabs(zv) > eps) bad = 1;
-        else zv = 0.0;
-        z[v] = zv;
+    stage_l11(tv.S + k0 + (size_t)k0 * nt, nt, nc, Ls);
+    if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
+    __syncthreads();
+    if (wv == 0) {
+        int bad = 0;
+        const double zr = tri_upper(lane < nc ? z[tc + k0 + lane] : 0.0, Ls, lv, nc, *epsp, bad);
+        if (lane < nc) zb[lane] = zr;
+        if (blockIdx.x == 0) {
+            if (lane < nc) z[tc + k0 + lane] = zr;
+            if (bad) atomicOr(&p.flags[1], 1);
+        }
     }
     __syncthreads();
-    for (int kb = tv.ntb - 1; kb >= 0; kb--) {
-        const int k0 = kb * PC, nc = min(PC, nt - k0);
-        for (int j = wv; j < nc; j += NTB / 64)
-            Ls[j][lane] = lane < j ? tv.S[(k0 + lane) + (size_t)(k0 + j) * nt] : 0.0;
-        if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
-        for (int k = wv; k < nc; k += NTB / 64) {
-            const double* col = tv.S + (size_t)(k0 + k) * nt;
-            double acc = 0.0;
-            for (int r = k0 + nc + lane; r < nt; r += 64) acc += col[r] * z[tc + r];
-            acc = wave_sum(acc);
-            if (lane == 0) zl[k] = z[tc + k0 + k] - acc;
-        }
-        __syncthreads();
-        if (wv == 0) {
-            double zr = lane < nc ? zl[lane] : 0.0;
-            for (int j = nc - 1; j >= 0; j--) {
-                const int alive = lv[j];
-                if (lane == j && !alive) {
-                    if (fabs(zr) > eps) bad = 1;
-                    else zr = 0.0;
-                }
-                const double zj = __shfl(zr, j, 64);
-                if (alive && lane < j) zr -= Ls[j][lane] * zj;
-            }
-            if (lane < nc) z[tc + k0 + lane] = zr;
-        }
-        __syncthreads();
+    const int j = blockIdx.x * 64 + lane;
+    const int kq = wv * 16, nq = min(16, nc - kq);
+    double acc = 0.0;
+    if (j < k0 && nq > 0) {
+        const double* __restrict__ col = tv.S + (k0 + kq) + (size_t)j * nt;
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+            if (q < nq) acc += col[q] * zb[kq + q];
     }
-    if (bad) atomicOr(&p.flags[1], 1);
+    red[wv][lane] = acc;
+    __syncthreads();
+    if (wv == 0 && j < k0) z[tc + j] = z[tc + j] - (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
 }
 
 // -------------------------------------------------------- refinement glue
@@ -728,7 +886,6 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     damap_.upload(plan_.amap, s);
     ddslot_.upload(plan_.dslot, s);
     drelptr_.upload(plan_.relptr, s);
-    dfrow_pos_.upload(plan_.frow_pos, s);
     dunit_sup_.upload(plan_.unit_sup, s);
     dunit_tile_.upload(plan_.unit_tile, s);
     dtask_ptr_.upload(plan_.task_ptr, s);
@@ -740,8 +897,34 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dupd_r1_.upload(plan_.upd_r1, s);
     drel_.upload(plan_.rel, s);
     dlevel_sups_.upload(plan_.level_sups, s);
-    dfrow_ptr_.upload(plan_.frow_ptr, s);
-    dfrow_col_.upload(plan_.frow_col, s);
+    {   // solve chunks: levels holding a panel with more than kChunkRows rows below
+        // its diagonal block are solved in 64-row chunks (two launches each way)
+        constexpr int kChunkRows = 128;
+        std::vector<int> csup, cr0, chunk0(plan_.nsup, -1);
+        chunk_ptr_.assign(plan_.nlevels + 1, 0);
+        for (int l = 0; l < plan_.nlevels; l++) {
+            bool big = false;
+            for (int q = plan_.level_ptr[l]; q < plan_.level_ptr[l + 1]; q++) {
+                const int sp = plan_.level_sups[q];
+                big |= plan_.rowptr[sp + 1] - plan_.rowptr[sp] > kChunkRows;
+            }
+            if (big)
+                for (int q = plan_.level_ptr[l]; q < plan_.level_ptr[l + 1]; q++) {
+                    const int sp = plan_.level_sups[q], hb = plan_.rowptr[sp + 1] - plan_.rowptr[sp];
+                    chunk0[sp] = static_cast<int>(csup.size());
+                    for (int r0 = 0; r0 < hb; r0 += 64) { csup.push_back(sp); cr0.push_back(r0); }
+                }
+            chunk_ptr_[l + 1] = static_cast<int>(csup.size());
+        }
+        dchunk_sup_.upload(csup, s);
+        dchunk_r0_.upload(cr0, s);
+        dsup_chunk0_.upload(chunk0, s);
+        dPartial_.alloc(csup.empty() ? 1 : csup.size() * kPanelCols);
+        IPO_HIP_CHECK(hipStreamSynchronize(s));   // csup / cr0 / chunk0 are stack vectors
+    }
+    dyrow_ptr_.upload(plan_.yrow_ptr, s);
+    dyrow_idx_.upload(plan_.yrow_idx, s);
+    dYbuf_.alloc(plan_.rowptr.back() > 0 ? plan_.rowptr.back() : 1);
     dkslot_.upload(plan_.kslot, s);
     dkslot_ptr_.upload(plan_.kslot_ptr, s);
     dutasks_.upload(reinterpret_cast<const uint64_t*>(plan_.utasks.data()), plan_.utasks.size() * 4, s);
@@ -929,19 +1112,43 @@ void KktDevice::rawsolve(double* dz) {
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev2_, s));
     for (int l = 0; l < plan_.nlevels; l++) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
-        hipLaunchKernelGGL(k_forward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dfrow_ptr_.get(),
-                           dfrow_col_.get(), dfrow_pos_.get(), dz, epsp);
+        const int cb = chunk_ptr_[l], ce = chunk_ptr_[l + 1];
+        if (ce > cb) {
+            hipLaunchKernelGGL(k_fwd_diag, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dyrow_ptr_.get(),
+                               dyrow_idx_.get(), dYbuf_.get(), dz, epsp);
+            hipLaunchKernelGGL(k_fwd_gemv, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(), cb,
+                               dYbuf_.get(), dz);
+        } else {
+            hipLaunchKernelGGL(k_forward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dyrow_ptr_.get(),
+                               dyrow_idx_.get(), dYbuf_.get(), dz, epsp);
+        }
     }
     if (plan_.nt > 0) {
         const TailView tv = tail_view();
-        hipLaunchKernelGGL(k_tail_gather, dim3(ceil_div(plan_.nt, 4)), dim3(NT), 0, s, pv, tv, dfrow_ptr_.get(),
-                           dfrow_col_.get(), dfrow_pos_.get(), dz);
-        hipLaunchKernelGGL(k_tail_fwd, dim3(1), dim3(NTB), 0, s, pv, tv, dz, epsp);
-        hipLaunchKernelGGL(k_tail_bwd, dim3(1), dim3(NTB), 0, s, pv, tv, dz, epsp);
+        const int nt = plan_.nt;
+        hipLaunchKernelGGL(k_tail_gather, dim3(ceil_div(nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(), dyrow_idx_.get(),
+                           dYbuf_.get(), dz);
+        for (int kb = 0; kb < plan_.ntb; kb++) {
+            const int below = nt - std::min(nt, (kb + 1) * kPanelCols);
+            hipLaunchKernelGGL(k_tail_fwd, dim3(std::max(1, ceil_div(below, 64))), dim3(NT), 0, s, pv, tv, kb, dz, epsp);
+        }
+        hipLaunchKernelGGL(k_tail_dscale, dim3(ceil_div(nt, NT)), dim3(NT), 0, s, pv, tv, dz, epsp);
+        for (int kb = plan_.ntb - 1; kb >= 0; kb--) {
+            const int left = kb * kPanelCols;
+            hipLaunchKernelGGL(k_tail_bwd, dim3(std::max(1, ceil_div(left, 64))), dim3(NT), 0, s, pv, tv, kb, dz, epsp);
+        }
     }
     for (int l = plan_.nlevels - 1; l >= 0; l--) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
-        hipLaunchKernelGGL(k_backward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dz, epsp);
+        const int cb = chunk_ptr_[l], ce = chunk_ptr_[l + 1];
+        if (ce > cb) {
+            hipLaunchKernelGGL(k_bwd_partial, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(), cb,
+                               dz, dPartial_.get());
+            hipLaunchKernelGGL(k_bwd_finish, dim3(q1 - q0), dim3(64), 0, s, pv, dlevel_sups_.get(), q0,
+                               dsup_chunk0_.get(), dPartial_.get(), dz, epsp);
+        } else {
+            hipLaunchKernelGGL(k_backward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dz, epsp);
+        }
     }
     IPO_HIP_CHECK(hipGetLastError());
     if (timing_) {

@@ -108,11 +108,12 @@ struct KktPlan {
     //  list padded to a multiple of kSlab.
     std::vector<int> kslot, kslot_ptr;            // per factor unit
     std::vector<int> tail_kslot, tail_kslot_ptr;  // per tail tile
-    //  forward-solve row lists: for row v, the L entries (v, col) whose column
-    //  lies in another supernode: Lx slot and column.
-    std::vector<int> frow_ptr;         // [T+1]
-    std::vector<int> frow_col;
-    std::vector<int64_t> frow_pos;
+    //  forward-solve update lists.  After supernode s is solved, the forward
+    //  sweep stores y_s = L21_s z_s in ybuf[rowptr[s] .. rowptr[s+1]) (one
+    //  value per row of R_s); row v later subtracts every y entry aimed at
+    //  it: ybuf[yrow_idx[yrow_ptr[v] .. yrow_ptr[v+1])], ascending s.
+    std::vector<int> yrow_ptr;         // [T+1]
+    std::vector<int> yrow_idx;
 
     // reference statistics
     int64_t lnz = 0;                // nnz strict lower L (reference pattern)

@@ -459,29 +459,14 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
         if (P.nt > 0) build(P.tail_task_ptr, P.tail_tasks, P.tail_kslot, P.tail_kslot_ptr);
     }
 
-    // ---- forward-solve row lists (entries of sparse panels, by row)
+    // ---- forward-solve update lists (rows of every sparse panel, by row)
     {
-        P.frow_ptr.assign(T + 1, 0);
-        for (int d = 0; d < ns; d++) {
-            const int nc = P.col0[d + 1] - P.col0[d];
-            for (int i = P.rowptr[d]; i < P.rowptr[d + 1]; i++) P.frow_ptr[P.rows[i] + 1] += nc;
-        }
-        for (int v = 0; v < T; v++) P.frow_ptr[v + 1] += P.frow_ptr[v];
-        P.frow_col.resize(P.frow_ptr[T]);
-        P.frow_pos.resize(P.frow_ptr[T]);
-        std::vector<int> fill(P.frow_ptr.begin(), P.frow_ptr.end() - 1);
-        for (int d = 0; d < ns; d++) {
-            const int nc = P.col0[d + 1] - P.col0[d];
-            const int hb = P.rowptr[d + 1] - P.rowptr[d];
-            const int h = nc + hb;
-            for (int k = 0; k < nc; k++)
-                for (int i = 0; i < hb; i++) {
-                    const int row = P.rows[P.rowptr[d] + i];
-                    const int e = fill[row]++;
-                    P.frow_col[e] = P.col0[d] + k;
-                    P.frow_pos[e] = P.off[d] + static_cast<int64_t>(k) * h + nc + i;
-                }
-        }
+        P.yrow_ptr.assign(T + 1, 0);
+        for (int i = 0; i < P.rowptr[ns]; i++) P.yrow_ptr[P.rows[i] + 1]++;
+        for (int v = 0; v < T; v++) P.yrow_ptr[v + 1] += P.yrow_ptr[v];
+        P.yrow_idx.resize(P.yrow_ptr[T]);
+        std::vector<int> fill(P.yrow_ptr.begin(), P.yrow_ptr.end() - 1);
+        for (int i = 0; i < P.rowptr[ns]; i++) P.yrow_idx[fill[P.rows[i]]++] = i;
     }
 
     for (int s = 0; s < ns; s++) {
