@@ -1,0 +1,296 @@
+// kkt_dense.hip -- dense per-panel kernels of the supernodal LDL':
+// diagonal-block factorisation (register fast path + the dependent-pivot
+// path of ldlt.c:600-614) and the panel triangular solve L21 = A21 L11^-T D^-1.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "dev_common.h"
+#include "kkt_kernels.h"
+
+namespace ipo {
+
+namespace {
+
+constexpr int TR = kTileRows;     // 64
+constexpr int PC = kPanelCols;    // 64
+constexpr int NT = 256;
+
+// Thread (row r = lane, part q0 = wave) of a 256-thread workgroup keeps
+// the entries (r, 4q + q0), q = 0..15, of a 64-column row in registers.
+// Column k = 4 qk + pk is visited with qk unrolled (a static register
+// index) and pk a runtime loop, which keeps the code small: the dependency
+// chain, not the flops, bounds these kernels, and a fully unrolled 64 x 64
+// body does not fit the instruction cache.
+// Fast path of the diagonal-block LDL' (256 threads, layout above).  Same
+// operations in the same order as factor_diag_block below (bitwise
+// identical results); returns false -- having written nothing -- as soon as
+// a pivot fails the zero test, and the caller reruns the block with
+// factor_diag_block, which owns the dependent-pivot rule (ldlt.c:600-614).
+// On success stores L11' in the block's upper triangle, D in dg, mark = 1.
+__device__ __forceinline__ bool factor_diag_fast(const PlanView& p, double* panel, int ld, int nc, int c0,
+                                                 double (*B)[PC + 1]) {
+    __shared__ double colk[PC];
+    __shared__ double piv[2];
+    __shared__ double dv[PC];
+    const int tid = threadIdx.x, r = tid & 63, q0 = tid >> 6;
+    double a[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int c = 4 * q + q0;
+        const bool ok = r < nc && c <= r;
+        const double t = panel[ok ? r + (size_t)c * ld : 0];
+        a[q] = ok ? t : 0.0;
+    }
+    double dsc = (r < nc && (r & 3) == q0) ? p.dscale[c0 + r] : 0.0;   // kept by the diagonal's owner
+    // k = 4 qk + pk: qk unrolled (static register index), pk a runtime loop
+    bool tiny = false;
+#pragma unroll
+    for (int qk = 0; qk < 16; qk++) {
+        for (int pk = 0; pk < 4; pk++) {
+            const int k = 4 * qk + pk;
+            if (k >= nc || tiny) break;
+            if (r == k && q0 == pk) { piv[0] = a[qk]; piv[1] = dsc; }
+            __syncthreads();
+            const double dk = piv[0];
+            if (fabs(dk) <= p.tau * piv[1]) { tiny = true; break; }      // uniform
+            if (tid == 0) dv[k] = dk;
+            if (q0 == pk && r > k && r < nc) {
+                const double l = a[qk] / dk;
+                a[qk] = l;
+                colk[r] = l;
+            }
+            __syncthreads();
+            if (r > k && r < nc) {
+                const double lr = colk[r];
+#pragma unroll
+                for (int q = qk; q < 16; q++) {
+                    const int c = 4 * q + q0;
+                    if (c > k && c <= r) {
+                        const double tk = lr * (colk[c] * dk);
+                        a[q] -= tk;
+                        if (c == r) dsc += fabs(tk);
+                    }
+                }
+            }
+        }
+    }
+    if (tiny) return false;
+    __syncthreads();
+    // L11(r, c) -> upper slot (c, r) through an LDS transpose
+#pragma unroll
+    for (int q = 0; q < 16; q++) B[r][4 * q + q0] = a[q];
+    __syncthreads();
+    for (int rr = q0; rr < nc; rr += 4)
+        if (r < rr) panel[r + (size_t)rr * ld] = B[rr][r];
+    if (tid < nc) { p.dg[c0 + tid] = dv[tid]; p.live[c0 + tid] = 1; }
+    return true;
+}
+
+__device__ __attribute__((noinline)) void factor_diag_block(const PlanView& p, double* panel, int ld, int nc, int h, int c0) {
+    __shared__ double B[PC][PC + 1];
+    __shared__ double dv[PC];
+    __shared__ int lv[PC];
+    __shared__ double dsc[PC];
+    __shared__ double red[4];
+    __shared__ int ndep_sh;
+    const int tid = threadIdx.x, nthr = blockDim.x, np = nthr >> 6;
+    const int tr = tid & 63, tp = tid >> 6;     // row, part (np parts stride the columns)
+    for (int c = tp; c < nc; c += np) B[tr][c] = (tr < nc && tr >= c) ? panel[tr + (size_t)c * ld] : 0.0;
+    for (int k = tid; k < nc; k += nthr) dsc[k] = p.dscale[c0 + k];
+    if (tid == 0) ndep_sh = 0;
+    __syncthreads();
+    for (int k = 0; k < nc; k++) {
+        double dk = B[k][k];
+        int alive = 1;
+        if (fabs(dk) <= p.tau * dsc[k]) {         // ldlt.c:600 with a rounding-aware zero test
+            // largest off-diagonal magnitude of column k after every update
+            // from columns < k; rows below the block are rebuilt from the
+            // (not yet solved) panel by a partial forward substitution
+            double mx = 0.0;
+            for (int r = k + 1 + tid; r < nc; r += nthr) mx = ref_max(mx, ref_abs(B[r][k]));
+            for (int rr = nc + tid; rr < h; rr += nthr) {
+                double w[PC];
+                for (int c = 0; c <= k; c++) w[c] = panel[rr + (size_t)c * ld];
+                for (int j = 0; j < k; j++) {
+                    const double lj = lv[j] ? w[j] / dv[j] : 0.0;
+                    for (int c = j + 1; c <= k; c++) w[c] -= lj * (B[c][j] * dv[j]);
+                }
+                mx = ref_max(mx, ref_abs(w[k]));
+            }
+            mx = wave_max(mx);
+            if (tr == 0) red[tp] = mx;
+            __syncthreads();
+            if (tid == 0) {
+                double m2 = red[0];
+                for (int q = 1; q < np; q++) m2 = ref_max(m2, red[q]);
+                red[0] = m2;
+            }
+            __syncthreads();
+            mx = red[0];
+            if (mx < 1.0e+6 * 1.0e-8) alive = 0;                    // column dropped, d keeps its value
+            else dk = (p.sign[c0 + k] < 0 ? -1.0 : 1.0) * 1.0e-8;   // y-nodes -, x-nodes +
+            if (tid == 0) ndep_sh++;
+            __syncthreads();
+        }
+        if (tid == 0) { dv[k] = dk; lv[k] = alive; }
+        // scale column k first (lij = a / d), then update with lij * (ljk * d)
+        for (int r = k + 1 + tid; r < nc; r += nthr) B[r][k] = alive ? B[r][k] / dk : 0.0;
+        __syncthreads();
+        if (alive && tr > k && tr < nc) {
+            const double lr = B[tr][k];
+            for (int c = k + 1 + tp; c <= tr; c += np) {
+                const double tk = lr * (B[c][k] * dk);
+                B[tr][c] -= tk;
+                if (tr == c) dsc[c] += fabs(tk);
+            }
+        }
+        __syncthreads();
+    }
+    // L11(r, c) -> upper slot (c, r): thread tr writes row c = tr of the slot image
+    for (int r = tp; r < nc; r += np)
+        if (tr < r) panel[tr + (size_t)r * ld] = B[r][tr];
+    for (int k = tid; k < nc; k += nthr) { p.dg[c0 + k] = dv[k]; p.live[c0 + k] = lv[k]; }
+    if (tid == 0 && ndep_sh) atomicAdd(&p.flags[0], ndep_sh);
+}
+
+
+// ------------------------------------------------------- L21 = A21 L11^-T D^-1
+// Rows [rlo, rhi) (at most 64) of a panel (ld, nc columns starting at global
+// column c0), against the factored diagonal block (L11' in its upper
+// triangle); 256 threads, row r = lane, columns 4q + wave in registers.
+// Bl(c, k) = L11(c, k) d_k in LDS.  With wbuf != nullptr also writes
+// W = L21 D (ldw, rows relative to wrow0) for the dense tail's trailing
+// update.  Reference form: l = w / d, w -= l * (l11 * d).
+__device__ void solve_rows(const PlanView& p, double* panel, int ld, int nc, int c0, int rlo, int rhi,
+                           double* wbuf, int ldw, int wrow0) {
+    __shared__ double Bl[PC][PC + 1];     // Bl[c][k] = L11(c, k) * d_k
+    __shared__ double dv[PC];
+    __shared__ int lv[PC];
+    __shared__ double lk[64];
+    const int tid = threadIdx.x, r = tid & 63, q0 = tid >> 6;
+    for (int k = tid; k < nc; k += NT) { dv[k] = p.dg[c0 + k]; lv[k] = p.live[c0 + k]; }
+    __syncthreads();
+    for (int idx = tid; idx < PC * PC; idx += NT) {
+        const int k = idx & 63, c = idx >> 6;        // slot (k, c) holds L11(c, k)
+        Bl[c][k] = (k < c && c < nc) ? panel[k + (size_t)c * ld] * dv[k] : 0.0;
+    }
+    const int row = rlo + r;
+    const bool okr = row < rhi;
+    double a[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int c = 4 * q + q0;
+        const bool ok = okr && c < nc;
+        const double t = panel[ok ? row + (size_t)c * ld : 0];
+        a[q] = ok ? t : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int qk = 0; qk < 16; qk++) {
+        for (int pk = 0; pk < 4; pk++) {
+            const int k = 4 * qk + pk;
+            if (k >= nc) break;
+            if (q0 == pk) {
+                const double l = lv[k] ? a[qk] / dv[k] : 0.0;
+                a[qk] = l;
+                lk[r] = l;
+            }
+            __syncthreads();
+            const double l = lk[r];
+#pragma unroll
+            for (int q = qk; q < 16; q++) {
+                const int c = 4 * q + q0;
+                if (c > k) a[q] -= l * Bl[c][k];          // Bl = 0 beyond nc
+            }
+            __syncthreads();
+        }
+    }
+    if (okr) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int c = 4 * q + q0;
+            if (c < nc) {
+                panel[row + (size_t)c * ld] = a[q];
+                if (wbuf) wbuf[(wrow0 + r) + (size_t)c * ldw] = a[q] * dv[c];
+            }
+        }
+    }
+}
+
+// one kernel for both the sparse panels (level_sups != nullptr) and the
+// dense tail, so the unrolled fast path is compiled once
+__global__ void __launch_bounds__(NT)
+k_diag(PlanView p, const int* __restrict__ level_sups, int q0, TailView tv, int kb) {
+    __shared__ double Bt[PC][PC + 1];
+    __shared__ int ok;
+    double* panel;
+    int ld, nc, h, c0;
+    if (level_sups) {
+        const int s = level_sups[q0 + blockIdx.x];
+        c0 = p.col0[s];
+        nc = p.col0[s + 1] - c0;
+        h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+        ld = h;
+        panel = p.Lx + p.off[s];
+    } else {
+        const int k0 = kb * PC;
+        nc = min(PC, tv.nt - k0);
+        ld = tv.nt;
+        h = tv.nt - k0;
+        c0 = tv.tc + k0;
+        panel = tv.S + k0 + (size_t)k0 * tv.nt;
+    }
+    const bool f = factor_diag_fast(p, panel, ld, nc, c0, Bt);
+    if (threadIdx.x == 0) ok = f;
+    __syncthreads();
+    if (!ok) factor_diag_block(p, panel, ld, nc, h, c0);
+}
+
+__global__ void __launch_bounds__(NT)
+k_trsm(PlanView p, int u0, TailView tv, int kb) {
+    double* panel;
+    double* wbuf = nullptr;
+    int ld, nc, c0, rlo, rhi, ldw = 0, wrow0 = 0;
+    if (kb < 0) {
+        const int u = u0 + blockIdx.x;
+        const int s = p.unit_sup[u], t = p.unit_tile[u];
+        c0 = p.col0[s];
+        nc = p.col0[s + 1] - c0;
+        ld = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+        rlo = max(t * TR, nc);
+        rhi = min(t * TR + TR, ld);
+        panel = p.Lx + p.off[s];
+    } else {
+        const int k0 = kb * PC;
+        nc = min(PC, tv.nt - k0);
+        rlo = nc + blockIdx.x * TR;            // rows relative to the block column
+        rhi = min(rlo + TR, tv.nt - k0);
+        ld = tv.nt;
+        c0 = tv.tc + k0;
+        panel = tv.S + k0 + (size_t)k0 * tv.nt;
+        wbuf = tv.W;
+        ldw = tv.nt;
+        wrow0 = rlo;
+    }
+    if (rhi <= rlo) return;
+    solve_rows(p, panel, ld, nc, c0, rlo, rhi, wbuf, ldw, wrow0);
+}
+
+}  // namespace
+
+void launch_diag(const PlanView& pv, const int* level_sups, int q0, int count, const TailView& tv, int kb,
+                 hipStream_t s) {
+    hipLaunchKernelGGL(k_diag, dim3(level_sups ? count : 1), dim3(NT), 0, s, pv, level_sups, q0, tv, kb);
+}
+
+void launch_trsm(const PlanView& pv, int u0, int count, const TailView& tv, int kb, hipStream_t s) {
+    if (count >= 0) {
+        hipLaunchKernelGGL(k_trsm, dim3(count), dim3(NT), 0, s, pv, u0, tv, -1);
+    } else {
+        const int below = tv.nt - kb * PC - min(PC, tv.nt - kb * PC);
+        if (below > 0) hipLaunchKernelGGL(k_trsm, dim3((below + TR - 1) / TR), dim3(NT), 0, s, pv, 0, tv, kb);
+    }
+}
+
+}  // namespace ipo

@@ -28,6 +28,7 @@
 
 #include "dev_common.h"
 #include "kkt_device.h"
+#include "kkt_kernels.h"
 #include "lp_io.h"
 
 namespace ipo {
@@ -38,30 +39,7 @@ constexpr int TR = kTileRows;     // 64
 constexpr int PC = kPanelCols;    // 64
 constexpr int NT = 256;           // threads per workgroup
 
-struct PlanView {
-    const int* col0;
-    const int* rowptr;
-    const int* rows;
-    const int64_t* off;
-    const int* unit_sup;
-    const int* unit_tile;
-    const int* task_ptr;
-    const int* task_pair;
-    const int* task_i0;
-    const int* task_i1;
-    const int* upd_src;
-    const int* upd_r0;
-    const int* upd_r1;
-    const int64_t* relptr;
-    const int* rel;
-    double* Lx;
-    double* dg;
-    int* live;
-    int* flags;      // [0] dependent pivots, [1] inconsistent system
-    const int* sign; // node class per new index: -1 y-node, +1 x-node
-    double* dscale;  // sum of |terms| that formed each pivot (zero-pivot test)
-    double tau;      // pivot d is "zero" when |d| <= tau * dscale
-};
+
 
 // ---------------------------------------------------------------- assembly
 __global__ void __launch_bounds__(NT)
@@ -217,129 +195,6 @@ k_update(PlanView p, const TailTask* __restrict__ tasks, const int* __restrict__
 // the reference's update form l_r * (l_c * d), and stores L11' in the
 // block's UPPER triangle (the lower one keeps the input), D in dg, mark in
 // live.  One 256-thread workgroup.
-__device__ void factor_diag_block(const PlanView& p, double* panel, int ld, int nc, int h, int c0) {
-    __shared__ double B[PC][PC + 1];
-    __shared__ double dv[PC];
-    __shared__ int lv[PC];
-    __shared__ double dsc[PC];
-    __shared__ double red[4];
-    __shared__ int ndep_sh;
-    const int tid = threadIdx.x;
-    const int tr = tid & 63, tp = tid >> 6;     // row, part (4 parts stride the columns)
-    for (int c = tp; c < nc; c += 4) B[tr][c] = (tr < nc && tr >= c) ? panel[tr + (size_t)c * ld] : 0.0;
-    for (int k = tid; k < nc; k += NT) dsc[k] = p.dscale[c0 + k];
-    if (tid == 0) ndep_sh = 0;
-    __syncthreads();
-    for (int k = 0; k < nc; k++) {
-        double dk = B[k][k];
-        int alive = 1;
-        if (fabs(dk) <= p.tau * dsc[k]) {         // ldlt.c:600 with a rounding-aware zero test
-            // largest off-diagonal magnitude of column k after every update
-            // from columns < k; rows below the block are rebuilt from the
-            // (not yet solved) panel by a partial forward substitution
-            double mx = 0.0;
-            for (int r = k + 1 + tid; r < nc; r += NT) mx = ref_max(mx, ref_abs(B[r][k]));
-            for (int rr = nc + tid; rr < h; rr += NT) {
-                double w[PC];
-                for (int c = 0; c <= k; c++) w[c] = panel[rr + (size_t)c * ld];
-                for (int j = 0; j < k; j++) {
-                    const double lj = lv[j] ? w[j] / dv[j] : 0.0;
-                    for (int c = j + 1; c <= k; c++) w[c] -= lj * (B[c][j] * dv[j]);
-                }
-                mx = ref_max(mx, ref_abs(w[k]));
-            }
-            mx = block_max(mx, red);
-            if (tid == 0) red[0] = mx;
-            __syncthreads();
-            mx = red[0];
-            if (mx < 1.0e+6 * 1.0e-8) alive = 0;                    // column dropped, d keeps its value
-            else dk = (p.sign[c0 + k] < 0 ? -1.0 : 1.0) * 1.0e-8;   // y-nodes -, x-nodes +
-            if (tid == 0) ndep_sh++;
-            __syncthreads();
-        }
-        if (tid == 0) { dv[k] = dk; lv[k] = alive; }
-        // scale column k first (lij = a / d), then update with lij * (ljk * d)
-        for (int r = k + 1 + tid; r < nc; r += NT) B[r][k] = alive ? B[r][k] / dk : 0.0;
-        __syncthreads();
-        if (alive && tr > k && tr < nc) {
-            const double lr = B[tr][k];
-            for (int c = k + 1 + tp; c <= tr; c += 4) {
-                const double tk = lr * (B[c][k] * dk);
-                B[tr][c] -= tk;
-                if (tr == c) dsc[c] += fabs(tk);
-            }
-        }
-        __syncthreads();
-    }
-    // L11(r, c) -> upper slot (c, r): thread tr writes row c = tr of the slot image
-    for (int r = tp; r < nc; r += 4)
-        if (tr < r) panel[tr + (size_t)r * ld] = B[r][tr];
-    for (int k = tid; k < nc; k += NT) { p.dg[c0 + k] = dv[k]; p.live[c0 + k] = lv[k]; }
-    if (tid == 0 && ndep_sh) atomicAdd(&p.flags[0], ndep_sh);
-}
-
-__global__ void __launch_bounds__(NT)
-k_diag(PlanView p, const int* __restrict__ level_sups, int q0) {
-    const int s = level_sups[q0 + blockIdx.x];
-    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
-    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
-    factor_diag_block(p, p.Lx + p.off[s], h, nc, h, c0);
-}
-
-// ------------------------------------------------------- L21 = A21 L11^-T D^-1
-// Rows [rlo, rhi) of a panel (ld, nc columns starting at global column c0),
-// against the factored diagonal block (L11' in its upper triangle).  With
-// wbuf != nullptr also writes W = L21 * D (row-major-by-column, ldw) for the
-// dense tail's trailing update.  Reference form: l = w / d, w -= l * (l11 * d).
-__device__ void solve_rows(const PlanView& p, double* panel, int ld, int nc, int c0, int rlo, int rhi,
-                           double* wbuf, int ldw, int wrow0) {
-    __shared__ double B[PC][PC + 1];      // L11(c, k) * d_k
-    __shared__ double R[TR][PC + 1];
-    __shared__ double dv[PC];
-    __shared__ int lv[PC];
-    const int nrow = rhi - rlo;
-    const int tid = threadIdx.x;
-    for (int k = tid; k < nc; k += NT) { dv[k] = p.dg[c0 + k]; lv[k] = p.live[c0 + k]; }
-    __syncthreads();
-    {
-        const int cc = tid & 63, rp = tid >> 6;    // slot (cc, r) holds L11(r, cc)
-        for (int r = rp; r < nc; r += 4) B[r][cc] = (cc < r) ? panel[cc + (size_t)r * ld] * dv[cc] : 0.0;
-    }
-    for (int idx = tid; idx < nrow * nc; idx += NT) {
-        const int r = idx % nrow, c = idx / nrow;
-        R[r][c] = panel[(rlo + r) + (size_t)c * ld];
-    }
-    __syncthreads();
-    const int r = tid & 63, part = tid >> 6;
-    for (int k = 0; k < nc; k++) {
-        const double lk = (r < nrow && lv[k]) ? R[r][k] / dv[k] : 0.0;
-        __syncthreads();
-        if (r < nrow) {
-            for (int c = k + 1 + part; c < nc; c += 4) R[r][c] -= lk * B[c][k];
-            if (part == 0) R[r][k] = lk;
-        }
-        __syncthreads();
-    }
-    for (int idx = tid; idx < nrow * nc; idx += NT) {
-        const int rr = idx % nrow, c = idx / nrow;
-        const double l = R[rr][c];
-        panel[(rlo + rr) + (size_t)c * ld] = l;
-        if (wbuf) wbuf[(wrow0 + rr) + (size_t)c * ldw] = l * dv[c];
-    }
-}
-
-__global__ void __launch_bounds__(NT)
-k_trsm(PlanView p, int u0) {
-    const int u = u0 + blockIdx.x;
-    const int s = p.unit_sup[u], t = p.unit_tile[u];
-    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
-    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
-    const int rbase = t * TR;
-    const int rlo = max(rbase, nc), rhi = min(rbase + TR, h);
-    if (rhi <= rlo) return;
-    solve_rows(p, p.Lx + p.off[s], h, nc, c0, rlo, rhi, nullptr, 0, 0);
-}
-
 // ======================================================== dense tail
 // S = Lx + off_tail, nt x nt column-major (ld = nt), columns tail_c0.. .
 // (TailView is declared in kkt_device.h)
@@ -358,22 +213,6 @@ k_tail_update(PlanView p, TailView tv, const int* __restrict__ kslot, const int*
                 bi == bj ? p.dscale + tv.tc + bj * TR : nullptr);
 }
 
-__global__ void __launch_bounds__(NT)
-k_tail_diag(PlanView p, TailView tv, int kb) {
-    const int k0 = kb * PC;
-    const int nc = min(PC, tv.nt - k0);
-    factor_diag_block(p, tv.S + k0 + (size_t)k0 * tv.nt, tv.nt, nc, tv.nt - k0, tv.tc + k0);
-}
-
-__global__ void __launch_bounds__(NT)
-k_tail_trsm(PlanView p, TailView tv, int kb) {
-    const int k0 = kb * PC;
-    const int nc = min(PC, tv.nt - k0);
-    const int rlo = nc + blockIdx.x * TR;            // rows relative to the block column
-    const int rhi = min(rlo + TR, tv.nt - k0);
-    if (rhi <= rlo) return;
-    solve_rows(p, tv.S + k0 + (size_t)k0 * tv.nt, tv.nt, nc, tv.tc + k0, rlo, rhi, tv.W, tv.nt, rlo);
-}
 
 // Trailing update S(bi, bj) -= L(bi, kb) * W(bj, kb)'  for bi >= bj > kb,
 // with v_mfma_f64_16x16x4_f64: 4 waves, each a 32x32 quarter (2x2 MFMA tiles).
@@ -436,45 +275,52 @@ k_tail_syrk(PlanView p, TailView tv, int kb) {
 }
 
 // -------------------------------------------------------------- solves
-// value of v in lane j (j wave-uniform), via two v_readlane_b32
-__device__ __forceinline__ double lane_bcast(double v, int j) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane(static_cast<int>(b), j);
-    const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), j);
-    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
-}
-
 // One wave solves a unit-lower nc x nc block in place: lane r holds z_r on
-// entry and on exit; Ls[r][j] = L(r, j).  A dropped column j (mark false)
-// keeps z_j when |z_j| > eps (and the system is flagged inconsistent), else
-// z_j = 0 -- ldlt.c:446-470.
+// entry and on exit; Ls[r][j] = L(r, j) (zero for j >= r).  Lane r keeps its
+// row of L in registers; z_j is broadcast by v_readlane.  A dropped column j
+// (mark false) keeps z_j when |z_j| > eps (and the system is flagged
+// inconsistent), else z_j = 0 -- ldlt.c:446-470.
 __device__ __forceinline__ double tri_lower(double zr, const double (*Ls)[PC + 1], const int* lv, int nc, double eps,
                                             int& bad) {
     const int lane = threadIdx.x & 63;
-    for (int j = 0; j < nc; j++) {
-        const int alive = lv[j];
-        if (lane == j && !alive) {
-            if (fabs(zr) > eps) bad = 1;
-            else zr = 0.0;
+    const uint64_t lm = __ballot(lane < nc && lv[lane]);
+    double lr[PC];
+#pragma unroll
+    for (int j = 0; j < PC; j++) lr[j] = lane < nc ? Ls[lane][j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < PC; j++) {
+        if (j < nc) {
+            const bool alive = (lm >> j) & 1ull;
+            if (!alive && lane == j) {
+                if (fabs(zr) > eps) bad = 1;
+                else zr = 0.0;
+            }
+            const double zj = lane_bcast(zr, j);
+            if (alive && lane > j) zr -= lr[j] * zj;
         }
-        const double zj = lane_bcast(zr, j);
-        if (alive && lane > j && lane < nc) zr -= Ls[lane][j] * zj;
     }
     return zr;
 }
 
-// unit-upper (L11') counterpart; Ls[j][r] = L(j, r)
+// unit-upper (L11') counterpart; Ls[j][r] = L(j, r) (zero for r >= j)
 __device__ __forceinline__ double tri_upper(double zr, const double (*Ls)[PC + 1], const int* lv, int nc, double eps,
                                             int& bad) {
     const int lane = threadIdx.x & 63;
-    for (int j = nc - 1; j >= 0; j--) {
-        const int alive = lv[j];
-        if (lane == j && !alive) {
-            if (fabs(zr) > eps) bad = 1;
-            else zr = 0.0;
+    const uint64_t lm = __ballot(lane < nc && lv[lane]);
+    double lc[PC];
+#pragma unroll
+    for (int j = 0; j < PC; j++) lc[j] = j < nc ? Ls[j][lane] : 0.0;
+#pragma unroll
+    for (int j = PC - 1; j >= 0; j--) {
+        if (j < nc) {
+            const bool alive = (lm >> j) & 1ull;
+            if (!alive && lane == j) {
+                if (fabs(zr) > eps) bad = 1;
+                else zr = 0.0;
+            }
+            const double zj = lane_bcast(zr, j);
+            if (alive && lane < j) zr -= lc[j] * zj;
         }
-        const double zj = lane_bcast(zr, j);
-        if (alive && lane < j) zr -= Ls[j][lane] * zj;
     }
     return zr;
 }
@@ -487,11 +333,26 @@ __device__ __forceinline__ double dscale_rule(const PlanView& p, int v, double z
     return zv;
 }
 
-// Stage L11 of a panel (ld = h): rowform -> Ls[r][j] = L(r, j), else
-// Ls[j][r] = L(j, r); both read the upper-triangle slot image (j, r).
+// Stage L11 of a panel (ld = h) from the upper-triangle slot image:
+// Ls[r][j] = L(r, j) for j < r, 0 elsewhere.  Each wave issues all its
+// loads before the first LDS store (addresses clamped in bounds).
 __device__ __forceinline__ void stage_l11(const double* panel, size_t ld, int nc, double (*Ls)[PC + 1]) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int r = wv; r < nc; r += nw) Ls[r][lane] = lane < r ? panel[lane + (size_t)r * ld] : 0.0;
+    for (int r0 = wv; r0 < PC; r0 += 16 * nw) {
+        double t[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int r = r0 + q * nw;
+            const bool ok = r < nc && lane < r;
+            t[q] = panel[ok ? lane + (size_t)r * ld : 0];
+            t[q] = ok ? t[q] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int r = r0 + q * nw;
+            if (r < PC) Ls[r][lane] = t[q];
+        }
+    }
 }
 
 // Forward, diagonal part of supernode s: subtract the y values of solved
@@ -582,9 +443,12 @@ k_fwd_gemv(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict_
     double acc = 0.0;
     if (i < hb && nq > 0) {
         const double* __restrict__ row = p.Lx + p.off[s] + nc + i + (size_t)kq * h;
+        double t[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) t[q] = row[(size_t)min(q, nq - 1) * h];
 #pragma unroll
         for (int q = 0; q < 16; q++)
-            if (q < nq) acc += row[(size_t)q * h] * zs[kq + q];
+            if (q < nq) acc += t[q] * zs[kq + q];
     }
     red[wv][lane] = acc;
     __syncthreads();
@@ -617,9 +481,12 @@ k_backward(PlanView p, const int* __restrict__ level_sups, int q0, double* __res
         for (int i = lane; i < hb; i += 64) {
             const double zi = z[rows[i]];
             const double* __restrict__ col = panel + nc + i + (size_t)kq * h;
+            double t[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, nq - 1) * h];
 #pragma unroll
             for (int q = 0; q < 16; q++)
-                if (q < nq) acc[q] += col[(size_t)q * h] * zi;
+                if (q < nq) acc[q] += t[q] * zi;
         }
 #pragma unroll
         for (int q = 0; q < 16; q++) {
@@ -651,12 +518,17 @@ k_bwd_partial(PlanView p, const int* __restrict__ chunk_sup, const int* __restri
     const int kq = wv * 16, nq = min(16, nc - kq);
     if (nq <= 0) return;
     const int i = r0 + lane;
-    const double zi = i < hb ? z[p.rows[p.rowptr[s] + i]] : 0.0;
-    const double* __restrict__ col = p.Lx + p.off[s] + nc + i + (size_t)kq * h;
+    const bool okr = i < hb;
+    const int ic = okr ? i : 0;
+    const double zi = z[p.rows[p.rowptr[s] + ic]];
+    const double* __restrict__ col = p.Lx + p.off[s] + nc + ic + (size_t)kq * h;
+    double t[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, nq - 1) * h];
 #pragma unroll
     for (int q = 0; q < 16; q++) {
-        const double t = wave_sum((i < hb && q < nq) ? col[(size_t)q * h] * zi : 0.0);
-        if (lane == 0 && q < nq) part[(size_t)c * PC + kq + q] = t;
+        const double v = wave_sum((okr && q < nq) ? t[q] * zi : 0.0);
+        if (lane == 0 && q < nq) part[(size_t)c * PC + kq + q] = v;
     }
 }
 
@@ -733,9 +605,12 @@ k_tail_fwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double
     double acc = 0.0;
     if (r < nt && nq > 0) {
         const double* __restrict__ row = tv.S + r + (size_t)(k0 + kq) * nt;
+        double t[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) t[q] = row[(size_t)min(q, nq - 1) * nt];
 #pragma unroll
         for (int q = 0; q < 16; q++)
-            if (q < nq) acc += row[(size_t)q * nt] * zb[kq + q];
+            if (q < nq) acc += t[q] * zb[kq + q];
     }
     red[wv][lane] = acc;
     __syncthreads();
@@ -782,9 +657,12 @@ k_tail_bwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double
     double acc = 0.0;
     if (j < k0 && nq > 0) {
         const double* __restrict__ col = tv.S + (k0 + kq) + (size_t)j * nt;
+        double t[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) t[q] = col[min(q, nq - 1)];
 #pragma unroll
         for (int q = 0; q < 16; q++)
-            if (q < nq) acc += col[q] * zb[kq + q];
+            if (q < nq) acc += t[q] * zb[kq + q];
     }
     red[wv][lane] = acc;
     __syncthreads();
@@ -1041,8 +919,8 @@ void KktDevice::factor(const double* dE, const double* dD) {
         }
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 2], s));
-        hipLaunchKernelGGL(k_diag, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0);
-        hipLaunchKernelGGL(k_trsm, dim3(u1 - u0), dim3(NT), 0, s, pv, u0);
+        launch_diag(pv, dlevel_sups_.get(), q0, q1 - q0, tv, 0, s);
+        launch_trsm(pv, u0, u1 - u0, tv, 0, s);
         if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 3], s));
     }
     if (plan_.nt > 0) {
@@ -1053,10 +931,10 @@ void KktDevice::factor(const double* dE, const double* dD) {
         if (timing_) IPO_HIP_CHECK(hipEventRecord(ev3_, s));
         for (int kb = 0; kb < plan_.ntb; kb++) {
             const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
-            hipLaunchKernelGGL(k_tail_diag, dim3(1), dim3(NT), 0, s, pv, tv, kb);
+            launch_diag(pv, nullptr, 0, 1, tv, kb, s);
             const int below = plan_.nt - k0 - nc;
             if (below > 0) {
-                hipLaunchKernelGGL(k_tail_trsm, dim3(ceil_div(below, kTileRows)), dim3(NT), 0, s, pv, tv, kb);
+                launch_trsm(pv, 0, -1, tv, kb, s);
                 const int nb = plan_.ntb - kb - 1;
                 hipLaunchKernelGGL(k_tail_syrk, dim3(nb * (nb + 1) / 2), dim3(NT), 0, s, pv, tv, kb);
             }

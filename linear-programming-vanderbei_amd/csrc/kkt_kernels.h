@@ -1,0 +1,56 @@
+// kkt_kernels.h -- what the KKT kernel translation units share: the device
+// view of the symbolic plan and the launchers of the dense per-panel kernels
+// (kkt_dense.hip), which live in their own translation unit because their
+// fully unrolled register code dominates compile time.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kkt_device.h"
+#include "kkt_plan.h"
+
+namespace ipo {
+
+struct PlanView {
+    const int* col0;
+    const int* rowptr;
+    const int* rows;
+    const int64_t* off;
+    const int* unit_sup;
+    const int* unit_tile;
+    const int* task_ptr;
+    const int* task_pair;
+    const int* task_i0;
+    const int* task_i1;
+    const int* upd_src;
+    const int* upd_r0;
+    const int* upd_r1;
+    const int64_t* relptr;
+    const int* rel;
+    double* Lx;
+    double* dg;
+    int* live;
+    int* flags;      // [0] dependent pivots, [1] inconsistent system
+    const int* sign; // node class per new index: -1 y-node, +1 x-node
+    double* dscale;  // sum of |terms| that formed each pivot (zero-pivot test)
+    double tau;      // pivot d is "zero" when |d| <= tau * dscale
+};
+
+// value of v in lane j (j wave-uniform), via two v_readlane_b32
+static __device__ __forceinline__ double lane_bcast(double v, int j) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane(static_cast<int>(b), j);
+    const int hi = __builtin_amdgcn_readlane(static_cast<int>(b >> 32), j);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
+// Diagonal-block LDL' of every supernode of one level (level_sups[q0..q0+count)),
+// or, with level_sups == nullptr, of block column kb of the dense tail.
+void launch_diag(const PlanView& pv, const int* level_sups, int q0, int count, const TailView& tv, int kb,
+                 hipStream_t s);
+// L21 = A21 L11^-T D^-1 for factor units [u0, u0+count), or, with
+// count < 0, for the rows below block column kb of the dense tail.
+void launch_trsm(const PlanView& pv, int u0, int count, const TailView& tv, int kb, hipStream_t s);
+
+}  // namespace ipo
