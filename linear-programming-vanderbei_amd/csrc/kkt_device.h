@@ -86,6 +86,7 @@ class KktDevice {
 
   private:
     TailView tail_view() const;
+    void launch_gather(const struct PlanView& pv, const TailView& tv, int tail, int group, hipStream_t s);
     void launch_reduce_maxabs2(const double* a, int na, const double* b, int nb, double* dst);
 
     int m_, n_, T_;
@@ -119,7 +120,11 @@ class KktDevice {
     DevBuf<double> dYbuf_;
     std::vector<int> chunk_ptr_;          // per level: solve chunks [chunk_ptr_[l], chunk_ptr_[l+1])
     DevBuf<int> dchunk_sup_, dchunk_r0_, dsup_chunk0_;
-    DevBuf<double> dPartial_;    // backward partial sums, one 64-vector per chunk      // forward-sweep update values, one per row of every R_s
+    DevBuf<double> dPartial_;    // backward partial sums, one 64-vector per chunk
+    // split-K gather chunks per group (sparse level l, group nlevels = tail)
+    std::vector<int> ck_ptr_, sp_ptr_;
+    DevBuf<int> dck_u_, dck_b_, dck_e_, dck_part_, dsp_u_, dsp_p0_, dsp_n_;
+    DevBuf<double> dPartialTile_;      // forward-sweep update values, one per row of every R_s
     DevBuf<int> dtail_task_ptr_, dkslot_, dkslot_ptr_, dtail_kslot_, dtail_kslot_ptr_;
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;

@@ -98,25 +98,60 @@ __device__ __forceinline__ void stage_slab(const PlanView& p, const TailTask* __
     }
 }
 
-__device__ void gather_tile(const PlanView& p, const TailTask* __restrict__ tasks, const int* __restrict__ kslot,
-                            int kb, int ke, double* out, size_t ld, int nrow, int ncol, int row0, int col0,
-                            double* dscale_col) {
+// Output tile of one gather unit: a 64-row tile of a sparse panel
+// (tail < 0) or tile `tail` of the dense tail.
+struct GatherTile {
+    double* out;
+    size_t ld;
+    int nrow, ncol, row0, col0;
+    double* dscale_col;      // non-null on tiles that hold diagonal entries
+};
+
+__device__ __forceinline__ GatherTile unit_tile(const PlanView& p, const TailView& tv, int u, int tail) {
+    GatherTile g;
+    if (tail < 0) {
+        const int s = p.unit_sup[u], t = p.unit_tile[u];
+        const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+        const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+        const int rbase = t * TR;
+        g.out = p.Lx + p.off[s] + rbase;
+        g.ld = h;
+        g.nrow = min(TR, h - rbase);
+        g.ncol = nc;
+        g.row0 = rbase;
+        g.col0 = 0;
+        g.dscale_col = t == 0 ? p.dscale + c0 : nullptr;
+    } else {
+        int bi = 0;
+        while ((bi + 1) * (bi + 2) / 2 <= u) bi++;
+        const int bj = u - bi * (bi + 1) / 2;
+        g.out = tv.S + bi * TR + (size_t)(bj * TR) * tv.nt;
+        g.ld = tv.nt;
+        g.nrow = min(TR, tv.nt - bi * TR);
+        g.ncol = min(TR, tv.nt - bj * TR);
+        g.row0 = bi * TR;
+        g.col0 = bj * TR;
+        g.dscale_col = bi == bj ? p.dscale + tv.tc + bj * TR : nullptr;
+    }
+    return g;
+}
+
+// MFMA accumulation of slots [kb, ke) into this thread's 16 tile entries
+// (acc[a][b][i] = entry (wr + 16a + (lane>>4) + 4i, wc + 16b + (lane&15)))
+// and, for lanes on a diagonal entry, the |terms| of that entry (dabs).
+__device__ void gather_acc(const PlanView& p, const TailTask* __restrict__ tasks, const int* __restrict__ kslot,
+                           int kb, int ke, int dcol, bool has_diag, double4_t (&acc)[2][2], double& dabs) {
     __shared__ double As[2][TR][KS + 1];
     __shared__ double Bs[2][TR][KS + 1];
-    __shared__ double dred[4][TR];
     const int tid = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
     const int li = lane & 15, lk = lane >> 4;
-    // diagonal entries of this tile: row r meets column c = row0 + r - col0
-    const int dcol = row0 + lane - col0;
-    const bool has_diag = dscale_col && dcol >= 0 && dcol < ncol && lane < nrow;
-    double4_t acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
-    double dabs = 0.0;
+    dabs = 0.0;
     double ra[KS / 4], rb[KS / 4];
     const int nslab = (ke - kb) / KS;
     stage_slab(p, tasks, kslot, kb, wv, lane, ra, rb);
@@ -155,6 +190,14 @@ __device__ void gather_tile(const PlanView& p, const TailTask* __restrict__ task
         }
         __syncthreads();
     }
+}
+
+// out -= acc on the tile's lower part; dscale += the four waves' dabs in order
+__device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], double dabs, bool has_diag,
+                             int dcol) {
+    __shared__ double dred[4][TR];
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -163,28 +206,75 @@ __device__ void gather_tile(const PlanView& p, const TailTask* __restrict__ task
             for (int i = 0; i < 4; i++) {
                 const int rr = wr + a * 16 + (lane >> 4) + 4 * i;
                 const int cc = wc + b * 16 + (lane & 15);
-                if (rr >= nrow || cc >= ncol || row0 + rr < col0 + cc) continue;
-                out[rr + (size_t)cc * ld] -= acc[a][b][i];
+                if (rr >= g.nrow || cc >= g.ncol || g.row0 + rr < g.col0 + cc) continue;
+                g.out[rr + (size_t)cc * g.ld] -= acc[a][b][i];
             }
-    if (dscale_col) {
+    if (g.dscale_col) {
         dred[wv][lane] = dabs;
         __syncthreads();
-        if (wv == 0 && has_diag) dscale_col[dcol] += ((dred[0][lane] + dred[1][lane]) + dred[2][lane]) + dred[3][lane];
+        if (wv == 0 && has_diag) g.dscale_col[dcol] += ((dred[0][lane] + dred[1][lane]) + dred[2][lane]) + dred[3][lane];
     }
 }
 
+// Gather chunks: chunk c covers slots [ck_b[c], ck_e[c]) of unit ck_u[c].
+// ck_part[c] < 0: the unit's only chunk, subtract directly; else store the
+// partial tile (thread-fragment order) and dabs at partial slot ck_part[c].
+// tail >= 0: units are dense-tail tiles.
 __global__ void __launch_bounds__(NT)
-k_update(PlanView p, const TailTask* __restrict__ tasks, const int* __restrict__ kslot,
-         const int* __restrict__ kslot_ptr, int u0) {
-    const int u = u0 + blockIdx.x;
-    const int kb = kslot_ptr[u], ke = kslot_ptr[u + 1];
-    if (kb == ke) return;
-    const int s = p.unit_sup[u], t = p.unit_tile[u];
-    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
-    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
-    const int rbase = t * TR;
-    gather_tile(p, tasks, kslot, kb, ke, p.Lx + p.off[s] + rbase, h, min(TR, h - rbase), nc, rbase, 0,
-                t == 0 ? p.dscale + c0 : nullptr);
+k_update(PlanView p, TailView tv, int tail, const TailTask* __restrict__ tasks, const int* __restrict__ kslot,
+         const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
+         const int* __restrict__ ck_part, int c0, double* __restrict__ partial) {
+    const int c = c0 + blockIdx.x;
+    const int u = ck_u[c], kb = ck_b[c], ke = ck_e[c], pi = ck_part[c];
+    const GatherTile g = unit_tile(p, tv, u, tail);
+    const int lane = threadIdx.x & 63;
+    const int dcol = g.row0 + lane - g.col0;
+    const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
+    double4_t acc[2][2];
+    double dabs;
+    gather_acc(p, tasks, kslot, kb, ke, dcol, has_diag, acc, dabs);
+    if (pi < 0) {
+        gather_store(g, acc, dabs, has_diag, dcol);
+        return;
+    }
+    double* dst = partial + (size_t)pi * (TR * TR + 4 * TR);
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) dst[((a * 2 + b) * 4 + i) * NT + tid] = acc[a][b][i];
+    dst[TR * TR + tid] = dabs;
+}
+
+// Split units: sum their chunks' partial tiles in chunk order, then store.
+__global__ void __launch_bounds__(NT)
+k_update_reduce(PlanView p, TailView tv, int tail, const int* __restrict__ sp_u, const int* __restrict__ sp_p0,
+                const int* __restrict__ sp_n, int s0, const double* __restrict__ partial) {
+    const int q = s0 + blockIdx.x;
+    const int u = sp_u[q], p0 = sp_p0[q], np = sp_n[q];
+    const GatherTile g = unit_tile(p, tv, u, tail);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int dcol = g.row0 + lane - g.col0;
+    const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
+    double4_t acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    double dabs = 0.0;
+    for (int j = 0; j < np; j++) {
+        const double* src = partial + (size_t)(p0 + j) * (TR * TR + 4 * TR);
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) acc[a][b][i] += src[((a * 2 + b) * 4 + i) * NT + tid];
+        dabs += src[TR * TR + tid];
+    }
+    gather_store(g, acc, dabs, has_diag, dcol);
 }
 
 // ------------------------------------------------- diagonal block LDL'
@@ -199,19 +289,6 @@ k_update(PlanView p, const TailTask* __restrict__ tasks, const int* __restrict__
 // S = Lx + off_tail, nt x nt column-major (ld = nt), columns tail_c0.. .
 // (TailView is declared in kkt_device.h)
 
-// Gather of all sparse panels' contributions into one 64x64 tile of S.
-__global__ void __launch_bounds__(NT)
-k_tail_update(PlanView p, TailView tv, const int* __restrict__ kslot, const int* __restrict__ kslot_ptr) {
-    const int tile = blockIdx.x;
-    int bi = 0;
-    while ((bi + 1) * (bi + 2) / 2 <= tile) bi++;
-    const int bj = tile - bi * (bi + 1) / 2;
-    const int kb = kslot_ptr[tile], ke = kslot_ptr[tile + 1];
-    if (kb == ke) return;
-    const int nrow = min(TR, tv.nt - bi * TR), ncol = min(TR, tv.nt - bj * TR);
-    gather_tile(p, tv.tasks, kslot, kb, ke, tv.S + bi * TR + (size_t)(bj * TR) * tv.nt, tv.nt, nrow, ncol, bi * TR, bj * TR,
-                bi == bj ? p.dscale + tv.tc + bj * TR : nullptr);
-}
 
 
 // Trailing update S(bi, bj) -= L(bi, kb) * W(bj, kb)'  for bi >= bj > kb,
@@ -805,6 +882,50 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dYbuf_.alloc(plan_.rowptr.back() > 0 ? plan_.rowptr.back() : 1);
     dkslot_.upload(plan_.kslot, s);
     dkslot_ptr_.upload(plan_.kslot_ptr, s);
+    {   // gather chunks (split K): groups = sparse levels, then the dense tail
+        std::vector<int> cu, cb, ce, cp, su, sp0, sn;
+        ck_ptr_.assign(plan_.nlevels + 2, 0);
+        sp_ptr_.assign(plan_.nlevels + 2, 0);
+        size_t max_part = 0;
+        auto group = [&](int u0, int u1, const std::vector<int>& kptr) {
+            long sumk = 0;
+            for (int u = u0; u < u1; u++) sumk += kptr[u + 1] - kptr[u];
+            // aim at >= 512 workgroups per launch, chunks of 64..512 slots
+            long kmax = (sumk / 512 + kSlab - 1) / kSlab * kSlab;
+            kmax = std::max<long>(64, std::min<long>(512, kmax));
+            int np = 0;
+            for (int u = u0; u < u1; u++) {
+                const int kb = kptr[u], ke = kptr[u + 1];
+                if (ke == kb) continue;
+                const int nch = static_cast<int>((ke - kb + kmax - 1) / kmax);
+                if (nch > 1) { su.push_back(u); sp0.push_back(np); sn.push_back(nch); }
+                for (int j = 0; j < nch; j++) {
+                    cu.push_back(u);
+                    cb.push_back(kb + static_cast<int>(j * kmax));
+                    ce.push_back(std::min<int>(ke, kb + static_cast<int>((j + 1) * kmax)));
+                    cp.push_back(nch > 1 ? np++ : -1);
+                }
+            }
+            max_part = std::max<size_t>(max_part, np);
+        };
+        for (int l = 0; l < plan_.nlevels; l++) {
+            if (l > 0) group(plan_.unit_level_ptr[l], plan_.unit_level_ptr[l + 1], plan_.kslot_ptr);
+            ck_ptr_[l + 1] = static_cast<int>(cu.size());
+            sp_ptr_[l + 1] = static_cast<int>(su.size());
+        }
+        if (plan_.nt > 0) group(0, plan_.ntb * (plan_.ntb + 1) / 2, plan_.tail_kslot_ptr);
+        ck_ptr_[plan_.nlevels + 1] = static_cast<int>(cu.size());
+        sp_ptr_[plan_.nlevels + 1] = static_cast<int>(su.size());
+        dck_u_.upload(cu, s);
+        dck_b_.upload(cb, s);
+        dck_e_.upload(ce, s);
+        dck_part_.upload(cp, s);
+        dsp_u_.upload(su, s);
+        dsp_p0_.upload(sp0, s);
+        dsp_n_.upload(sn, s);
+        dPartialTile_.alloc(std::max<size_t>(1, max_part) * (kTileRows * kTileRows + 4 * kTileRows));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+    }
     dutasks_.upload(reinterpret_cast<const uint64_t*>(plan_.utasks.data()), plan_.utasks.size() * 4, s);
     if (plan_.nt > 0) {
         dtail_task_ptr_.upload(plan_.tail_task_ptr, s);
@@ -913,8 +1034,7 @@ void KktDevice::factor(const double* dE, const double* dD) {
         if (u1 <= u0) continue;
         if (l > 0) {
             if (timing_) { IPO_HIP_CHECK(hipEventRecord(kev_[4 * l], s)); upd_used[l] = 1; }
-            hipLaunchKernelGGL(k_update, dim3(u1 - u0), dim3(NT), 0, s, pv,
-                               reinterpret_cast<const TailTask*>(dutasks_.get()), dkslot_.get(), dkslot_ptr_.get(), u0);
+            launch_gather(pv, tv, -1, l, s);
             if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 1], s));
         }
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
@@ -926,8 +1046,8 @@ void KktDevice::factor(const double* dE, const double* dD) {
     if (plan_.nt > 0) {
         const int ntiles = plan_.ntb * (plan_.ntb + 1) / 2;
         if (timing_) IPO_HIP_CHECK(hipEventRecord(ev2_, s));
-        hipLaunchKernelGGL(k_tail_update, dim3(ntiles), dim3(NT), 0, s, pv, tv, dtail_kslot_.get(),
-                           dtail_kslot_ptr_.get());
+        (void)ntiles;
+        launch_gather(pv, tv, 0, plan_.nlevels, s);
         if (timing_) IPO_HIP_CHECK(hipEventRecord(ev3_, s));
         for (int kb = 0; kb < plan_.ntb; kb++) {
             const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
@@ -972,6 +1092,22 @@ void KktDevice::factor(const double* dE, const double* dD) {
     tm_.factors++;
     ndep_ = hFlags_[0];
     if (-hScal_[0] < 1.0e-14) epsdiag_ *= 10;
+}
+
+// Gather launches of one level (tail < 0) or of the dense tail (group =
+// nlevels): the chunks, then the in-order reduction of the split units.
+void KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, int group, hipStream_t s) {
+    const int c0 = ck_ptr_[group], c1 = ck_ptr_[group + 1];
+    if (c1 <= c0) return;
+    const TailTask* tasks = tail < 0 ? reinterpret_cast<const TailTask*>(dutasks_.get())
+                                     : reinterpret_cast<const TailTask*>(dtail_tasks_.get());
+    const int* kslot = tail < 0 ? dkslot_.get() : dtail_kslot_.get();
+    hipLaunchKernelGGL(k_update, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, tasks, kslot, dck_u_.get(), dck_b_.get(),
+                       dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get());
+    const int s0 = sp_ptr_[group], s1 = sp_ptr_[group + 1];
+    if (s1 > s0)
+        hipLaunchKernelGGL(k_update_reduce, dim3(s1 - s0), dim3(NT), 0, s, pv, tv, tail, dsp_u_.get(), dsp_p0_.get(),
+                           dsp_n_.get(), s0, dPartialTile_.get());
 }
 
 void KktDevice::rawsolve(double* dz) {
