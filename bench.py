@@ -14,9 +14,9 @@ N > 1: dfl001 does not shard, so ranks run independent
 replicas; value = all ranks' iterations / max wall time over ranks.
 
 Also reported:
-  roofline      -- the dominant kernel (k_update, the left-looking gather of
-                   the supernodal factorisation), measured live with HIP events
-                   on its own stream during the timed region;
+  roofline      -- the dominant phase of the KKT core (most device time in the
+                   timed region), measured live with HIP events on the
+                   solver's stream; "phases" lists every phase the same way;
   cpu_baseline  -- the CPU oracle (oracle/, a single-threaded restatement of
                    the reference's ipo) timed on this host over a bounded
                    sample of the same workload (rank 0, N = 1).
@@ -34,7 +34,10 @@ sys.path.insert(0, os.path.join(REPO, "linear-programming-vanderbei_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 METRIC = "IPM iterations/sec (ADA^T factor+solve) on netlib dfl001; duality gap ≤1e-8"
-FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, spec
+FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, AMD spec (the guide has no fp64 row)
+PHASE_KERNELS = {"gather": "k_update+k_update_reduce", "diag": "k_diag", "trsm": "k_trsm", "tail_syrk": "k_tail_syrk",
+                 "forward": "k_forward|k_fwd_diag|k_fwd_gemv|k_tail_gather|k_tail_fwd",
+                 "backward": "k_backward|k_bwd_partial|k_bwd_finish|k_tail_dscale|k_tail_bwd"}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak, MI355X_MICROARCH.md
 
 
@@ -154,31 +157,39 @@ def main():
     total_iters = d.sum(iters)
     value = total_iters / elapsed
 
-    # dominant kernel: the supernodal gather (k_update); algorithmic flops/bytes
-    # per factorisation from the symbolic plan, device time from HIP events
-    roof = None
-    if st["update_ms"] > 0 and st["update_launches"] > 0:
-        nfac = st["factors"]
-        secs = st["update_ms"] * 1e-3
-        flops = st["flops_update"] * nfac
-        byts = st["bytes_update"] * nfac
-        t_flop = flops / (FP64_PEAK_TFLOPS * 1e12)
-        t_byte = byts / (HBM_PEAK_GBS * 1e9)
-        per_launch_s = secs / st["update_launches"]
-        if t_flop >= t_byte:
-            ach = flops / secs / 1e12
+    # dominant kernel: the phase with the most device time in the timed
+    # region (HIP events on the solver's stream); algorithmic work per
+    # occurrence from the symbolic plan (DESIGN.md "Kernels")
+    roof, phases = None, {}
+    if not args.no_timing and sum(st["phase_ms"]) > 0:
+        for i, name in enumerate(ipo_amd.PHASES):
+            ms, nl, cnt = st["phase_ms"][i], st["phase_launches"][i], st["phase_count"][i]
+            if nl == 0 or ms <= 0:
+                continue
+            flops, byts = st["phase_flops"][i] * cnt, st["phase_bytes"][i] * cnt
+            secs = ms * 1e-3
+            phases[name] = {"kernels": PHASE_KERNELS[name], "ms_total": ms, "launches": nl,
+                            "avg_launch_us": 1e3 * ms / nl, "share_of_timed_region": secs / max(elapsed, 1e-12),
+                            "gflop_per_s": flops / secs / 1e9, "gbyte_per_s": byts / secs / 1e9,
+                            "flops_per_occurrence": st["phase_flops"][i], "bytes_per_occurrence": st["phase_bytes"][i],
+                            "occurrences": cnt}
+        top = max(phases, key=lambda k: phases[k]["ms_total"])
+        ph = phases[top]
+        i = ipo_amd.PHASES.index(top)
+        flops_l = st["phase_flops"][i] * st["phase_count"][i] / ph["launches"]
+        bytes_l = st["phase_bytes"][i] * st["phase_count"][i] / ph["launches"]
+        t_l = ph["avg_launch_us"] * 1e-6
+        if flops_l / (FP64_PEAK_TFLOPS * 1e12) >= bytes_l / (HBM_PEAK_GBS * 1e9):
+            ach = flops_l / t_l / 1e12
             roof = {"bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": ach / FP64_PEAK_TFLOPS, "traffic": None}
         else:
-            ach = byts / secs / 1e9
+            ach = bytes_l / t_l / 1e9
             roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": ach / HBM_PEAK_GBS, "traffic": None}
-        roof.update({"kernel": "k_update", "avg_launch_us": per_launch_s * 1e6,
-                     "launches": st["update_launches"],
-                     "algorithmic_flops_per_factor": st["flops_update"],
-                     "algorithmic_bytes_per_factor": st["bytes_update"],
-                     "share_of_timed_region": secs / max(st["t_solve_s"], 1e-12),
-                     "panel_kernel_ms": st["panel_ms"], "sweep_ms": st["sweep_ms"]})
+        roof.update({"phase": top, "kernels": ph["kernels"], "avg_launch_us": ph["avg_launch_us"],
+                     "launches": ph["launches"], "algorithmic_flops_per_launch": flops_l,
+                     "algorithmic_bytes_per_launch": bytes_l, "share_of_timed_region": ph["share_of_timed_region"]})
 
     out = {
         "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": d.world, "steps": iters,
@@ -193,6 +204,7 @@ def main():
                    "factor_ms_total": st["factor_ms"], "solve_ms_total": st["solve_ms"],
                    "refine_passes": st["refine_passes"], "kernel_timing": not args.no_timing},
         "roofline": roof,
+        "phases": phases,
         "cpu_baseline": None,
     }
     if d.rank == 0 and d.world == 1 and args.cpu_iters > 0:

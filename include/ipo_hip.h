@@ -66,6 +66,14 @@ typedef struct {
     long   update_launches, panel_launches;
     double flops_update;     /* algorithmic flops of the gather kernel per factorisation */
     double bytes_update;     /* algorithmic bytes of the gather kernel per factorisation */
+    /* per phase (timing mode): 0 gather (k_update + k_update_reduce), 1 diagonal
+     * block LDL' (k_diag), 2 panel solve (k_trsm), 3 dense-tail trailing update
+     * (k_tail_syrk), 4 forward sweep, 5 backward sweep */
+    double phase_ms[6];      /* device time (HIP events on the solver's stream)      */
+    long   phase_launches[6];/* kernel launches                                       */
+    long   phase_count[6];   /* occurrences (factorisations / sweeps)                 */
+    double phase_flops[6];   /* algorithmic flops of one occurrence                   */
+    double phase_bytes[6];   /* algorithmic bytes of one occurrence                   */
 } ipo_hip_stats;
 
 /* method: 0 = hsd, 1 = intpt.  trace may be NULL (silent).  timing != 0

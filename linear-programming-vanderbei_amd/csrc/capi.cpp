@@ -48,7 +48,8 @@ void print_small(FILE* tr, int m, int n, const int* kA, const int* iA, const dou
     std::fprintf(tr, "\n");
 }
 
-void fill_stats(ipo_hip_stats* st, const ipo::IpmResult& r, const ipo::KktPlan* P) {
+void fill_stats(ipo_hip_stats* st, const ipo::IpmResult& r, const ipo::KktDevice* K) {
+    const ipo::KktPlan* P = K ? &K->plan() : nullptr;
     if (!st) return;
     std::memset(st, 0, sizeof(*st));
     st->iters = r.iters;
@@ -66,11 +67,21 @@ void fill_stats(ipo_hip_stats* st, const ipo::IpmResult& r, const ipo::KktPlan* 
     st->final_dobj = r.final_dobj;
     st->final_pinf = r.final_pinf;
     st->final_dinf = r.final_dinf;
-    st->update_ms = r.kkt.update_ms;
-    st->panel_ms = r.kkt.panel_ms;
+    st->update_ms = r.kkt.phase_ms[ipo::kPhGather];
+    st->panel_ms = r.kkt.phase_ms[ipo::kPhDiag] + r.kkt.phase_ms[ipo::kPhTrsm] + r.kkt.phase_ms[ipo::kPhSyrk];
     st->sweep_ms = r.kkt.sweep_ms;
-    st->update_launches = r.kkt.update_launches;
-    st->panel_launches = r.kkt.panel_launches;
+    st->update_launches = r.kkt.phase_launches[ipo::kPhGather];
+    st->panel_launches = r.kkt.phase_launches[ipo::kPhDiag] + r.kkt.phase_launches[ipo::kPhTrsm] +
+                         r.kkt.phase_launches[ipo::kPhSyrk];
+    for (int ph = 0; ph < ipo::kNumPhases; ph++) {
+        st->phase_ms[ph] = r.kkt.phase_ms[ph];
+        st->phase_launches[ph] = r.kkt.phase_launches[ph];
+        st->phase_count[ph] = r.kkt.phase_count[ph];
+        if (K) {
+            st->phase_flops[ph] = K->work_flops[ph];
+            st->phase_bytes[ph] = K->work_bytes[ph];
+        }
+    }
     if (P) {
         st->flops_update = P->flops_update;
         st->bytes_update = P->bytes_update;
@@ -98,7 +109,7 @@ int solve_impl(ipo::Method method, int m, int n, int nz, const int* iA, const in
         (void)nz;
         const int status = S.run(opt, &res);
         S.download(x, y, w, z);
-        fill_stats(stats, res, &S.kkt().plan());
+        fill_stats(stats, res, &S.kkt());
         return status;
     } catch (const std::exception& e) {
         set_err(e.what());
@@ -164,7 +175,7 @@ int ipo_hip_ctx_run(ipo_hip_ctx* ctx, int method, int max_iter, FILE* trace, int
         opt.timing = timing != 0;
         ipo::IpmResult res;
         const int st = ctx->solver->run(opt, &res);
-        fill_stats(stats, res, &ctx->solver->kkt().plan());
+        fill_stats(stats, res, &ctx->solver->kkt());
         return st;
     } catch (const std::exception& e) {
         set_err(e.what());

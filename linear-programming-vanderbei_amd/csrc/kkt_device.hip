@@ -926,6 +926,60 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dPartialTile_.alloc(std::max<size_t>(1, max_part) * (kTileRows * kTileRows + 4 * kTileRows));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
     }
+    {   // launches per sweep and algorithmic work per phase occurrence
+        fwd_launches_ = bwd_launches_ = 0;
+        for (int l = 0; l < plan_.nlevels; l++) {
+            const int k = chunk_ptr_[l + 1] > chunk_ptr_[l] ? 2 : 1;
+            fwd_launches_ += k;
+            bwd_launches_ += k;
+        }
+        if (plan_.nt > 0) { fwd_launches_ += 1 + plan_.ntb; bwd_launches_ += 1 + plan_.ntb; }
+        const auto& P = plan_;
+        double gf = 0, gb = 0;
+        auto tasks_work = [&](const std::vector<TailTask>& ts) {
+            for (const TailTask& t : ts) {
+                const double ncd = P.col0[t.src + 1] - P.col0[t.src];
+                const double nr = __builtin_popcountll(t.rmask), ncl = __builtin_popcountll(t.cmask);
+                gf += 2.0 * ncd * nr * ncl;
+                gb += 8.0 * ncd * (nr + ncl);
+            }
+        };
+        tasks_work(P.utasks);
+        tasks_work(P.tail_tasks);
+        double df = 0, db = 0, tf = 0, tb = 0, sf = 0, sb = 0, lxs = 0;
+        for (int sp = 0; sp < P.nsup; sp++) {
+            const double nc = P.col0[sp + 1] - P.col0[sp], hb = P.rowptr[sp + 1] - P.rowptr[sp];
+            df += 2.0 * nc * nc * nc / 3.0;
+            db += 8.0 * 1.5 * nc * nc;
+            tf += hb * nc * nc;
+            tb += 16.0 * hb * nc;
+            lxs += (nc + hb) * nc;
+            gb += 16.0 * (nc + hb) * nc;      // read-modify-write of every target panel
+        }
+        for (int kb = 0; kb < P.ntb; kb++) {
+            const double nc = std::min(kPanelCols, P.nt - kb * kPanelCols), below = P.nt - kb * kPanelCols - nc;
+            df += 2.0 * nc * nc * nc / 3.0;
+            db += 8.0 * 1.5 * nc * nc;
+            tf += below * nc * nc;
+            tb += 24.0 * below * nc;                                // L21 read + write, W write
+            const double nb = P.ntb - kb - 1;
+            sf += 2.0 * nc * (nb * (nb + 1) / 2) * kTileRows * kTileRows;
+            sb += (nb * (nb + 1) / 2) * (16.0 * kTileRows * kTileRows + 16.0 * kTileRows * nc);
+        }
+        gb += 16.0 * 0.5 * P.nt * P.nt;                                 // tail block read-modify-write
+        work_flops[kPhGather] = gf; work_bytes[kPhGather] = gb;
+        work_flops[kPhDiag] = df; work_bytes[kPhDiag] = db;
+        work_flops[kPhTrsm] = tf; work_bytes[kPhTrsm] = tb;
+        work_flops[kPhSyrk] = sf; work_bytes[kPhSyrk] = sb;
+        // a sweep reads every factor entry once (sparse panels + the tail's
+        // lower triangle) and the vector / update values it touches
+        const double tail_tri = 0.5 * P.nt * (P.nt + 1.0);
+        const double nrowsR = P.rowptr.empty() ? 0 : P.rowptr.back();
+        for (int ph : {kPhForward, kPhBackward}) {
+            work_flops[ph] = 2.0 * (lxs + tail_tri);
+            work_bytes[ph] = 8.0 * (lxs + tail_tri) + 8.0 * 2 * T_ + (ph == kPhForward ? 12.0 : 12.0) * nrowsR;
+        }
+    }
     dutasks_.upload(reinterpret_cast<const uint64_t*>(plan_.utasks.data()), plan_.utasks.size() * 4, s);
     if (plan_.nt > 0) {
         dtail_task_ptr_.upload(plan_.tail_task_ptr, s);
@@ -1022,41 +1076,41 @@ void KktDevice::factor(const double* dE, const double* dD) {
     if (nz > 0) hipLaunchKernelGGL(k_assemble_A, dim3(ceil_div(nz, NT)), dim3(NT), 0, s, nz, dA_.get(), damap_.get(), dLx_.get());
     hipLaunchKernelGGL(k_assemble_diag, dim3(ceil_div(T_, NT)), dim3(NT), 0, s, T_, m_, dperm_.get(), dE, dD, epsdiag_,
                        ddslot_.get(), dLx_.get(), dLive_.get(), dDscale_.get());
-    if (timing_ && kev_.size() < static_cast<size_t>(4 * plan_.nlevels)) {
-        for (hipEvent_t e : kev_) (void)hipEventDestroy(e);
-        kev_.assign(4 * plan_.nlevels, nullptr);
-        for (hipEvent_t& e : kev_) IPO_HIP_CHECK(hipEventCreate(&e));
-    }
-    std::vector<char> upd_used(timing_ ? plan_.nlevels : 0, 0);
     const TailView tv = tail_view();
     for (int l = 0; l < plan_.nlevels; l++) {
         const int u0 = plan_.unit_level_ptr[l], u1 = plan_.unit_level_ptr[l + 1];
         if (u1 <= u0) continue;
         if (l > 0) {
-            if (timing_) { IPO_HIP_CHECK(hipEventRecord(kev_[4 * l], s)); upd_used[l] = 1; }
-            launch_gather(pv, tv, -1, l, s);
-            if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 1], s));
+            ph_begin(s);
+            const int nl = launch_gather(pv, tv, -1, l, s);
+            ph_end(kPhGather, nl, s);
         }
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
-        if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 2], s));
+        ph_begin(s);
         launch_diag(pv, dlevel_sups_.get(), q0, q1 - q0, tv, 0, s);
+        ph_end(kPhDiag, 1, s);
+        ph_begin(s);
         launch_trsm(pv, u0, u1 - u0, tv, 0, s);
-        if (timing_) IPO_HIP_CHECK(hipEventRecord(kev_[4 * l + 3], s));
+        ph_end(kPhTrsm, 1, s);
     }
     if (plan_.nt > 0) {
-        const int ntiles = plan_.ntb * (plan_.ntb + 1) / 2;
-        if (timing_) IPO_HIP_CHECK(hipEventRecord(ev2_, s));
-        (void)ntiles;
-        launch_gather(pv, tv, 0, plan_.nlevels, s);
-        if (timing_) IPO_HIP_CHECK(hipEventRecord(ev3_, s));
+        ph_begin(s);
+        const int nl = launch_gather(pv, tv, 0, plan_.nlevels, s);
+        ph_end(kPhGather, nl, s);
         for (int kb = 0; kb < plan_.ntb; kb++) {
             const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
+            ph_begin(s);
             launch_diag(pv, nullptr, 0, 1, tv, kb, s);
+            ph_end(kPhDiag, 1, s);
             const int below = plan_.nt - k0 - nc;
             if (below > 0) {
+                ph_begin(s);
                 launch_trsm(pv, 0, -1, tv, kb, s);
+                ph_end(kPhTrsm, 1, s);
                 const int nb = plan_.ntb - kb - 1;
+                ph_begin(s);
                 hipLaunchKernelGGL(k_tail_syrk, dim3(nb * (nb + 1) / 2), dim3(NT), 0, s, pv, tv, kb);
+                ph_end(kPhSyrk, 1, s);
             }
         }
     }
@@ -1072,22 +1126,8 @@ void KktDevice::factor(const double* dE, const double* dD) {
         float ms = 0;
         IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
         tm_.factor_ms += ms;
-        for (int l = 0; l < plan_.nlevels; l++) {
-            if (plan_.unit_level_ptr[l + 1] <= plan_.unit_level_ptr[l]) continue;
-            if (upd_used[l]) {
-                IPO_HIP_CHECK(hipEventElapsedTime(&ms, kev_[4 * l], kev_[4 * l + 1]));
-                tm_.update_ms += ms;
-                tm_.update_launches++;
-            }
-            IPO_HIP_CHECK(hipEventElapsedTime(&ms, kev_[4 * l + 2], kev_[4 * l + 3]));
-            tm_.panel_ms += ms;
-            tm_.panel_launches++;
-        }
-        if (plan_.nt > 0) {
-            IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev2_, ev3_));
-            tm_.tail_update_ms += ms;
-            tm_.tail_update_launches++;
-        }
+        ph_collect();
+        for (int ph : {kPhGather, kPhDiag, kPhTrsm, kPhSyrk}) tm_.phase_count[ph]++;
     }
     tm_.factors++;
     ndep_ = hFlags_[0];
@@ -1096,9 +1136,9 @@ void KktDevice::factor(const double* dE, const double* dD) {
 
 // Gather launches of one level (tail < 0) or of the dense tail (group =
 // nlevels): the chunks, then the in-order reduction of the split units.
-void KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, int group, hipStream_t s) {
+int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, int group, hipStream_t s) {
     const int c0 = ck_ptr_[group], c1 = ck_ptr_[group + 1];
-    if (c1 <= c0) return;
+    if (c1 <= c0) return 0;
     const TailTask* tasks = tail < 0 ? reinterpret_cast<const TailTask*>(dutasks_.get())
                                      : reinterpret_cast<const TailTask*>(dtail_tasks_.get());
     const int* kslot = tail < 0 ? dkslot_.get() : dtail_kslot_.get();
@@ -1108,6 +1148,40 @@ void KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, 
     if (s1 > s0)
         hipLaunchKernelGGL(k_update_reduce, dim3(s1 - s0), dim3(NT), 0, s, pv, tv, tail, dsp_u_.get(), dsp_p0_.get(),
                            dsp_n_.get(), s0, dPartialTile_.get());
+    return s1 > s0 ? 2 : 1;
+}
+
+hipEvent_t KktDevice::next_event() {
+    if (kev_used_ == kev_.size()) {
+        hipEvent_t e;
+        IPO_HIP_CHECK(hipEventCreate(&e));
+        kev_.push_back(e);
+    }
+    return kev_[kev_used_++];
+}
+
+void KktDevice::ph_begin(hipStream_t s) {
+    if (!timing_) return;
+    mark_b_ = next_event();
+    IPO_HIP_CHECK(hipEventRecord(mark_b_, s));
+}
+
+void KktDevice::ph_end(int phase, int launches, hipStream_t s) {
+    if (!timing_) return;
+    hipEvent_t e = next_event();
+    IPO_HIP_CHECK(hipEventRecord(e, s));
+    marks_.push_back({mark_b_, e, phase, launches});
+}
+
+void KktDevice::ph_collect() {
+    for (const PhaseMark& mk : marks_) {
+        float ms = 0;
+        IPO_HIP_CHECK(hipEventElapsedTime(&ms, mk.b, mk.e));
+        tm_.phase_ms[mk.phase] += ms;
+        tm_.phase_launches[mk.phase] += mk.launches;
+    }
+    marks_.clear();
+    kev_used_ = 0;
 }
 
 void KktDevice::rawsolve(double* dz) {
@@ -1124,6 +1198,7 @@ void KktDevice::rawsolve(double* dz) {
         IPO_HIP_CHECK(hipMemsetAsync(epsp, 0, sizeof(double), s));
     }
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev2_, s));
+    ph_begin(s);
     for (int l = 0; l < plan_.nlevels; l++) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         const int cb = chunk_ptr_[l], ce = chunk_ptr_[l + 1];
@@ -1146,6 +1221,12 @@ void KktDevice::rawsolve(double* dz) {
             const int below = nt - std::min(nt, (kb + 1) * kPanelCols);
             hipLaunchKernelGGL(k_tail_fwd, dim3(std::max(1, ceil_div(below, 64))), dim3(NT), 0, s, pv, tv, kb, dz, epsp);
         }
+    }
+    ph_end(kPhForward, fwd_launches_, s);
+    ph_begin(s);
+    if (plan_.nt > 0) {
+        const TailView tv = tail_view();
+        const int nt = plan_.nt;
         hipLaunchKernelGGL(k_tail_dscale, dim3(ceil_div(nt, NT)), dim3(NT), 0, s, pv, tv, dz, epsp);
         for (int kb = plan_.ntb - 1; kb >= 0; kb--) {
             const int left = kb * kPanelCols;
@@ -1164,6 +1245,7 @@ void KktDevice::rawsolve(double* dz) {
             hipLaunchKernelGGL(k_backward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dz, epsp);
         }
     }
+    ph_end(kPhBackward, bwd_launches_, s);
     IPO_HIP_CHECK(hipGetLastError());
     if (timing_) {
         IPO_HIP_CHECK(hipEventRecord(ev3_, s));
@@ -1171,6 +1253,9 @@ void KktDevice::rawsolve(double* dz) {
         float ms = 0;
         IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev2_, ev3_));
         tm_.sweep_ms += ms;
+        ph_collect();
+        tm_.phase_count[kPhForward]++;
+        tm_.phase_count[kPhBackward]++;
     }
     tm_.rawsolves++;
 }

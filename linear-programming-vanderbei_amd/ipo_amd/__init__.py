@@ -49,14 +49,22 @@ class Stats(C.Structure):
         ("update_ms", C.c_double), ("panel_ms", C.c_double), ("sweep_ms", C.c_double),
         ("update_launches", C.c_long), ("panel_launches", C.c_long),
         ("flops_update", C.c_double), ("bytes_update", C.c_double),
+        ("phase_ms", C.c_double * 6), ("phase_launches", C.c_long * 6), ("phase_count", C.c_long * 6),
+        ("phase_flops", C.c_double * 6), ("phase_bytes", C.c_double * 6),
     ]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            d[k] = list(v) if isinstance(v, C.Array) else v
+        return d
 
 
 _lib = None
 _libc = None
+
+PHASES = ["gather", "diag", "trsm", "tail_syrk", "forward", "backward"]
 
 EXPORTED = [
     "solver", "ldltfac", "forwardbackward", "inv_clo",
