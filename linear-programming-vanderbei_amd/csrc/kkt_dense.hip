@@ -16,6 +16,19 @@ constexpr int TR = kTileRows;     // 64
 constexpr int PC = kPanelCols;    // 64
 constexpr int NT = 256;
 
+// What the diagonal-block routines need from the plan, passed by value: a
+// reference to the kernel's PlanView argument would force a copy of it into
+// scratch memory (and a scratch load per use) once a non-inlined callee
+// takes its address.
+struct DiagCtx {
+    double* dscale;
+    double* dg;
+    int* live;
+    int* flags;
+    const int* sign;
+    double tau;
+};
+
 // Thread (row r = lane, part q0 = wave) of a 256-thread workgroup keeps
 // the entries (r, 4q + q0), q = 0..15, of a 64-column row in registers.
 // Column k = 4 qk + pk is visited with qk unrolled (a static register
@@ -28,7 +41,7 @@ constexpr int NT = 256;
 // a pivot fails the zero test, and the caller reruns the block with
 // factor_diag_block, which owns the dependent-pivot rule (ldlt.c:600-614).
 // On success stores L11' in the block's upper triangle, D in dg, mark = 1.
-__device__ __forceinline__ bool factor_diag_fast(const PlanView& p, double* panel, int ld, int nc, int c0,
+__device__ __forceinline__ bool factor_diag_fast(const DiagCtx p, double* panel, int ld, int nc, int c0,
                                                  double (*B)[PC + 1]) {
     __shared__ double colk[PC];
     __shared__ double piv[2];
@@ -87,7 +100,10 @@ __device__ __forceinline__ bool factor_diag_fast(const PlanView& p, double* pane
     return true;
 }
 
-__device__ __attribute__((noinline)) void factor_diag_block(const PlanView& p, double* panel, int ld, int nc, int h, int c0) {
+__device__ __attribute__((noinline)) void factor_diag_block(double* dscale, double* dgp, int* livep, int* flags,
+                                                          const int* sign, double tau, double* panel, int ld, int nc, int h,
+                                                          int c0) {
+    const DiagCtx p{dscale, dgp, livep, flags, sign, tau};
     __shared__ double B[PC][PC + 1];
     __shared__ double dv[PC];
     __shared__ int lv[PC];
@@ -162,7 +178,7 @@ __device__ __attribute__((noinline)) void factor_diag_block(const PlanView& p, d
 // Bl(c, k) = L11(c, k) d_k in LDS.  With wbuf != nullptr also writes
 // W = L21 D (ldw, rows relative to wrow0) for the dense tail's trailing
 // update.  Reference form: l = w / d, w -= l * (l11 * d).
-__device__ void solve_rows(const PlanView& p, double* panel, int ld, int nc, int c0, int rlo, int rhi,
+__device__ void solve_rows(const DiagCtx p, double* panel, int ld, int nc, int c0, int rlo, int rhi,
                            double* wbuf, int ldw, int wrow0) {
     __shared__ double Bl[PC][PC + 1];     // Bl[c][k] = L11(c, k) * d_k
     __shared__ double dv[PC];
@@ -241,10 +257,11 @@ k_diag(PlanView p, const int* __restrict__ level_sups, int q0, TailView tv, int 
         c0 = tv.tc + k0;
         panel = tv.S + k0 + (size_t)k0 * tv.nt;
     }
-    const bool f = factor_diag_fast(p, panel, ld, nc, c0, Bt);
+    const DiagCtx dc{p.dscale, p.dg, p.live, p.flags, p.sign, p.tau};
+    const bool f = factor_diag_fast(dc, panel, ld, nc, c0, Bt);
     if (threadIdx.x == 0) ok = f;
     __syncthreads();
-    if (!ok) factor_diag_block(p, panel, ld, nc, h, c0);
+    if (!ok) factor_diag_block(p.dscale, p.dg, p.live, p.flags, p.sign, p.tau, panel, ld, nc, h, c0);
 }
 
 __global__ void __launch_bounds__(NT)
@@ -274,7 +291,7 @@ k_trsm(PlanView p, int u0, TailView tv, int kb) {
         wrow0 = rlo;
     }
     if (rhi <= rlo) return;
-    solve_rows(p, panel, ld, nc, c0, rlo, rhi, wbuf, ldw, wrow0);
+    solve_rows(DiagCtx{p.dscale, p.dg, p.live, p.flags, p.sign, p.tau}, panel, ld, nc, c0, rlo, rhi, wbuf, ldw, wrow0);
 }
 
 }  // namespace

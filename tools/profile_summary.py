@@ -1,0 +1,80 @@
+"""Turn the rocprofv3 databases of tools/profile_round.sh into the files
+committed under profiles/ (developer tool).
+
+  profiles/<tag>_kernel_stats.csv   top_kernels of the --kernel-trace --stats run
+                                    (name, calls, total_us, avg_us, percent)
+  profiles/<tag>_pmc_traffic.json   HBM bytes per launch from the FETCH_SIZE /
+                                    WRITE_SIZE passes, per kernel and per phase
+  profiles/<tag>_bench.json         the bench.py JSON line of the same run
+
+FETCH_SIZE on gfx950 counts half of the bytes of wide streaming reads
+(MI355X_MICROARCH.md, HBM section): it is doubled here; WRITE_SIZE is taken
+as reported.  Both are KB in rocprofv3.
+usage: python tools/profile_summary.py r01 [gpurun_out]"""
+import csv
+import json
+import os
+import re
+import sqlite3
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from bench import PHASE_KERNELS  # noqa: E402
+
+tag = sys.argv[1]
+src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "gpurun_out")
+dst = os.path.join(REPO, "profiles")
+os.makedirs(dst, exist_ok=True)
+
+
+def short(name):
+    return name.replace("ipo::(anonymous namespace)::", "").replace("ipo::", "").split("(")[0]
+
+
+c = sqlite3.connect(os.path.join(src, f"{tag}_trace", "run_results.db"))
+rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels "
+                      "order by total_duration desc"))
+with open(os.path.join(dst, f"{tag}_kernel_stats.csv"), "w", newline="") as fh:
+    w = csv.writer(fh)
+    w.writerow(["kernel", "calls", "total_us", "avg_us", "percent"])
+    for n, calls, tot, avg, pct in rows:
+        w.writerow([short(n), calls, f"{tot:.1f}", f"{avg:.2f}", f"{pct:.2f}"])
+
+
+def per_kernel(db, counter):
+    c = sqlite3.connect(db)
+    acc = {}
+    for name, val in c.execute("select kernel_name, value from counters_collection where counter_name = ?",
+                               (counter,)):
+        k = short(name)
+        s, n = acc.get(k, (0.0, 0))
+        acc[k] = (s + val, n + 1)
+    return acc
+
+
+fetch = per_kernel(os.path.join(src, f"{tag}_pmc_fetch", "run_results.db"), "FETCH_SIZE")
+write = per_kernel(os.path.join(src, f"{tag}_pmc_write", "run_results.db"), "WRITE_SIZE")
+kern = {}
+for k in sorted(set(fetch) | set(write)):
+    fs, fn = fetch.get(k, (0.0, 0))
+    ws, wn = write.get(k, (0.0, 0))
+    n = max(fn, wn, 1)
+    kern[k] = {"launches": n, "fetch_bytes_per_launch": 2 * 1024 * fs / max(fn, 1),
+               "write_bytes_per_launch": 1024 * ws / max(wn, 1)}
+    kern[k]["hbm_bytes_per_launch"] = kern[k]["fetch_bytes_per_launch"] + kern[k]["write_bytes_per_launch"]
+phases = {}
+for ph, names in PHASE_KERNELS.items():
+    ks = [k for k in re.split(r"[|+]", names) if k in kern]
+    tot = sum(kern[k]["hbm_bytes_per_launch"] * kern[k]["launches"] for k in ks)
+    nl = sum(kern[k]["launches"] for k in ks)
+    if nl:
+        phases[ph] = {"kernels": ks, "launches": nl, "hbm_bytes_per_launch": tot / nl}
+with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:
+    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, bench.py --steps 10 --no-timing "
+                         "(dfl001 hsd, first 10 iterations); FETCH_SIZE doubled (gfx950)",
+               "phases": phases, "kernels": kern}, fh, indent=1)
+line = [ln for ln in open(os.path.join(src, f"{tag}_bench.log")) if ln.startswith("{")][-1]
+with open(os.path.join(dst, f"{tag}_bench.json"), "w") as fh:
+    fh.write(line)
+print("wrote", dst)
