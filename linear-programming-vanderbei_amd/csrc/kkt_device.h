@@ -140,7 +140,9 @@ class KktDevice {
     // split-K gather chunks per group (sparse level l, group nlevels = tail)
     std::vector<int> ck_ptr_, sp_ptr_;
     DevBuf<int> dck_u_, dck_b_, dck_e_, dck_part_, dsp_u_, dsp_p0_, dsp_n_;
-    DevBuf<double> dPartialTile_;      // forward-sweep update values, one per row of every R_s
+    DevBuf<double> dPartialTile_;
+    DevBuf<int> dChainFlags_;    // dense-tail sweep chains: per block, epoch of the last completed sweep
+    int chain_epoch_ = 0;      // forward-sweep update values, one per row of every R_s
     DevBuf<int> dtail_task_ptr_, dkslot_, dkslot_ptr_, dtail_kslot_, dtail_kslot_ptr_;
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;

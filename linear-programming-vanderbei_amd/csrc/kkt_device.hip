@@ -447,8 +447,19 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
         const int k = base + (tid >> 2), part = tid & 3;
         double acc = 0.0;
         if (k < nc) {
+            // four entries in flight per thread: index loads first, then values
             const int v = c0 + k;
-            for (int e = yrow_ptr[v] + part; e < yrow_ptr[v + 1]; e += 4) acc += ybuf[yrow_idx[e]];
+            const int e1 = yrow_ptr[v + 1];
+            int e = yrow_ptr[v] + part;
+            for (; e + 12 < e1; e += 16) {
+                const int i0 = yrow_idx[e], i1 = yrow_idx[e + 4], i2 = yrow_idx[e + 8], i3 = yrow_idx[e + 12];
+                const double y0 = ybuf[i0], y1 = ybuf[i1], y2 = ybuf[i2], y3 = ybuf[i3];
+                acc += y0;
+                acc += y1;
+                acc += y2;
+                acc += y3;
+            }
+            for (; e < e1; e += 4) acc += ybuf[yrow_idx[e]];
         }
         const double o1 = __shfl_xor(acc, 1, 64);
         const double pr = (part & 1) ? o1 + acc : acc + o1;
@@ -610,27 +621,32 @@ k_bwd_partial(PlanView p, const int* __restrict__ chunk_sup, const int* __restri
 }
 
 // part 2: one wave per supernode sums its chunks in order, then D^{-1} and L11'.
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(NT)
 k_bwd_finish(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ sup_chunk0,
              const double* __restrict__ part, double* __restrict__ z, const double* __restrict__ epsp) {
     __shared__ double Ls[PC][PC + 1];
     __shared__ int lv[PC];
+    __shared__ double xs[4][PC];
     const int s = level_sups[q0 + blockIdx.x];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     stage_l11(p.Lx + p.off[s], h, nc, Ls);
-    if (lane < nc) lv[lane] = p.live[c0 + lane];
+    if (tid < nc) lv[tid] = p.live[c0 + tid];
+    {   // wave w sums chunks w, w+4, ...; the four partials are added in wave order
+        const int cf = sup_chunk0[s], nch = (hb + 63) / 64;
+        double x = 0.0;
+        if (lane < nc)
+            for (int c = wv; c < nch; c += 4) x += part[(size_t)(cf + c) * PC + lane];
+        xs[wv][lane] = x;
+    }
     __syncthreads();
+    if (wv != 0) return;
     const double eps = *epsp;
     int bad = 0;
     double zr = 0.0;
-    if (lane < nc) {
-        const int cf = sup_chunk0[s], nch = (hb + 63) / 64;
-        double x = 0.0;
-        for (int c = 0; c < nch; c++) x += part[(size_t)(cf + c) * PC + lane];
-        zr = dscale_rule(p, c0 + lane, z[c0 + lane], eps, bad) - x;
-    }
+    if (lane < nc)
+        zr = dscale_rule(p, c0 + lane, z[c0 + lane], eps, bad) - (((xs[0][lane] + xs[1][lane]) + xs[2][lane]) + xs[3][lane]);
     zr = tri_upper(zr, Ls, lv, nc, eps, bad);
     if (lane < nc) z[c0 + lane] = zr;
     if (bad) atomicOr(&p.flags[1], 1);
@@ -744,6 +760,136 @@ k_tail_bwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double
     red[wv][lane] = acc;
     __syncthreads();
     if (wv == 0 && j < k0) z[tc + j] = z[tc + j] - (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+}
+
+// ------------------------------------------- dense-tail sweeps, one launch
+// Sync-free block-row chains: workgroup i owns 64-row block i of the tail
+// and waits, block by block, for the blocks it depends on (flags[j] ==
+// epoch).  Hand-off per MI355X_MICROARCH.md (inter-workgroup visibility,
+// table row 1): the producer stores its block with sc1 stores (relaxed
+// agent-scope atomics), waits vmcnt(0), joins a barrier, and one lane
+// stores the flag sc1; the consumer polls the flag with sc1 loads from one
+// lane, joins a barrier and reads the block with sc1 loads.  One
+// workgroup per CU is enforced with dynamic LDS.  Every workgroup only
+// waits on blocks of lower rank in its own launch order, so the grid
+// drains as long as it is resident (ntb <= kChainMaxBlocks).
+constexpr int kChainMaxBlocks = 200;
+constexpr size_t kChainLds = 96 * 1024;
+
+__device__ __forceinline__ void sc1_store(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double sc1_load(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void chain_wait(const int* flags, int j, int epoch) {
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(const_cast<int*>(flags + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch)
+            __builtin_amdgcn_s_sleep(1);
+    __syncthreads();
+}
+__device__ __forceinline__ void chain_publish(int* flags, int i, int epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flags + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// forward: z_i -= sum_{j<i} L(i, j) z_j, then the unit-lower L11 solve of block i
+__global__ void __launch_bounds__(NT)
+k_tail_fwd_chain(PlanView p, TailView tv, double* __restrict__ z, const double* __restrict__ epsp,
+                 int* __restrict__ flags, int epoch) {
+    extern __shared__ double lds_pad[];
+    __shared__ double Ls[PC][PC + 1];
+    __shared__ int lv[PC];
+    __shared__ double zb[PC];
+    __shared__ double red[4][64];
+    const int nt = tv.nt, tc = tv.tc, i = blockIdx.x, k0 = i * PC, nc = min(PC, nt - k0);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) lds_pad[0] = 0.0;
+    stage_l11(tv.S + k0 + (size_t)k0 * nt, nt, nc, Ls);
+    if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
+    const int row = k0 + (lane < nc ? lane : 0);
+    double acc = 0.0;
+    for (int j = 0; j < i; j++) {
+        // the L(i, j) tile does not depend on z: load it before waiting
+        const double* __restrict__ col = tv.S + row + (size_t)(j * PC + wv * 16) * nt;
+        double t[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) t[q] = col[(size_t)q * nt];
+        chain_wait(flags, j, epoch);
+        if (tid < PC) zb[tid] = sc1_load(z + tc + j * PC + tid);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc += t[q] * zb[wv * 16 + q];
+        __syncthreads();
+    }
+    red[wv][lane] = acc;
+    __syncthreads();
+    if (wv == 0) {
+        int bad = 0;
+        double zr = 0.0;
+        if (lane < nc) zr = z[tc + k0 + lane] - (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
+        zr = tri_lower(zr, Ls, lv, nc, *epsp, bad);
+        if (lane < nc) sc1_store(z + tc + k0 + lane, zr);
+        if (bad) atomicOr(&p.flags[1], 1);
+    }
+    chain_publish(flags, i, epoch);
+}
+
+// backward (launch order = blocks from the last): z_i = D^{-1} z_i
+// - sum_{j>i} L(j, i)' z_j, then the L11' solve.  Wave w owns 16 columns of
+// block i, lanes stride the rows of block j (coalesced column reads).
+__global__ void __launch_bounds__(NT)
+k_tail_bwd_chain(PlanView p, TailView tv, double* __restrict__ z, const double* __restrict__ epsp,
+                 int* __restrict__ flags, int epoch) {
+    extern __shared__ double lds_pad[];
+    __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L(j, r)
+    __shared__ int lv[PC];
+    __shared__ double zb[PC];
+    __shared__ double xs[PC];
+    const int nt = tv.nt, tc = tv.tc, ntb = tv.ntb;
+    const int i = ntb - 1 - blockIdx.x, k0 = i * PC, nc = min(PC, nt - k0);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) lds_pad[0] = 0.0;
+    stage_l11(tv.S + k0 + (size_t)k0 * nt, nt, nc, Ls);
+    if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
+    const int kq = wv * 16, nq = min(16, nc - kq);
+    double acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) acc[q] = 0.0;
+    for (int j = ntb - 1; j > i; j--) {
+        const int r0 = j * PC, nr = min(PC, nt - r0);
+        const int rr = r0 + (lane < nr ? lane : 0);
+        const double* __restrict__ col = tv.S + rr + (size_t)(k0 + (nq > 0 ? kq : 0)) * nt;
+        double t[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, max(nq, 1) - 1) * nt];
+        chain_wait(flags, j, epoch);
+        if (tid < PC) zb[tid] = tid < nr ? sc1_load(z + tc + r0 + tid) : 0.0;
+        __syncthreads();
+        const double zr = lane < nr ? zb[lane] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc[q] += t[q] * zr;
+        __syncthreads();
+    }
+    if (nq > 0) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const double v = wave_sum(acc[q]);
+            if (lane == 0 && q < nq) xs[kq + q] = v;
+        }
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const double eps = *epsp;
+        int bad = 0;
+        double zr = 0.0;
+        if (lane < nc) zr = dscale_rule(p, tc + k0 + lane, z[tc + k0 + lane], eps, bad) - (i < ntb - 1 ? xs[lane] : 0.0);
+        zr = tri_upper(zr, Ls, lv, nc, eps, bad);
+        if (lane < nc) sc1_store(z + tc + k0 + lane, zr);
+        if (bad) atomicOr(&p.flags[1], 1);
+    }
+    chain_publish(flags, i, epoch);
 }
 
 // -------------------------------------------------------- refinement glue
@@ -933,7 +1079,11 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             fwd_launches_ += k;
             bwd_launches_ += k;
         }
-        if (plan_.nt > 0) { fwd_launches_ += 1 + plan_.ntb; bwd_launches_ += 1 + plan_.ntb; }
+        if (plan_.nt > 0) {
+            const int chain = plan_.ntb <= kChainMaxBlocks;
+            fwd_launches_ += 1 + (chain ? 1 : plan_.ntb);
+            bwd_launches_ += chain ? 1 : 1 + plan_.ntb;
+        }
         const auto& P = plan_;
         double gf = 0, gb = 0;
         auto tasks_work = [&](const std::vector<TailTask>& ts) {
@@ -988,6 +1138,14 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         static_assert(sizeof(TailTask) == 32, "TailTask layout");
         dtail_tasks_.upload(reinterpret_cast<const uint64_t*>(plan_.tail_tasks.data()), plan_.tail_tasks.size() * 4, s);
         dW_.alloc(static_cast<size_t>(plan_.nt) * kPanelCols);
+        dChainFlags_.alloc(plan_.ntb);
+        IPO_HIP_CHECK(hipMemsetAsync(dChainFlags_.get(), 0, plan_.ntb * sizeof(int), s));
+        if (plan_.ntb <= kChainMaxBlocks) {
+            IPO_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tail_fwd_chain),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
+            IPO_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tail_bwd_chain),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
+        }
     }
 
     dLx_.alloc(plan_.lx_size > 0 ? plan_.lx_size : 1);
@@ -1217,9 +1375,15 @@ void KktDevice::rawsolve(double* dz) {
         const int nt = plan_.nt;
         hipLaunchKernelGGL(k_tail_gather, dim3(ceil_div(nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(), dyrow_idx_.get(),
                            dYbuf_.get(), dz);
-        for (int kb = 0; kb < plan_.ntb; kb++) {
-            const int below = nt - std::min(nt, (kb + 1) * kPanelCols);
-            hipLaunchKernelGGL(k_tail_fwd, dim3(std::max(1, ceil_div(below, 64))), dim3(NT), 0, s, pv, tv, kb, dz, epsp);
+        if (plan_.ntb <= kChainMaxBlocks) {
+            hipLaunchKernelGGL(k_tail_fwd_chain, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, dz, epsp,
+                               dChainFlags_.get(), ++chain_epoch_);
+        } else {
+            for (int kb = 0; kb < plan_.ntb; kb++) {
+                const int below = nt - std::min(nt, (kb + 1) * kPanelCols);
+                hipLaunchKernelGGL(k_tail_fwd, dim3(std::max(1, ceil_div(below, 64))), dim3(NT), 0, s, pv, tv, kb, dz,
+                                   epsp);
+            }
         }
     }
     ph_end(kPhForward, fwd_launches_, s);
@@ -1227,10 +1391,16 @@ void KktDevice::rawsolve(double* dz) {
     if (plan_.nt > 0) {
         const TailView tv = tail_view();
         const int nt = plan_.nt;
-        hipLaunchKernelGGL(k_tail_dscale, dim3(ceil_div(nt, NT)), dim3(NT), 0, s, pv, tv, dz, epsp);
-        for (int kb = plan_.ntb - 1; kb >= 0; kb--) {
-            const int left = kb * kPanelCols;
-            hipLaunchKernelGGL(k_tail_bwd, dim3(std::max(1, ceil_div(left, 64))), dim3(NT), 0, s, pv, tv, kb, dz, epsp);
+        if (plan_.ntb <= kChainMaxBlocks) {
+            hipLaunchKernelGGL(k_tail_bwd_chain, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, dz, epsp,
+                               dChainFlags_.get(), ++chain_epoch_);
+        } else {
+            hipLaunchKernelGGL(k_tail_dscale, dim3(ceil_div(nt, NT)), dim3(NT), 0, s, pv, tv, dz, epsp);
+            for (int kb = plan_.ntb - 1; kb >= 0; kb--) {
+                const int left = kb * kPanelCols;
+                hipLaunchKernelGGL(k_tail_bwd, dim3(std::max(1, ceil_div(left, 64))), dim3(NT), 0, s, pv, tv, kb, dz,
+                                   epsp);
+            }
         }
     }
     for (int l = plan_.nlevels - 1; l >= 0; l--) {
@@ -1239,7 +1409,7 @@ void KktDevice::rawsolve(double* dz) {
         if (ce > cb) {
             hipLaunchKernelGGL(k_bwd_partial, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(), cb,
                                dz, dPartial_.get());
-            hipLaunchKernelGGL(k_bwd_finish, dim3(q1 - q0), dim3(64), 0, s, pv, dlevel_sups_.get(), q0,
+            hipLaunchKernelGGL(k_bwd_finish, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
                                dsup_chunk0_.get(), dPartial_.get(), dz, epsp);
         } else {
             hipLaunchKernelGGL(k_backward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dz, epsp);
