@@ -75,15 +75,18 @@ __device__ __forceinline__ bool factor_diag_fast(const DiagCtx p, double* panel,
             }
             __syncthreads();
             if (r > k && r < nc) {
+                // all LDS reads first, then branch-free selects
                 const double lr = colk[r];
+                double ck[16];
+#pragma unroll
+                for (int q = qk; q < 16; q++) ck[q] = colk[4 * q + q0];
 #pragma unroll
                 for (int q = qk; q < 16; q++) {
                     const int c = 4 * q + q0;
-                    if (c > k && c <= r) {
-                        const double tk = lr * (colk[c] * dk);
-                        a[q] -= tk;
-                        if (c == r) dsc += fabs(tk);
-                    }
+                    const double tk = lr * (ck[q] * dk);
+                    const bool u = c > k && c <= r;
+                    a[q] = u ? a[q] - tk : a[q];
+                    dsc = (u && c == r) ? dsc + fabs(tk) : dsc;
                 }
             }
         }
@@ -214,10 +217,13 @@ __device__ void solve_rows(const DiagCtx p, double* panel, int ld, int nc, int c
             }
             __syncthreads();
             const double l = lk[r];
+            double bk[16];
+#pragma unroll
+            for (int q = qk; q < 16; q++) bk[q] = Bl[4 * q + q0][k];
 #pragma unroll
             for (int q = qk; q < 16; q++) {
                 const int c = 4 * q + q0;
-                if (c > k) a[q] -= l * Bl[c][k];          // Bl = 0 beyond nc
+                a[q] = c > k ? a[q] - l * bk[q] : a[q];   // Bl = 0 beyond nc
             }
             __syncthreads();
         }
@@ -233,6 +239,7 @@ __device__ void solve_rows(const DiagCtx p, double* panel, int ld, int nc, int c
         }
     }
 }
+
 
 // one kernel for both the sparse panels (level_sups != nullptr) and the
 // dense tail, so the unrolled fast path is compiled once
