@@ -18,8 +18,9 @@ extern "C" {
 #endif
 
 /* ---- METHOD plug-in ------------------------------------------------------
- * Replaces solver() of src/ipo/hsd.c:27-29 (default, like makefile:57) and
- * src/ipo/intpt.c:33-35 (set IPO_HIP_METHOD=intpt); prototype from
+ * Replaces solver() of src/ipo/hsd.c:27-29 (default, like makefile:57),
+ * src/ipo/intpt.c:33-35 (set IPO_HIP_METHOD=intpt) and src/ipo/hsdls.c:38-40
+ * (IPO_HIP_METHOD=hsdls); prototype from
  * src/common/solve.c:24-26.  Solves  max c'x + f  s.t.  Ax <= b, x >= 0,
  * A m x n CSC (kA[n+1], iA[nz], A[nz]), 0-based.  x, z: n; y, w: m (the
  * caller may allocate more, as solve.c:194-197 does).  Prints the banner
@@ -76,7 +77,7 @@ typedef struct {
     double phase_bytes[6];   /* algorithmic bytes of one occurrence                   */
 } ipo_hip_stats;
 
-/* method: 0 = hsd, 1 = intpt.  trace may be NULL (silent).  timing != 0
+/* method: 0 = hsd, 1 = intpt, 2 = hsdls.  trace may be NULL (silent).  timing != 0
  * records per-phase HIP-event times. */
 int ipo_hip_solve(int method, int m, int n, int nz, const int *iA, const int *kA, const double *A,
                   const double *b, const double *c, double f, double *x, double *y, double *w, double *z,

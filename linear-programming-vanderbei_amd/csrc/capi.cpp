@@ -27,8 +27,16 @@ const char* kStatusText[] = {"optimal solution", "primal unbounded", "primal inf
 ipo::Method method_from_env() {
     const char* e = std::getenv("IPO_HIP_METHOD");
     if (e && !std::strcmp(e, "intpt")) return ipo::Method::Intpt;
+    if (e && !std::strcmp(e, "hsdls")) return ipo::Method::Hsdls;
     return ipo::Method::Hsd;
 }
+
+ipo::Method method_from_int(int m) {
+    return m == 1 ? ipo::Method::Intpt : m == 2 ? ipo::Method::Hsdls : ipo::Method::Hsd;
+}
+
+// MAX_ITER of each method: hsd.c:25, intpt.c:31, hsdls.c:25
+int default_max_iter(ipo::Method m) { return m == ipo::Method::Hsdls ? 600 : 200; }
 
 // hsd.c:70-92 / intpt.c:70-92: tiny problems are echoed before the banner
 void print_small(FILE* tr, int m, int n, const int* kA, const int* iA, const double* A, const double* b,
@@ -98,12 +106,12 @@ int solve_impl(ipo::Method method, int m, int n, int nz, const int* iA, const in
                const double* b, const double* c, double f, double* x, double* y, double* w, double* z, FILE* trace,
                int max_iter, int timing, ipo_hip_stats* stats) {
     try {
-        print_small(trace, m, n, kA, iA, A, b, c);
+        if (method != ipo::Method::Hsdls) print_small(trace, m, n, kA, iA, A, b, c);   // hsdls.c has no echo
         ipo::IpmSolver S(m, n, kA, iA, A, b, c, f);
         ipo::IpmOptions opt;
         opt.method = method;
         opt.trace = trace;
-        opt.max_iter = max_iter > 0 ? max_iter : 200;
+        opt.max_iter = max_iter > 0 ? max_iter : default_max_iter(method);
         opt.timing = timing != 0;
         ipo::IpmResult res;
         (void)nz;
@@ -144,13 +152,13 @@ extern "C" {
 
 int solver(int m, int n, int nz, int* iA, int* kA, double* A, double* b, double* c, double f, double* x, double* y,
            double* w, double* z) {
-    return solve_impl(method_from_env(), m, n, nz, iA, kA, A, b, c, f, x, y, w, z, stdout, 200, 0, nullptr);
+    return solve_impl(method_from_env(), m, n, nz, iA, kA, A, b, c, f, x, y, w, z, stdout, 0, 0, nullptr);
 }
 
 int ipo_hip_solve(int method, int m, int n, int nz, const int* iA, const int* kA, const double* A, const double* b,
                   const double* c, double f, double* x, double* y, double* w, double* z, FILE* trace, int max_iter,
                   int timing, ipo_hip_stats* stats) {
-    return solve_impl(method == 1 ? ipo::Method::Intpt : ipo::Method::Hsd, m, n, nz, iA, kA, A, b, c, f, x, y, w, z,
+    return solve_impl(method_from_int(method), m, n, nz, iA, kA, A, b, c, f, x, y, w, z,
                       trace, max_iter, timing, stats);
 }
 
@@ -169,9 +177,9 @@ ipo_hip_ctx* ipo_hip_ctx_create(int m, int n, const int* kA, const int* iA, cons
 int ipo_hip_ctx_run(ipo_hip_ctx* ctx, int method, int max_iter, FILE* trace, int timing, ipo_hip_stats* stats) {
     try {
         ipo::IpmOptions opt;
-        opt.method = method == 1 ? ipo::Method::Intpt : ipo::Method::Hsd;
+        opt.method = method_from_int(method);
         opt.trace = trace;
-        opt.max_iter = max_iter > 0 ? max_iter : 200;
+        opt.max_iter = max_iter > 0 ? max_iter : default_max_iter(opt.method);
         opt.timing = timing != 0;
         ipo::IpmResult res;
         const int st = ctx->solver->run(opt, &res);
@@ -228,7 +236,7 @@ int ipo_hip_run_mps(const char* path, int method, FILE* out, int timing, ipo_hip
             std::fprintf(out, "\n");
         }
         std::vector<double> x(s.n + s.m, 0.0), y(s.n + s.m, 0.0), w(s.m > 0 ? s.m : 1, 0.0), z(s.n > 0 ? s.n : 1, 0.0);
-        status = solve_impl(method == 1 ? ipo::Method::Intpt : ipo::Method::Hsd, s.m, s.n, s.nz, s.iA.data(),
+        status = solve_impl(method_from_int(method), s.m, s.n, s.nz, s.iA.data(),
                             s.kA.data(), s.A.data(), s.b.data(), s.c.data(), s.f, x.data(), y.data(), w.data(),
                             z.data(), out, 200, timing, stats);
     }

@@ -2,6 +2,7 @@
 //
 //   Method::Hsd    homogeneous self-dual predictor-corrector, src/ipo/hsd.c:27-311
 //   Method::Intpt  primal-dual path following,               src/ipo/intpt.c:33-261
+//   Method::Hsdls  homogeneous self-dual long step,          src/ipo/hsdls.c:38-296
 //
 // The host keeps the handful of scalars the reference keeps (phi, psi, mu,
 // theta, ...) and prints the reference's per-iteration trace; every O(m+n)
@@ -17,11 +18,11 @@
 
 namespace ipo {
 
-enum class Method { Hsd = 0, Intpt = 1 };
+enum class Method { Hsd = 0, Intpt = 1, Hsdls = 2 };
 
 struct IpmOptions {
     Method method = Method::Hsd;
-    int max_iter = 200;          // MAX_ITER, hsd.c:25 / intpt.c:31
+    int max_iter = 200;          // MAX_ITER, hsd.c:25 / intpt.c:31 (hsdls.c:25: 600)
     FILE* trace = nullptr;       // banner + one line per iteration, reference format
     bool timing = false;         // per-phase HIP-event timing
 };
@@ -53,6 +54,7 @@ class IpmSolver {
   private:
     int run_hsd(const IpmOptions& opt, IpmResult* res);
     int run_intpt(const IpmOptions& opt, IpmResult* res);
+    int run_hsdls(const IpmOptions& opt, IpmResult* res);
     void reduce(const struct RedJobs& j, int nout);
 
     int m_, n_;

@@ -113,6 +113,55 @@ k_unscale(int m, int n, double phi, double* __restrict__ x, double* __restrict__
     else if (i < n + m) { const int j = i - n; y[j] /= phi; w[j] /= phi; }
 }
 
+// ---------------------------------------------------------------- hsdls
+// hsdls.c:298-336: largest step keeping x z >= (1-beta) mu along the direction
+__device__ __forceinline__ double ls_step(double xj, double zj, double dxj, double dzj, double beta, double delta,
+                                          double mu) {
+    const double a = dxj * dzj;
+    const double b = zj * dxj + xj * dzj + (1 - beta) * (1 - delta) * mu;
+    const double c = xj * zj - (1 - beta) * mu;
+    const double d = b * b - 4 * a * c;
+    if (a == 0.0) return -c / b;
+    if (a > 0) {
+        if (b < 0) {
+            if (d >= 0) return 2 * c / (-b + sqrt(d));
+            return HUGE_VAL;
+        }
+        return HUGE_VAL;
+    }
+    if (b < 0) return 2 * c / (-b + sqrt(d));
+    return (-b - sqrt(d)) / (2 * a);
+}
+
+// directions (hsdls.c:209-215) + the linesearch minimum (hsdls.c:221-230),
+// returned as a max of -step so the common max finisher applies
+__global__ void __launch_bounds__(NT)
+k_hsdls_directions(int m, int n, double dphi, double beta, double delta, double mu, const double* __restrict__ fx,
+                   const double* __restrict__ gx, const double* __restrict__ fy, const double* __restrict__ gy,
+                   const double* __restrict__ x, const double* __restrict__ z, const double* __restrict__ y,
+                   const double* __restrict__ w, const double* __restrict__ D, const double* __restrict__ E,
+                   double* __restrict__ dx, double* __restrict__ dz, double* __restrict__ dy, double* __restrict__ dw,
+                   double* __restrict__ part) {
+    __shared__ double sh[4];
+    double th = -HUGE_VAL;
+    for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
+        if (i < n) {
+            const double ddx = fx[i] - gx[i] * dphi;
+            const double ddz = delta * mu / x[i] - z[i] - D[i] * ddx;
+            dx[i] = ddx; dz[i] = ddz;
+            th = fmax(th, -ls_step(x[i], z[i], ddx, ddz, beta, delta, mu));
+        } else {
+            const int j = i - n;
+            const double ddy = fy[j] - gy[j] * dphi;
+            const double ddw = delta * mu / y[j] - w[j] - E[j] * ddy;
+            dy[j] = ddy; dw[j] = ddw;
+            th = fmax(th, -ls_step(y[j], w[j], ddy, ddw, beta, delta, mu));
+        }
+    }
+    th = block_max(th, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = th;
+}
+
 // ---------------------------------------------------------------- intpt
 // rho = b - A x - w, sigma = c - A'y + z and their squared norms (intpt.c:139-149)
 __global__ void __launch_bounds__(NT)
@@ -179,6 +228,18 @@ k_pf_directions(int m, int n, double mu, const double* __restrict__ x, const dou
     }
     th = block_max(th, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = th;
+}
+
+// host copy of ls_step for the (phi, psi) pair (hsdls.c:229)
+double ls_step_host(double xj, double zj, double dxj, double dzj, double beta, double delta, double mu) {
+    const double a = dxj * dzj;
+    const double b = zj * dxj + xj * dzj + (1 - beta) * (1 - delta) * mu;
+    const double c = xj * zj - (1 - beta) * mu;
+    const double d = b * b - 4 * a * c;
+    if (a == 0.0) return -c / b;
+    if (a > 0) return (b < 0 && d >= 0) ? 2 * c / (-b + std::sqrt(d)) : HUGE_VAL;
+    if (b < 0) return 2 * c / (-b + std::sqrt(d));
+    return (-b - std::sqrt(d)) / (2 * a);
 }
 
 double now_s() {
@@ -248,7 +309,9 @@ int IpmSolver::run(const IpmOptions& opt, IpmResult* res) {
     res->t_setup_s = t_setup_;
     kkt_->enable_timing(opt.timing);
     const double t0 = now_s();
-    const int st = opt.method == Method::Intpt ? run_intpt(opt, res) : run_hsd(opt, res);
+    const int st = opt.method == Method::Intpt   ? run_intpt(opt, res)
+                   : opt.method == Method::Hsdls ? run_hsdls(opt, res)
+                                                 : run_hsd(opt, res);
     res->t_solve_s = now_s() - t0;
     res->status = st;
     res->kkt = kkt_->timers();
@@ -336,6 +399,103 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
         if (theta < -dphi / phi) theta = -dphi / phi;
         if (theta < -dpsi / psi) theta = -dpsi / psi;
         theta = (0.95 / theta > 1.0) ? 1.0 : 0.95 / theta;
+
+        hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, theta, x_.get(), dx_.get(), z_.get(), dz_.get(),
+                           y_.get(), dy_.get(), w_.get(), dw_.get());
+        phi = phi + theta * dphi;
+        psi = psi + theta * dpsi;
+    }
+    hipLaunchKernelGGL(k_unscale, dim3(gv), dim3(NT), 0, s, m, n, phi, x_.get(), z_.get(), y_.get(), w_.get());
+    IPO_HIP_CHECK(hipGetLastError());
+    IPO_HIP_CHECK(hipStreamSynchronize(s));
+    res->iters = iter;
+    res->phi = phi;
+    res->psi = psi;
+    return status;
+}
+
+// hsdls.c:38-296 -- same residuals and solves as HSD with a fixed centring
+// delta = 2 (1 - beta), beta = 0.8, and a quadratic linesearch for theta
+int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
+    const int m = m_, n = n_;
+    hipStream_t s = stream_;
+    const int gv = ceil_div(m + n, NT);
+    FILE* tr = opt.trace;
+    hipLaunchKernelGGL(k_fill, dim3(ceil_div(n, NT)), dim3(NT), 0, s, n, 1.0, x_.get());
+    hipLaunchKernelGGL(k_fill, dim3(ceil_div(n, NT)), dim3(NT), 0, s, n, 1.0, z_.get());
+    hipLaunchKernelGGL(k_fill, dim3(ceil_div(m, NT)), dim3(NT), 0, s, m, 1.0, w_.get());
+    hipLaunchKernelGGL(k_fill, dim3(ceil_div(m, NT)), dim3(NT), 0, s, m, 1.0, y_.get());
+    double phi = 1.0, psi = 1.0;
+    if (tr) {
+        std::fprintf(tr, "m = %d,n = %d,nz = %d\n", m, n, (int)kkt_->plan().amap.size());
+        std::fputs(kHsdHeader, tr);
+        std::fflush(tr);
+    }
+    const double beta = 0.80, delta = 2 * (1 - beta);
+    KktDevice& K = *kkt_;
+    int status = 5, iter;
+    for (iter = 0; iter < opt.max_iter; iter++) {
+        RedJobs j{};
+        j.nj = 4;
+        j.a[0] = z_.get(); j.b[0] = x_.get(); j.len[0] = n; j.op[0] = 0;
+        j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = m; j.op[1] = 0;
+        j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
+        j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = m; j.op[3] = 0;
+        reduce(j, 4);
+        const double mu = (hs_[0] + hs_[1] + phi * psi) / (n + m + 1);
+        const double pobj = hs_[2], dobj = hs_[3];
+        if (mu < 1.0e-12) {                                   // hsdls.c:131-153
+            if (phi > 1.0e-12) status = 0;
+            else if (dobj < 0.0) status = 2;
+            else if (pobj > 0.0) status = 4;
+            else status = 7;
+            break;
+        }
+        hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(NT), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
+                           K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), phi, delta, mu,
+                           E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get());
+        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get());
+        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        const double normr = std::sqrt(hs_[0]) / phi;
+        const double norms = std::sqrt(hs_[1]) / phi;
+        const double gamma = -(1 - delta) * (dobj - pobj + psi) + psi - delta * mu / phi;
+        if (tr) {
+            std::fprintf(tr, "%8d   %14.7e  %8.1e    %14.7e  %8.1e  %8.1e \n", iter, pobj / phi + f_, normr,
+                         dobj / phi + f_, norms, mu);
+            std::fflush(tr);
+        }
+        res->final_mu = mu; res->final_pobj = pobj / phi + f_; res->final_dobj = dobj / phi + f_;
+        res->final_pinf = normr; res->final_dinf = norms;
+
+        K.factor(E_.get(), D_.get());
+        K.solve(E_.get(), D_.get(), fy_.get(), fx_.get());
+        res->refine_passes += K.last_passes();
+        K.solve(E_.get(), D_.get(), gy_.get(), gx_.get());
+        res->refine_passes += K.last_passes();
+
+        RedJobs q{};
+        q.nj = 4;
+        q.a[0] = c_.get(); q.b[0] = fx_.get(); q.len[0] = n; q.op[0] = 0;
+        q.a[1] = b_.get(); q.b[1] = fy_.get(); q.len[1] = m; q.op[1] = 0;
+        q.a[2] = c_.get(); q.b[2] = gx_.get(); q.len[2] = n; q.op[2] = 0;
+        q.a[3] = b_.get(); q.b[3] = gy_.get(); q.len[3] = m; q.op[3] = 0;
+        reduce(q, 4);
+        const double dphi = (hs_[0] - hs_[1] + gamma) / (hs_[2] - hs_[3] - psi / phi);
+        const double dpsi = delta * mu / phi - psi - (psi / phi) * dphi;
+
+        hipLaunchKernelGGL(k_hsdls_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dphi, beta, delta, mu, fx_.get(),
+                           gx_.get(), fy_.get(), gy_.get(), x_.get(), z_.get(), y_.get(), w_.get(), D_.get(), E_.get(),
+                           dx_.get(), dz_.get(), dy_.get(), dw_.get(), part_.get());
+        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 1, 1u, scal_.get());
+        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        double theta = 1.0;
+        const double tv = -hs_[0];                            // min over the vector entries
+        theta = theta < tv ? theta : tv;
+        const double tp = ls_step_host(phi, psi, dphi, dpsi, beta, delta, mu);
+        theta = theta < tp ? theta : tp;
+        if (theta < 1.0) theta *= 0.9999;
 
         hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, theta, x_.get(), dx_.get(), z_.get(), dz_.get(),
                            y_.get(), dy_.get(), w_.get(), dw_.get());

@@ -1,4 +1,4 @@
-// ipo_main.cpp -- `ipo_hip file.mps [hsd|intpt]`: the reference's ipo driver
+// ipo_main.cpp -- `ipo_hip file.mps [hsd|intpt|hsdls]`: the reference's ipo driver
 // (src/common/main.c:16-58) on top of libipo_hip.so; same stdout, no .out file.
 // Extra timing goes to stderr so stdout can be diffed against .sol traces.
 #include <cstdio>
@@ -8,10 +8,12 @@
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s file.mps [hsd|intpt]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s file.mps [hsd|intpt|hsdls]\n", argv[0]);
         return 1;
     }
-    const int method = (argc > 2 && !std::strcmp(argv[2], "intpt")) ? 1 : 0;
+    int method = 0;
+    if (argc > 2 && !std::strcmp(argv[2], "intpt")) method = 1;
+    if (argc > 2 && !std::strcmp(argv[2], "hsdls")) method = 2;
     ipo_hip_stats st;
     const int status = ipo_hip_run_mps(argv[1], method, stdout, 1, &st);
     std::fprintf(stderr,

@@ -29,7 +29,7 @@ STATUS_TEXT = {
     4: "dual infeasible", 5: "iteration limit", 6: "infinite lower bounds - not implemented",
     7: "suboptimal solution",
 }
-METHODS = {"hsd": 0, "intpt": 1}
+METHODS = {"hsd": 0, "intpt": 1, "hsdls": 2}
 
 
 class IpoHipError(RuntimeError):

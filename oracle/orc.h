@@ -124,6 +124,11 @@ int orc_intpt(int m, int n, int nz, const int *iA, const int *kA, const double *
 
 /* Whole ipo pipeline (main.c:16-58 minus writesol): banner, read, normalise,
  * solve, status line.  method: 0 = hsd, 1 = intpt.  Returns status. */
+int orc_hsdls(int m, int n, int nz, const int *iA, const int *kA, const double *A,
+              const double *b, const double *c, double f,
+              double *x, double *y, double *w, double *z, orc_run *run);
+double orc_linesearch(double xj, double zj, double dxj, double dzj, double beta, double delta, double mu);
+/* method: 0 hsd, 1 intpt, 2 hsdls */
 int orc_ipo_run(const char *mps_path, int method, FILE *out, orc_run *run);
 
 /* linalg.c helpers */

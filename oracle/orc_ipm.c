@@ -1,9 +1,10 @@
 /*
  * orc_ipm.c -- ORACLE (test infrastructure only, see orc.h).
  *
- * Restatements of the two solver() methods that ipo links:
+ * Restatements of the three solver() methods that ipo can link:
  *   orc_hsd    homogeneous self-dual predictor-corrector, src/ipo/hsd.c:27-311
  *   orc_intpt  primal-dual path following,               src/ipo/intpt.c:33-261
+ *   orc_hsdls  homogeneous self-dual long step,          src/ipo/hsdls.c:38-336
  * plus the BLAS-1 / SpMV helpers of src/common/linalg.c:17-116 and the
  * driver of src/common/main.c:16-58 (banner, read, solvelp, status text).
  * Every expression is written in the reference's evaluation order.
@@ -270,6 +271,140 @@ int orc_intpt(int m, int n, int nz, const int *iA, const int *kA, const double *
     return status;
 }
 
+/* hsdls.c:298-336 -- largest step keeping x z >= (1-beta) mu along the
+ * centred direction: root of a t^2 + b t + c = 0, HUGE_VAL when unbounded */
+double orc_linesearch(double xj, double zj, double dxj, double dzj, double beta, double delta, double mu)
+{
+    double a = dxj * dzj;
+    double b = zj * dxj + xj * dzj + (1 - beta) * (1 - delta) * mu;
+    double c = xj * zj - (1 - beta) * mu;
+    double d = b * b - 4 * a * c;
+    if (a == 0.0) return -c / b;
+    if (a > 0) {
+        if (b < 0) {
+            if (d >= 0) return 2 * c / (-b + sqrt(d));
+            return HUGE_VAL;
+        }
+        return HUGE_VAL;
+    }
+    if (b < 0) return 2 * c / (-b + sqrt(d));
+    return (-b - sqrt(d)) / (2 * a);
+}
+
+int orc_hsdls(int m, int n, int nz, const int *iA, const int *kA, const double *A,
+              const double *b, const double *c, double f,
+              double *x, double *y, double *w, double *z, orc_run *run)
+{
+    FILE *tr = run ? run->trace : NULL;
+    int maxit = run && run->max_iter > 0 ? run->max_iter : 600;      /* hsdls.c:25 */
+    const double eps = 1.0e-12;
+    double t0 = now_s();
+    double *dx = vec(n), *dw = vec(m), *dy = vec(m), *dz = vec(n);
+    double *rho = vec(m), *sig = vec(n), *D = vec(n), *E = vec(m);
+    double *fx = vec(n), *fy = vec(m), *gx = vec(n), *gy = vec(m);
+    double *At = vec(nz); int *iAt = malloc(sizeof(int) * (size_t)(nz ? nz : 1)), *kAt = malloc(sizeof(int) * (size_t)(m + 1));
+    int status = 5, iter;
+    double phi, psi, dphi, dpsi, normr, norms, gamma, beta, delta, mu, theta, pobj, dobj;
+    orc_kkt *K = NULL;
+
+    for (int j = 0; j < n; j++) { x[j] = 1.0; z[j] = 1.0; }
+    for (int i = 0; i < m; i++) { w[i] = 1.0; y[i] = 1.0; }
+    phi = 1.0; psi = 1.0;
+    orc_transpose(m, n, kA, iA, A, kAt, iAt, At);
+    if (tr) {
+        fprintf(tr, "m = %d,n = %d,nz = %d\n", m, n, nz);
+        fprintf(tr,
+"--------------------------------------------------------------------------\n"
+"         |           Primal          |            Dual           |       |\n"
+"  Iter   |  Obj Value       Infeas   |  Obj Value       Infeas   |  mu   |\n"
+"- - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - \n");
+        fflush(tr);
+    }
+    beta = 0.80;
+    delta = 2 * (1 - beta);
+    for (iter = 0; iter < maxit; iter++) {
+        mu = (orc_dot(z, x, n) + orc_dot(w, y, m) + phi * psi) / (n + m + 1);
+        pobj = orc_dot(c, x, n);
+        dobj = orc_dot(b, y, m);
+        if (mu < eps) {
+            if (phi > eps) status = 0;
+            else if (dobj < 0.0) status = 2;
+            else if (pobj > 0.0) status = 4;
+            else status = 7;
+            break;
+        }
+        orc_spmv(m, n, A, kA, iA, x, rho);
+        for (int i = 0; i < m; i++) rho[i] = rho[i] - b[i] * phi + w[i];
+        normr = sqrt(orc_dot(rho, rho, m)) / phi;
+        for (int i = 0; i < m; i++) rho[i] = -(1 - delta) * rho[i] + w[i] - delta * mu / y[i];
+
+        orc_spmv(n, m, At, kAt, iAt, y, sig);
+        for (int j = 0; j < n; j++) sig[j] = -sig[j] + c[j] * phi + z[j];
+        norms = sqrt(orc_dot(sig, sig, n)) / phi;
+        for (int j = 0; j < n; j++) sig[j] = -(1 - delta) * sig[j] + z[j] - delta * mu / x[j];
+
+        gamma = -(1 - delta) * (dobj - pobj + psi) + psi - delta * mu / phi;
+
+        if (tr) {
+            fprintf(tr, "%8d   %14.7e  %8.1e    %14.7e  %8.1e  %8.1e \n",
+                    iter, pobj / phi + f, normr, dobj / phi + f, norms, mu);
+            fflush(tr);
+        }
+        if (run) { run->final_mu = mu; run->final_pobj = pobj / phi + f; run->final_dobj = dobj / phi + f; run->final_pinf = normr; run->final_dinf = norms; }
+
+        for (int j = 0; j < n; j++) D[j] = z[j] / x[j];
+        for (int i = 0; i < m; i++) E[i] = w[i] / y[i];
+        if (!K) {
+            double ts = now_s();
+            K = orc_kkt_create(m, n, kA, iA, A, kAt, iAt, At);
+            if (run) run->t_setup = now_s() - ts;
+        }
+        orc_kkt_factor(K, E, D);
+        for (int j = 0; j < n; j++) fx[j] = -sig[j];
+        for (int i = 0; i < m; i++) fy[i] = rho[i];
+        orc_kkt_solve(K, E, D, fy, fx);
+        for (int j = 0; j < n; j++) gx[j] = -c[j];
+        for (int i = 0; i < m; i++) gy[i] = -b[i];
+        orc_kkt_solve(K, E, D, gy, gx);
+
+        dphi = (orc_dot(c, fx, n) - orc_dot(b, fy, m) + gamma) /
+               (orc_dot(c, gx, n) - orc_dot(b, gy, m) - psi / phi);
+        for (int j = 0; j < n; j++) dx[j] = fx[j] - gx[j] * dphi;
+        for (int i = 0; i < m; i++) dy[i] = fy[i] - gy[i] * dphi;
+        for (int j = 0; j < n; j++) dz[j] = delta * mu / x[j] - z[j] - D[j] * dx[j];
+        for (int i = 0; i < m; i++) dw[i] = delta * mu / y[i] - w[i] - E[i] * dy[i];
+        dpsi = delta * mu / phi - psi - (psi / phi) * dphi;
+
+        theta = 1.0;
+        for (int j = 0; j < n; j++) {
+            double t = orc_linesearch(x[j], z[j], dx[j], dz[j], beta, delta, mu);
+            theta = theta < t ? theta : t;                         /* MIN(theta, t) */
+        }
+        for (int i = 0; i < m; i++) {
+            double t = orc_linesearch(y[i], w[i], dy[i], dw[i], beta, delta, mu);
+            theta = theta < t ? theta : t;
+        }
+        {
+            double t = orc_linesearch(phi, psi, dphi, dpsi, beta, delta, mu);
+            theta = theta < t ? theta : t;
+        }
+        if (theta < 1.0) theta *= 0.9999;
+
+        for (int j = 0; j < n; j++) { x[j] = x[j] + theta * dx[j]; z[j] = z[j] + theta * dz[j]; }
+        for (int i = 0; i < m; i++) { y[i] = y[i] + theta * dy[i]; w[i] = w[i] + theta * dw[i]; }
+        phi = phi + theta * dphi;
+        psi = psi + theta * dpsi;
+    }
+    for (int j = 0; j < n; j++) { x[j] /= phi; z[j] /= phi; }
+    for (int i = 0; i < m; i++) { y[i] /= phi; w[i] /= phi; }
+
+    if (run) { run->iters = iter; run->t_total = now_s() - t0; }
+    orc_kkt_destroy(K);
+    free(dx); free(dw); free(dy); free(dz); free(rho); free(sig); free(D); free(E);
+    free(fx); free(fy); free(gx); free(gy); free(At); free(iAt); free(kAt);
+    return status;
+}
+
 static const char *status_text[] = {
     "optimal solution", "primal unbounded", "primal infeasible", "dual unbounded",
     "dual infeasible", "iteration limit", "infinite lower bounds - not implemented",
@@ -299,8 +434,9 @@ int orc_ipo_run(const char *path, int method, FILE *out, orc_run *run)
         int m = S.m, n = S.n;
         double *x = calloc((size_t)(n + m), sizeof(double)), *y = calloc((size_t)(n + m), sizeof(double));
         double *w = calloc((size_t)(m ? m : 1), sizeof(double)), *z = calloc((size_t)(n ? n : 1), sizeof(double));
-        if (method == 1) status = orc_intpt(m, n, S.nz, S.rowind, S.colptr, S.val, S.b, S.c, S.f, x, y, w, z, run);
-        else             status = orc_hsd(m, n, S.nz, S.rowind, S.colptr, S.val, S.b, S.c, S.f, x, y, w, z, run);
+        if (method == 1)      status = orc_intpt(m, n, S.nz, S.rowind, S.colptr, S.val, S.b, S.c, S.f, x, y, w, z, run);
+        else if (method == 2) status = orc_hsdls(m, n, S.nz, S.rowind, S.colptr, S.val, S.b, S.c, S.f, x, y, w, z, run);
+        else                  status = orc_hsd(m, n, S.nz, S.rowind, S.colptr, S.val, S.b, S.c, S.f, x, y, w, z, run);
         free(x); free(y); free(w); free(z);
     }
     if (out) { fprintf(out, "%s \n", status_text[status]); fflush(out); }

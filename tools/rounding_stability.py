@@ -43,8 +43,8 @@ def build_fma(out):
     return os.path.join(out, "ipo_oracle")
 
 
-# intpt has no published trace: the oracle (contract-off) run is the
-# reference there, and the FMA build classifies it the same way.
+# intpt and hsdls have no published trace: the oracle (contract-off) run is
+# the reference there, and the FMA build classifies it the same way.
 INTPT_SET = ["afiro", "adlittle", "blend", "sc50a", "sc50b", "kb2", "sc105", "share2b", "stocfor1", "recipe",
              "scagr7", "boeing2", "israel", "bandm", "e226", "ship04s", "25fv47", "capri", "degen2", "agg",
              "scsd1", "fit1d", "brandy", "vtp.base", "lotfi", "beaconfd", "grow7", "sctap1"]
@@ -84,20 +84,24 @@ def main():
     plain = os.path.join(REPO, "oracle", "build", "ipo_oracle")
     subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
 
-    def intpt(name):
-        a = subprocess.run([plain, mps_path(name), "intpt"], capture_output=True, text=True).stdout
-        b = subprocess.run([fma_exe, mps_path(name), "intpt"], capture_output=True, text=True).stdout
+    def other(name, meth):
+        a = subprocess.run([plain, mps_path(name), meth], capture_output=True, text=True).stdout
+        b = subprocess.run([fma_exe, mps_path(name), meth], capture_output=True, text=True).stdout
         return summarise(a), summarise(b)
 
-    with cf.ThreadPoolExecutor(args.j) as ex:
-        ires = dict(zip(INTPT_SET, ex.map(intpt, INTPT_SET)))
-    ip = {k: {"oracle_iters": a[0], "oracle_status": a[1], "fma_iters": b[0], "fma_status": b[1],
-              "stable": a[1] == b[1] and abs(a[0] - b[0]) <= 1} for k, (a, b) in ires.items()}
+    def classify(meth):
+        with cf.ThreadPoolExecutor(args.j) as ex:
+            r = dict(zip(INTPT_SET, ex.map(lambda n: other(n, meth), INTPT_SET)))
+        return {k: {"oracle_iters": a[0], "oracle_status": a[1], "fma_iters": b[0], "fma_status": b[1],
+                    "stable": a[1] == b[1] and abs(a[0] - b[0]) <= 1} for k, (a, b) in r.items()}
+
+    ip = classify("intpt")
+    hl = classify("hsdls")
     dst = os.path.join(REPO, "tests", "golden", "rounding_stability.json")
     with open(dst, "w") as f:
         json.dump({"method": "oracle rebuilt with -ffp-contract=fast -mfma vs golden traces (hsd) / "
-                             "vs the contract-off oracle (intpt)",
-                   "problems": res, "intpt": ip}, f, indent=1, sort_keys=True)
+                             "vs the contract-off oracle (intpt, hsdls)",
+                   "problems": res, "intpt": ip, "hsdls": hl}, f, indent=1, sort_keys=True)
     ns = sum(v["stable"] for v in res.values())
     print(f"{len(res)} problems, {ns} stable -> {dst}")
 
