@@ -374,9 +374,9 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
 
         K.factor(E_.get(), D_.get());
         if (full_trace_) std::fprintf(stderr, "FT   ndep=%d eps=%.1e\n", K.ndep(), K.epsdiag());
-        K.solve(E_.get(), D_.get(), fy_.get(), fx_.get());
-        res->refine_passes += K.last_passes();
-        K.solve(E_.get(), D_.get(), gy_.get(), gx_.get());
+        // the two forwardbackward calls of hsd.c:218-224 / hsdls.c:194-203,
+        // independent systems with one factor: sweeps batched
+        K.solve2(E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get());
         res->refine_passes += K.last_passes();
 
         RedJobs q{};
@@ -469,9 +469,9 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
         res->final_pinf = normr; res->final_dinf = norms;
 
         K.factor(E_.get(), D_.get());
-        K.solve(E_.get(), D_.get(), fy_.get(), fx_.get());
-        res->refine_passes += K.last_passes();
-        K.solve(E_.get(), D_.get(), gy_.get(), gx_.get());
+        // the two forwardbackward calls of hsd.c:218-224 / hsdls.c:194-203,
+        // independent systems with one factor: sweeps batched
+        K.solve2(E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get());
         res->refine_passes += K.last_passes();
 
         RedJobs q{};

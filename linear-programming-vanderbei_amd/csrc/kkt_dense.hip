@@ -43,8 +43,9 @@ struct DiagCtx {
 // On success stores L11' in the block's upper triangle, D in dg, mark = 1.
 __device__ __forceinline__ bool factor_diag_fast(const DiagCtx p, double* panel, int ld, int nc, int c0,
                                                  double (*B)[PC + 1]) {
-    __shared__ double colk[PC];
-    __shared__ double piv[2];
+    __shared__ double colk[2][PC];        // double-buffered: one barrier per column
+    __shared__ double dks[2];
+    __shared__ int tinys[2];
     __shared__ double dv[PC];
     const int tid = threadIdx.x, r = tid & 63, q0 = tid >> 6;
     double a[16];
@@ -56,30 +57,36 @@ __device__ __forceinline__ bool factor_diag_fast(const DiagCtx p, double* panel,
         a[q] = ok ? t : 0.0;
     }
     double dsc = (r < nc && (r & 3) == q0) ? p.dscale[c0 + r] : 0.0;   // kept by the diagonal's owner
-    // k = 4 qk + pk: qk unrolled (static register index), pk a runtime loop
+    // k = 4 qk + pk: qk unrolled (static register index), pk a runtime loop.
+    // Column k (pivot included) lives entirely in wave pk: that wave reads
+    // the pivot by v_readlane, scales the column and publishes it; one
+    // barrier later every wave applies the rank-1 update to its columns.
     bool tiny = false;
 #pragma unroll
     for (int qk = 0; qk < 16; qk++) {
         for (int pk = 0; pk < 4; pk++) {
             const int k = 4 * qk + pk;
             if (k >= nc || tiny) break;
-            if (r == k && q0 == pk) { piv[0] = a[qk]; piv[1] = dsc; }
-            __syncthreads();
-            const double dk = piv[0];
-            if (fabs(dk) <= p.tau * piv[1]) { tiny = true; break; }      // uniform
-            if (tid == 0) dv[k] = dk;
-            if (q0 == pk && r > k && r < nc) {
-                const double l = a[qk] / dk;
-                a[qk] = l;
-                colk[r] = l;
+            const int buf = k & 1;
+            if (q0 == pk) {
+                const double dk = lane_bcast(a[qk], k);
+                const double dsk = lane_bcast(dsc, k);
+                const bool tz = fabs(dk) <= p.tau * dsk;      // uniform in the wave
+                const bool below = !tz && r > k && r < nc;
+                const double l = below ? a[qk] / dk : 0.0;
+                if (below) a[qk] = l;
+                colk[buf][r] = l;
+                if (r == 0) { dks[buf] = dk; tinys[buf] = tz; dv[k] = dk; }
             }
             __syncthreads();
+            if (tinys[buf]) { tiny = true; break; }
+            const double dk = dks[buf];
             if (r > k && r < nc) {
                 // all LDS reads first, then branch-free selects
-                const double lr = colk[r];
+                const double lr = colk[buf][r];
                 double ck[16];
 #pragma unroll
-                for (int q = qk; q < 16; q++) ck[q] = colk[4 * q + q0];
+                for (int q = qk; q < 16; q++) ck[q] = colk[buf][4 * q + q0];
 #pragma unroll
                 for (int q = qk; q < 16; q++) {
                     const int c = 4 * q + q0;
@@ -186,7 +193,7 @@ __device__ void solve_rows(const DiagCtx p, double* panel, int ld, int nc, int c
     __shared__ double Bl[PC][PC + 1];     // Bl[c][k] = L11(c, k) * d_k
     __shared__ double dv[PC];
     __shared__ int lv[PC];
-    __shared__ double lk[64];
+    __shared__ double lk[2][64];          // double-buffered: one barrier per column
     const int tid = threadIdx.x, r = tid & 63, q0 = tid >> 6;
     for (int k = tid; k < nc; k += NT) { dv[k] = p.dg[c0 + k]; lv[k] = p.live[c0 + k]; }
     __syncthreads();
@@ -210,13 +217,14 @@ __device__ void solve_rows(const DiagCtx p, double* panel, int ld, int nc, int c
         for (int pk = 0; pk < 4; pk++) {
             const int k = 4 * qk + pk;
             if (k >= nc) break;
+            const int buf = k & 1;
             if (q0 == pk) {
                 const double l = lv[k] ? a[qk] / dv[k] : 0.0;
                 a[qk] = l;
-                lk[r] = l;
+                lk[buf][r] = l;
             }
             __syncthreads();
-            const double l = lk[r];
+            const double l = lk[buf][r];
             double bk[16];
 #pragma unroll
             for (int q = qk; q < 16; q++) bk[q] = Bl[4 * q + q0][k];
@@ -225,7 +233,6 @@ __device__ void solve_rows(const DiagCtx p, double* panel, int ld, int nc, int c
                 const int c = 4 * q + q0;
                 a[q] = c > k ? a[q] - l * bk[q] : a[q];   // Bl = 0 beyond nc
             }
-            __syncthreads();
         }
     }
     if (okr) {

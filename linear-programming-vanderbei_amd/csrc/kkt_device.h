@@ -69,9 +69,13 @@ class KktDevice {
     // In-place refined solve of  -E dy + A dx = fy,  A' dy + D dx = fx.
     // Returns the rawsolve consistency flag of the last pass (1 = consistent).
     int solve(const double* dE, const double* dD, double* dfy, double* dfx);
+    // Two independent refined solves with the same factor (hsd.c:218-224),
+    // their substitution sweeps batched; each keeps its own refinement loop.
+    int solve2(const double* dE, const double* dD, double* dfy1, double* dfx1, double* dfy2, double* dfx2);
+    void solve_multi(int R, const double* dE, const double* dD, double* const* dfy, double* const* dfx, int* ok);
 
-    // One unrefined sweep L D L' z = rhs on a permuted device vector.
-    void rawsolve(double* dz);
+    // One unrefined sweep L D L' z = rhs on R permuted device vectors at dz + r K.
+    void rawsolve(double* dz, int R = 1);
 
     double epsdiag() const { return epsdiag_; }
     void set_pivot_tolerance(double t) { pivot_tol_ = t; }
@@ -89,6 +93,11 @@ class KktDevice {
 
   private:
     TailView tail_view() const;
+    template <int R>
+    void sweep(double* dz, const double* epsp);
+    void sweep_blocked(double* dz, const double* epsp);
+    size_t ybuf_stride_ = 1, partial_stride_ = 1;
+    DevBuf<int> dIncons_;          // per right-hand side: inconsistent-system flag
     int launch_gather(const struct PlanView& pv, const TailView& tv, int tail, int group, hipStream_t s);
     int fwd_launches_ = 0, bwd_launches_ = 0;   // kernel launches per substitution sweep
     void launch_reduce_maxabs2(const double* a, int na, const double* b, int nb, double* dst);

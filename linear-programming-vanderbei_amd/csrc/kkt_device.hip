@@ -352,13 +352,19 @@ k_tail_syrk(PlanView p, TailView tv, int kb) {
 }
 
 // -------------------------------------------------------------- solves
+// Every sweep kernel handles R right-hand sides at once (R = 1 or 2; hsd and
+// hsdls solve two systems with the same factor per iteration, hsd.c:218-224):
+// vector r of a family lives at base + r * stride.  The dependency chain of a
+// sweep is the same for both, so the second vector rides along almost free.
+//
 // One wave solves a unit-lower nc x nc block in place: lane r holds z_r on
 // entry and on exit; Ls[r][j] = L(r, j) (zero for j >= r).  Lane r keeps its
 // row of L in registers; z_j is broadcast by v_readlane.  A dropped column j
 // (mark false) keeps z_j when |z_j| > eps (and the system is flagged
 // inconsistent), else z_j = 0 -- ldlt.c:446-470.
-__device__ __forceinline__ double tri_lower(double zr, const double (*Ls)[PC + 1], const int* lv, int nc, double eps,
-                                            int& bad) {
+template <int R>
+__device__ __forceinline__ void tri_lower(double (&zr)[R], const double (*Ls)[PC + 1], const int* lv, int nc,
+                                          const double (&eps)[R], int (&bad)[R]) {
     const int lane = threadIdx.x & 63;
     const uint64_t lm = __ballot(lane < nc && lv[lane]);
     double lr[PC];
@@ -368,20 +374,23 @@ __device__ __forceinline__ double tri_lower(double zr, const double (*Ls)[PC + 1
     for (int j = 0; j < PC; j++) {
         if (j < nc) {
             const bool alive = (lm >> j) & 1ull;
-            if (!alive && lane == j) {
-                if (fabs(zr) > eps) bad = 1;
-                else zr = 0.0;
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                if (!alive && lane == j) {
+                    if (fabs(zr[r]) > eps[r]) bad[r] = 1;
+                    else zr[r] = 0.0;
+                }
+                const double zj = lane_bcast(zr[r], j);
+                if (alive && lane > j) zr[r] -= lr[j] * zj;
             }
-            const double zj = lane_bcast(zr, j);
-            if (alive && lane > j) zr -= lr[j] * zj;
         }
     }
-    return zr;
 }
 
 // unit-upper (L11') counterpart; Ls[j][r] = L(j, r) (zero for r >= j)
-__device__ __forceinline__ double tri_upper(double zr, const double (*Ls)[PC + 1], const int* lv, int nc, double eps,
-                                            int& bad) {
+template <int R>
+__device__ __forceinline__ void tri_upper(double (&zr)[R], const double (*Ls)[PC + 1], const int* lv, int nc,
+                                          const double (&eps)[R], int (&bad)[R]) {
     const int lane = threadIdx.x & 63;
     const uint64_t lm = __ballot(lane < nc && lv[lane]);
     double lc[PC];
@@ -391,15 +400,30 @@ __device__ __forceinline__ double tri_upper(double zr, const double (*Ls)[PC + 1
     for (int j = PC - 1; j >= 0; j--) {
         if (j < nc) {
             const bool alive = (lm >> j) & 1ull;
-            if (!alive && lane == j) {
-                if (fabs(zr) > eps) bad = 1;
-                else zr = 0.0;
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                if (!alive && lane == j) {
+                    if (fabs(zr[r]) > eps[r]) bad[r] = 1;
+                    else zr[r] = 0.0;
+                }
+                const double zj = lane_bcast(zr[r], j);
+                if (alive && lane < j) zr[r] -= lc[j] * zj;
             }
-            const double zj = lane_bcast(zr, j);
-            if (alive && lane < j) zr -= lc[j] * zj;
         }
     }
-    return zr;
+}
+
+template <int R>
+__device__ __forceinline__ void flag_bad(const PlanView& p, const int (&bad)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        if (bad[r]) atomicOr(&p.incons[r], 1);
+}
+
+template <int R>
+__device__ __forceinline__ void load_eps(const double* epsp, double (&eps)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; r++) eps[r] = epsp[r];
 }
 
 // D^{-1} with the dropped-column rule (ldlt.c:473-480)
@@ -432,12 +456,21 @@ __device__ __forceinline__ void stage_l11(const double* panel, size_t ld, int nc
     }
 }
 
+// Vector families of a sweep: z (K entries each) and the forward update
+// values ybuf (one per row of every R_s).
+struct SweepVecs {
+    double* z;
+    size_t zs;          // stride between right-hand sides
+    double* y;
+    size_t ys;
+};
+
 // Forward, diagonal part of supernode s: subtract the y values of solved
-// descendants from its rows, solve L11.  Leaves z_s in zl and in z.
+// descendants from its rows, solve L11.  Leaves z_s in zl[r] and in z.
 // 4 threads per row; partial sums combined as (p0 + p1) + (p2 + p3).
+template <int R>
 __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
-                         const double* __restrict__ ybuf, double* __restrict__ z, double eps, double* zl,
-                         double (*Ls)[PC + 1], int* lv) {
+                         const SweepVecs& V, const double (&eps)[R], double (*zl)[PC], double (*Ls)[PC + 1], int* lv) {
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -445,7 +478,9 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
     if (tid < nc) lv[tid] = p.live[c0 + tid];
     for (int base = 0; base < nc; base += blockDim.x >> 2) {
         const int k = base + (tid >> 2), part = tid & 3;
-        double acc = 0.0;
+        double acc[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = 0.0;
         if (k < nc) {
             // four entries in flight per thread: index loads first, then values
             const int v = c0 + k;
@@ -453,26 +488,43 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
             int e = yrow_ptr[v] + part;
             for (; e + 12 < e1; e += 16) {
                 const int i0 = yrow_idx[e], i1 = yrow_idx[e + 4], i2 = yrow_idx[e + 8], i3 = yrow_idx[e + 12];
-                const double y0 = ybuf[i0], y1 = ybuf[i1], y2 = ybuf[i2], y3 = ybuf[i3];
-                acc += y0;
-                acc += y1;
-                acc += y2;
-                acc += y3;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const double* yb = V.y + r * V.ys;
+                    const double y0 = yb[i0], y1 = yb[i1], y2 = yb[i2], y3 = yb[i3];
+                    acc[r] += y0;
+                    acc[r] += y1;
+                    acc[r] += y2;
+                    acc[r] += y3;
+                }
             }
-            for (; e < e1; e += 4) acc += ybuf[yrow_idx[e]];
+            for (; e < e1; e += 4) {
+                const int i0 = yrow_idx[e];
+#pragma unroll
+                for (int r = 0; r < R; r++) acc[r] += V.y[r * V.ys + i0];
+            }
         }
-        const double o1 = __shfl_xor(acc, 1, 64);
-        const double pr = (part & 1) ? o1 + acc : acc + o1;
-        const double o2 = __shfl_xor(pr, 2, 64);
-        const double tot = (part & 2) ? o2 + pr : pr + o2;
-        if (part == 0 && k < nc) zl[k] = z[c0 + k] - tot;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const double o1 = __shfl_xor(acc[r], 1, 64);
+            const double pr = (part & 1) ? o1 + acc[r] : acc[r] + o1;
+            const double o2 = __shfl_xor(pr, 2, 64);
+            const double tot = (part & 2) ? o2 + pr : pr + o2;
+            if (part == 0 && k < nc) zl[r][k] = V.z[r * V.zs + c0 + k] - tot;
+        }
     }
     __syncthreads();
     if (wv == 0) {
-        int bad = 0;
-        const double zr = tri_lower(lane < nc ? zl[lane] : 0.0, Ls, lv, nc, eps, bad);
-        if (lane < nc) { z[c0 + lane] = zr; zl[lane] = zr; }
-        if (bad) atomicOr(&p.flags[1], 1);
+        int bad[R] = {};
+        double zr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) zr[r] = lane < nc ? zl[r][lane] : 0.0;
+        tri_lower<R>(zr, Ls, lv, nc, eps, bad);
+        if (lane < nc) {
+#pragma unroll
+            for (int r = 0; r < R; r++) { V.z[r * V.zs + c0 + lane] = zr[r]; zl[r][lane] = zr[r]; }
+        }
+        flag_bad<R>(p, bad);
     }
     __syncthreads();
 }
@@ -480,55 +532,70 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
 // Forward, one level of small supernodes per launch, one workgroup each:
 // diagonal part, then y_s = L21 z_s for the ancestors (one row per thread).
 // D^{-1} is applied at the start of the backward sweep.
+template <int R>
 __global__ void __launch_bounds__(NT)
 k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ yrow_ptr,
-          const int* __restrict__ yrow_idx, double* __restrict__ ybuf, double* __restrict__ z,
-          const double* __restrict__ epsp) {
-    __shared__ double zl[PC];
+          const int* __restrict__ yrow_idx, SweepVecs V, const double* __restrict__ epsp) {
+    __shared__ double zl[R][PC];
     __shared__ double Ls[PC][PC + 1];
     __shared__ int lv[PC];
+    double eps[R];
+    load_eps<R>(epsp, eps);
     const int s = level_sups[q0 + blockIdx.x];
-    fwd_diag(p, s, yrow_ptr, yrow_idx, ybuf, z, *epsp, zl, Ls, lv);
+    fwd_diag<R>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv);
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
     const double* panel = p.Lx + p.off[s];
-    double* __restrict__ y = ybuf + p.rowptr[s];
     for (int i = threadIdx.x; i < hb; i += NT) {
         const double* __restrict__ row = panel + nc + i;
-        double acc = 0.0;
+        double acc[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = 0.0;
 #pragma unroll 8
-        for (int k = 0; k < nc; k++) acc += row[(size_t)k * h] * zl[k];
-        y[i] = acc;
+        for (int k = 0; k < nc; k++) {
+            const double l = row[(size_t)k * h];
+#pragma unroll
+            for (int r = 0; r < R; r++) acc[r] += l * zl[r][k];
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) V.y[r * V.ys + p.rowptr[s] + i] = acc[r];
     }
 }
 
 // Forward for levels with large panels, part 1: diagonal parts only.
+template <int R>
 __global__ void __launch_bounds__(NT)
 k_fwd_diag(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ yrow_ptr,
-           const int* __restrict__ yrow_idx, const double* __restrict__ ybuf, double* __restrict__ z,
-           const double* __restrict__ epsp) {
-    __shared__ double zl[PC];
+           const int* __restrict__ yrow_idx, SweepVecs V, const double* __restrict__ epsp) {
+    __shared__ double zl[R][PC];
     __shared__ double Ls[PC][PC + 1];
     __shared__ int lv[PC];
-    fwd_diag(p, level_sups[q0 + blockIdx.x], yrow_ptr, yrow_idx, ybuf, z, *epsp, zl, Ls, lv);
+    double eps[R];
+    load_eps<R>(epsp, eps);
+    fwd_diag<R>(p, level_sups[q0 + blockIdx.x], yrow_ptr, yrow_idx, V, eps, zl, Ls, lv);
 }
 
 // part 2: y = L21 z_s over one 64-row chunk of R_s; wave w takes columns
 // 16w..16w+15, the four partial sums are added in wave order.
+template <int R>
 __global__ void __launch_bounds__(NT)
-k_fwd_gemv(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict__ chunk_r0, int cb,
-           double* __restrict__ ybuf, const double* __restrict__ z) {
-    __shared__ double zs[PC];
-    __shared__ double red[4][64];
+k_fwd_gemv(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict__ chunk_r0, int cb, SweepVecs V) {
+    __shared__ double zs[R][PC];
+    __shared__ double red[R][4][64];
     const int c = cb + blockIdx.x;
     const int s = chunk_sup[c], r0 = chunk_r0[c];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid < nc) zs[tid] = z[c0 + tid];
+    if (tid < nc) {
+#pragma unroll
+        for (int r = 0; r < R; r++) zs[r][tid] = V.z[r * V.zs + c0 + tid];
+    }
     __syncthreads();
     const int i = r0 + lane, kq = wv * 16, nq = min(16, nc - kq);
-    double acc = 0.0;
+    double acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = 0.0;
     if (i < hb && nq > 0) {
         const double* __restrict__ row = p.Lx + p.off[s] + nc + i + (size_t)kq * h;
         double t[16];
@@ -536,20 +603,28 @@ k_fwd_gemv(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict_
         for (int q = 0; q < 16; q++) t[q] = row[(size_t)min(q, nq - 1) * h];
 #pragma unroll
         for (int q = 0; q < 16; q++)
-            if (q < nq) acc += t[q] * zs[kq + q];
+            if (q < nq) {
+#pragma unroll
+                for (int r = 0; r < R; r++) acc[r] += t[q] * zs[r][kq + q];
+            }
     }
-    red[wv][lane] = acc;
+#pragma unroll
+    for (int r = 0; r < R; r++) red[r][wv][lane] = acc[r];
     __syncthreads();
-    if (wv == 0 && i < hb) ybuf[p.rowptr[s] + i] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    if (wv == 0 && i < hb) {
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            V.y[r * V.ys + p.rowptr[s] + i] = ((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane];
+    }
 }
 
 // Backward, one level of small supernodes per launch, one workgroup each:
 // z_s = D^{-1} z_s - L21' z_R, then L11'.  Wave w owns columns 16w..16w+15,
 // lanes stride the rows (coalesced column reads).
+template <int R>
 __global__ void __launch_bounds__(NT)
-k_backward(PlanView p, const int* __restrict__ level_sups, int q0, double* __restrict__ z,
-           const double* __restrict__ epsp) {
-    __shared__ double xs[PC];
+k_backward(PlanView p, const int* __restrict__ level_sups, int q0, SweepVecs V, const double* __restrict__ epsp) {
+    __shared__ double xs[R][PC];
     __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L(j, r)
     __shared__ int lv[PC];
     const int s = level_sups[q0 + blockIdx.x];
@@ -563,41 +638,58 @@ k_backward(PlanView p, const int* __restrict__ level_sups, int q0, double* __res
     if (tid < nc) lv[tid] = p.live[c0 + tid];
     const int kq = wv * 16, nq = min(16, nc - kq);
     if (nq > 0) {
-        double acc[16];
+        double acc[R][16];
 #pragma unroll
-        for (int q = 0; q < 16; q++) acc[q] = 0.0;
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) acc[r][q] = 0.0;
         for (int i = lane; i < hb; i += 64) {
-            const double zi = z[rows[i]];
+            const int ri = rows[i];
+            double zi[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) zi[r] = V.z[r * V.zs + ri];
             const double* __restrict__ col = panel + nc + i + (size_t)kq * h;
             double t[16];
 #pragma unroll
             for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, nq - 1) * h];
 #pragma unroll
             for (int q = 0; q < 16; q++)
-                if (q < nq) acc[q] += t[q] * zi;
+                if (q < nq) {
+#pragma unroll
+                    for (int r = 0; r < R; r++) acc[r][q] += t[q] * zi[r];
+                }
         }
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const double t = wave_sum(acc[q]);
-            if (lane == 0 && q < nq) xs[kq + q] = t;
-        }
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const double t = wave_sum(acc[r][q]);
+                if (lane == 0 && q < nq) xs[r][kq + q] = t;
+            }
     }
     __syncthreads();
     if (wv != 0) return;
-    const double eps = *epsp;
-    int bad = 0;
-    double zr = 0.0;
-    if (lane < nc) zr = dscale_rule(p, c0 + lane, z[c0 + lane], eps, bad) - xs[lane];
-    zr = tri_upper(zr, Ls, lv, nc, eps, bad);
-    if (lane < nc) z[c0 + lane] = zr;
-    if (bad) atomicOr(&p.flags[1], 1);
+    double eps[R];
+    load_eps<R>(epsp, eps);
+    int bad[R] = {};
+    double zr[R];
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        zr[r] = lane < nc ? dscale_rule(p, c0 + lane, V.z[r * V.zs + c0 + lane], eps[r], bad[r]) - xs[r][lane] : 0.0;
+    tri_upper<R>(zr, Ls, lv, nc, eps, bad);
+    if (lane < nc) {
+#pragma unroll
+        for (int r = 0; r < R; r++) V.z[r * V.zs + c0 + lane] = zr[r];
+    }
+    flag_bad<R>(p, bad);
 }
 
 // Backward for levels with large panels, part 1: per 64-row chunk of R_s,
 // part[c][k] = sum over the chunk's rows of L(row, k) z_row.
+template <int R>
 __global__ void __launch_bounds__(NT)
-k_bwd_partial(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict__ chunk_r0, int cb,
-              const double* __restrict__ z, double* __restrict__ part) {
+k_bwd_partial(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict__ chunk_r0, int cb, SweepVecs V,
+              double* __restrict__ part, size_t ps) {
     const int c = cb + blockIdx.x;
     const int s = chunk_sup[c], r0 = chunk_r0[c];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
@@ -608,69 +700,98 @@ k_bwd_partial(PlanView p, const int* __restrict__ chunk_sup, const int* __restri
     const int i = r0 + lane;
     const bool okr = i < hb;
     const int ic = okr ? i : 0;
-    const double zi = z[p.rows[p.rowptr[s] + ic]];
+    const int ri = p.rows[p.rowptr[s] + ic];
+    double zi[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) zi[r] = V.z[r * V.zs + ri];
     const double* __restrict__ col = p.Lx + p.off[s] + nc + ic + (size_t)kq * h;
     double t[16];
 #pragma unroll
     for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, nq - 1) * h];
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const double v = wave_sum((okr && q < nq) ? t[q] * zi : 0.0);
-        if (lane == 0 && q < nq) part[(size_t)c * PC + kq + q] = v;
-    }
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const double v = wave_sum((okr && q < nq) ? t[q] * zi[r] : 0.0);
+            if (lane == 0 && q < nq) part[r * ps + (size_t)c * PC + kq + q] = v;
+        }
 }
 
-// part 2: one wave per supernode sums its chunks in order, then D^{-1} and L11'.
+// part 2: sum the chunks of each supernode (wave w: chunks w, w+4, ...; the
+// four partials added in wave order), then D^{-1} and L11'.
+template <int R>
 __global__ void __launch_bounds__(NT)
 k_bwd_finish(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ sup_chunk0,
-             const double* __restrict__ part, double* __restrict__ z, const double* __restrict__ epsp) {
+             const double* __restrict__ part, size_t ps, SweepVecs V, const double* __restrict__ epsp) {
     __shared__ double Ls[PC][PC + 1];
     __shared__ int lv[PC];
-    __shared__ double xs[4][PC];
+    __shared__ double xs[R][4][PC];
     const int s = level_sups[q0 + blockIdx.x];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     stage_l11(p.Lx + p.off[s], h, nc, Ls);
     if (tid < nc) lv[tid] = p.live[c0 + tid];
-    {   // wave w sums chunks w, w+4, ...; the four partials are added in wave order
+    {
         const int cf = sup_chunk0[s], nch = (hb + 63) / 64;
-        double x = 0.0;
+        double x[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) x[r] = 0.0;
         if (lane < nc)
-            for (int c = wv; c < nch; c += 4) x += part[(size_t)(cf + c) * PC + lane];
-        xs[wv][lane] = x;
+            for (int c = wv; c < nch; c += 4) {
+#pragma unroll
+                for (int r = 0; r < R; r++) x[r] += part[r * ps + (size_t)(cf + c) * PC + lane];
+            }
+#pragma unroll
+        for (int r = 0; r < R; r++) xs[r][wv][lane] = x[r];
     }
     __syncthreads();
     if (wv != 0) return;
-    const double eps = *epsp;
-    int bad = 0;
-    double zr = 0.0;
-    if (lane < nc)
-        zr = dscale_rule(p, c0 + lane, z[c0 + lane], eps, bad) - (((xs[0][lane] + xs[1][lane]) + xs[2][lane]) + xs[3][lane]);
-    zr = tri_upper(zr, Ls, lv, nc, eps, bad);
-    if (lane < nc) z[c0 + lane] = zr;
-    if (bad) atomicOr(&p.flags[1], 1);
+    double eps[R];
+    load_eps<R>(epsp, eps);
+    int bad[R] = {};
+    double zr[R];
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        zr[r] = lane < nc ? dscale_rule(p, c0 + lane, V.z[r * V.zs + c0 + lane], eps[r], bad[r]) -
+                                (((xs[r][0][lane] + xs[r][1][lane]) + xs[r][2][lane]) + xs[r][3][lane])
+                          : 0.0;
+    tri_upper<R>(zr, Ls, lv, nc, eps, bad);
+    if (lane < nc) {
+#pragma unroll
+        for (int r = 0; r < R; r++) V.z[r * V.zs + c0 + lane] = zr[r];
+    }
+    flag_bad<R>(p, bad);
 }
 
 // ---------------------------------------------------- dense-tail solves
 // forward, part 1: tail rows subtract the y values the sparse panels left
+template <int R>
 __global__ void __launch_bounds__(NT)
-k_tail_gather(TailView tv, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
-              const double* __restrict__ ybuf, double* __restrict__ z) {
+k_tail_gather(TailView tv, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx, SweepVecs V) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int i = blockIdx.x * 4 + wv;
     if (i >= tv.nt) return;
     const int v = tv.tc + i;
-    double acc = 0.0;
-    for (int e = yrow_ptr[v] + lane; e < yrow_ptr[v + 1]; e += 64) acc += ybuf[yrow_idx[e]];
-    acc = wave_sum(acc);
-    if (lane == 0) z[v] = z[v] - acc;
+    double acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = 0.0;
+    for (int e = yrow_ptr[v] + lane; e < yrow_ptr[v + 1]; e += 64) {
+        const int i0 = yrow_idx[e];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] += V.y[r * V.ys + i0];
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const double a = wave_sum(acc[r]);
+        if (lane == 0) V.z[r * V.zs + v] = V.z[r * V.zs + v] - a;
+    }
 }
 
-// forward, part 2, block kb of the dense tail: every workgroup solves the
-// block's L11 in wave 0 (identical arithmetic, identical results; workgroup
-// 0 stores it), then updates 64 rows below it, z_r -= L(r, block) zb: lane
-// = row, wave w takes columns 16w..16w+15, partials added in wave order.
+// Per-block fallbacks for very large dense tails (ntb > kChainMaxBlocks),
+// one right-hand side.  forward, part 2, block kb: every workgroup solves
+// the block's L11 in wave 0 (identical arithmetic, identical results;
+// workgroup 0 stores it), then updates 64 rows below it.
 __global__ void __launch_bounds__(NT)
 k_tail_fwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double* __restrict__ epsp) {
     __shared__ double Ls[PC][PC + 1];
@@ -679,17 +800,18 @@ k_tail_fwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double
     __shared__ double red[4][64];
     const int nt = tv.nt, tc = tv.tc, k0 = kb * PC, nc = min(PC, nt - k0);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const double* blk = tv.S + k0 + (size_t)k0 * nt;
-    stage_l11(blk, nt, nc, Ls);
+    stage_l11(tv.S + k0 + (size_t)k0 * nt, nt, nc, Ls);
     if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
     __syncthreads();
     if (wv == 0) {
-        int bad = 0;
-        const double zr = tri_lower(lane < nc ? z[tc + k0 + lane] : 0.0, Ls, lv, nc, *epsp, bad);
-        if (lane < nc) zb[lane] = zr;
+        int bad[1] = {0};
+        double eps[1] = {*epsp};
+        double zr[1] = {lane < nc ? z[tc + k0 + lane] : 0.0};
+        tri_lower<1>(zr, Ls, lv, nc, eps, bad);
+        if (lane < nc) zb[lane] = zr[0];
         if (blockIdx.x == 0) {
-            if (lane < nc) z[tc + k0 + lane] = zr;
-            if (bad) atomicOr(&p.flags[1], 1);
+            if (lane < nc) z[tc + k0 + lane] = zr[0];
+            flag_bad<1>(p, bad);
         }
     }
     __syncthreads();
@@ -716,14 +838,13 @@ k_tail_dscale(PlanView p, TailView tv, double* __restrict__ z, const double* __r
     const int i = blockIdx.x * NT + threadIdx.x;
     if (i >= tv.nt) return;
     const int v = tv.tc + i;
-    int bad = 0;
-    z[v] = dscale_rule(p, v, z[v], *epsp, bad);
-    if (bad) atomicOr(&p.flags[1], 1);
+    int bad[1] = {0};
+    z[v] = dscale_rule(p, v, z[v], *epsp, bad[0]);
+    flag_bad<1>(p, bad);
 }
 
 // backward, part 2, block kb: L11' solve (every workgroup, workgroup 0
-// stores), then 64 columns j < k0 left of it: z_j -= sum_k L(k0 + k, j) zb_k;
-// lane = column, wave w takes k = 16w..16w+15, partials added in wave order.
+// stores), then 64 columns j < k0 left of it.
 __global__ void __launch_bounds__(NT)
 k_tail_bwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double* __restrict__ epsp) {
     __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L(j, r)
@@ -736,12 +857,14 @@ k_tail_bwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double
     if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
     __syncthreads();
     if (wv == 0) {
-        int bad = 0;
-        const double zr = tri_upper(lane < nc ? z[tc + k0 + lane] : 0.0, Ls, lv, nc, *epsp, bad);
-        if (lane < nc) zb[lane] = zr;
+        int bad[1] = {0};
+        double eps[1] = {*epsp};
+        double zr[1] = {lane < nc ? z[tc + k0 + lane] : 0.0};
+        tri_upper<1>(zr, Ls, lv, nc, eps, bad);
+        if (lane < nc) zb[lane] = zr[0];
         if (blockIdx.x == 0) {
-            if (lane < nc) z[tc + k0 + lane] = zr;
-            if (bad) atomicOr(&p.flags[1], 1);
+            if (lane < nc) z[tc + k0 + lane] = zr[0];
+            flag_bad<1>(p, bad);
         }
     }
     __syncthreads();
@@ -795,21 +918,24 @@ __device__ __forceinline__ void chain_publish(int* flags, int i, int epoch) {
 }
 
 // forward: z_i -= sum_{j<i} L(i, j) z_j, then the unit-lower L11 solve of block i
+template <int R>
 __global__ void __launch_bounds__(NT)
-k_tail_fwd_chain(PlanView p, TailView tv, double* __restrict__ z, const double* __restrict__ epsp,
-                 int* __restrict__ flags, int epoch) {
+k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, int* __restrict__ flags,
+                 int epoch) {
     extern __shared__ double lds_pad[];
     __shared__ double Ls[PC][PC + 1];
     __shared__ int lv[PC];
-    __shared__ double zb[PC];
-    __shared__ double red[4][64];
+    __shared__ double zb[R][PC];
+    __shared__ double red[R][4][64];
     const int nt = tv.nt, tc = tv.tc, i = blockIdx.x, k0 = i * PC, nc = min(PC, nt - k0);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid == 0) lds_pad[0] = 0.0;
     stage_l11(tv.S + k0 + (size_t)k0 * nt, nt, nc, Ls);
     if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
     const int row = k0 + (lane < nc ? lane : 0);
-    double acc = 0.0;
+    double acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = 0.0;
     for (int j = 0; j < i; j++) {
         // the L(i, j) tile does not depend on z: load it before waiting
         const double* __restrict__ col = tv.S + row + (size_t)(j * PC + wv * 16) * nt;
@@ -817,21 +943,37 @@ k_tail_fwd_chain(PlanView p, TailView tv, double* __restrict__ z, const double* 
 #pragma unroll
         for (int q = 0; q < 16; q++) t[q] = col[(size_t)q * nt];
         chain_wait(flags, j, epoch);
-        if (tid < PC) zb[tid] = sc1_load(z + tc + j * PC + tid);
+        if (tid < PC) {
+#pragma unroll
+            for (int r = 0; r < R; r++) zb[r][tid] = sc1_load(V.z + r * V.zs + tc + j * PC + tid);
+        }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 16; q++) acc += t[q] * zb[wv * 16 + q];
+        for (int q = 0; q < 16; q++) {
+#pragma unroll
+            for (int r = 0; r < R; r++) acc[r] += t[q] * zb[r][wv * 16 + q];
+        }
         __syncthreads();
     }
-    red[wv][lane] = acc;
+#pragma unroll
+    for (int r = 0; r < R; r++) red[r][wv][lane] = acc[r];
     __syncthreads();
     if (wv == 0) {
-        int bad = 0;
-        double zr = 0.0;
-        if (lane < nc) zr = z[tc + k0 + lane] - (((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
-        zr = tri_lower(zr, Ls, lv, nc, *epsp, bad);
-        if (lane < nc) sc1_store(z + tc + k0 + lane, zr);
-        if (bad) atomicOr(&p.flags[1], 1);
+        double eps[R];
+        load_eps<R>(epsp, eps);
+        int bad[R] = {};
+        double zr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            zr[r] = lane < nc ? V.z[r * V.zs + tc + k0 + lane] -
+                                    (((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane])
+                              : 0.0;
+        tri_lower<R>(zr, Ls, lv, nc, eps, bad);
+        if (lane < nc) {
+#pragma unroll
+            for (int r = 0; r < R; r++) sc1_store(V.z + r * V.zs + tc + k0 + lane, zr[r]);
+        }
+        flag_bad<R>(p, bad);
     }
     chain_publish(flags, i, epoch);
 }
@@ -839,14 +981,15 @@ k_tail_fwd_chain(PlanView p, TailView tv, double* __restrict__ z, const double* 
 // backward (launch order = blocks from the last): z_i = D^{-1} z_i
 // - sum_{j>i} L(j, i)' z_j, then the L11' solve.  Wave w owns 16 columns of
 // block i, lanes stride the rows of block j (coalesced column reads).
+template <int R>
 __global__ void __launch_bounds__(NT)
-k_tail_bwd_chain(PlanView p, TailView tv, double* __restrict__ z, const double* __restrict__ epsp,
-                 int* __restrict__ flags, int epoch) {
+k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, int* __restrict__ flags,
+                 int epoch) {
     extern __shared__ double lds_pad[];
     __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L(j, r)
     __shared__ int lv[PC];
-    __shared__ double zb[PC];
-    __shared__ double xs[PC];
+    __shared__ double zb[R][PC];
+    __shared__ double xs[R][PC];
     const int nt = tv.nt, tc = tv.tc, ntb = tv.ntb;
     const int i = ntb - 1 - blockIdx.x, k0 = i * PC, nc = min(PC, nt - k0);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -854,9 +997,11 @@ k_tail_bwd_chain(PlanView p, TailView tv, double* __restrict__ z, const double* 
     stage_l11(tv.S + k0 + (size_t)k0 * nt, nt, nc, Ls);
     if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
     const int kq = wv * 16, nq = min(16, nc - kq);
-    double acc[16];
+    double acc[R][16];
 #pragma unroll
-    for (int q = 0; q < 16; q++) acc[q] = 0.0;
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc[r][q] = 0.0;
     for (int j = ntb - 1; j > i; j--) {
         const int r0 = j * PC, nr = min(PC, nt - r0);
         const int rr = r0 + (lane < nr ? lane : 0);
@@ -865,29 +1010,45 @@ k_tail_bwd_chain(PlanView p, TailView tv, double* __restrict__ z, const double* 
 #pragma unroll
         for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, max(nq, 1) - 1) * nt];
         chain_wait(flags, j, epoch);
-        if (tid < PC) zb[tid] = tid < nr ? sc1_load(z + tc + r0 + tid) : 0.0;
-        __syncthreads();
-        const double zr = lane < nr ? zb[lane] : 0.0;
+        if (tid < PC) {
 #pragma unroll
-        for (int q = 0; q < 16; q++) acc[q] += t[q] * zr;
+            for (int r = 0; r < R; r++) zb[r][tid] = tid < nr ? sc1_load(V.z + r * V.zs + tc + r0 + tid) : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const double zr = lane < nr ? zb[r][lane] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; q++) acc[r][q] += t[q] * zr;
+        }
         __syncthreads();
     }
     if (nq > 0) {
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const double v = wave_sum(acc[q]);
-            if (lane == 0 && q < nq) xs[kq + q] = v;
-        }
+        for (int r = 0; r < R; r++)
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const double v = wave_sum(acc[r][q]);
+                if (lane == 0 && q < nq) xs[r][kq + q] = v;
+            }
     }
     __syncthreads();
     if (wv == 0) {
-        const double eps = *epsp;
-        int bad = 0;
-        double zr = 0.0;
-        if (lane < nc) zr = dscale_rule(p, tc + k0 + lane, z[tc + k0 + lane], eps, bad) - (i < ntb - 1 ? xs[lane] : 0.0);
-        zr = tri_upper(zr, Ls, lv, nc, eps, bad);
-        if (lane < nc) sc1_store(z + tc + k0 + lane, zr);
-        if (bad) atomicOr(&p.flags[1], 1);
+        double eps[R];
+        load_eps<R>(epsp, eps);
+        int bad[R] = {};
+        double zr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            zr[r] = lane < nc ? dscale_rule(p, tc + k0 + lane, V.z[r * V.zs + tc + k0 + lane], eps[r], bad[r]) -
+                                    (i < ntb - 1 ? xs[r][lane] : 0.0)
+                              : 0.0;
+        tri_upper<R>(zr, Ls, lv, nc, eps, bad);
+        if (lane < nc) {
+#pragma unroll
+            for (int r = 0; r < R; r++) sc1_store(V.z + r * V.zs + tc + k0 + lane, zr[r]);
+        }
+        flag_bad<R>(p, bad);
     }
     chain_publish(flags, i, epoch);
 }
@@ -1020,12 +1181,14 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dchunk_sup_.upload(csup, s);
         dchunk_r0_.upload(cr0, s);
         dsup_chunk0_.upload(chunk0, s);
-        dPartial_.alloc(csup.empty() ? 1 : csup.size() * kPanelCols);
+        partial_stride_ = csup.empty() ? 1 : csup.size() * kPanelCols;
+        dPartial_.alloc(2 * partial_stride_);
         IPO_HIP_CHECK(hipStreamSynchronize(s));   // csup / cr0 / chunk0 are stack vectors
     }
     dyrow_ptr_.upload(plan_.yrow_ptr, s);
     dyrow_idx_.upload(plan_.yrow_idx, s);
-    dYbuf_.alloc(plan_.rowptr.back() > 0 ? plan_.rowptr.back() : 1);
+    ybuf_stride_ = plan_.rowptr.back() > 0 ? static_cast<size_t>(plan_.rowptr.back()) : 1;
+    dYbuf_.alloc(2 * ybuf_stride_);
     dkslot_.upload(plan_.kslot, s);
     dkslot_ptr_.upload(plan_.kslot_ptr, s);
     {   // gather chunks (split K): groups = sparse levels, then the dense tail
@@ -1141,10 +1304,11 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dChainFlags_.alloc(plan_.ntb);
         IPO_HIP_CHECK(hipMemsetAsync(dChainFlags_.get(), 0, plan_.ntb * sizeof(int), s));
         if (plan_.ntb <= kChainMaxBlocks) {
-            IPO_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tail_fwd_chain),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
-            IPO_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_tail_bwd_chain),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
+            for (const void* f : {reinterpret_cast<const void*>(&k_tail_fwd_chain<1>),
+                                  reinterpret_cast<const void*>(&k_tail_fwd_chain<2>),
+                                  reinterpret_cast<const void*>(&k_tail_bwd_chain<1>),
+                                  reinterpret_cast<const void*>(&k_tail_bwd_chain<2>)})
+                IPO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
         }
     }
 
@@ -1160,11 +1324,12 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         for (int v = 0; v < T_; v++) fl[2 + v] = plan_.dsign[v];
         dFlags_.upload(fl, s);
     }
-    dZ_.alloc(T_ > 0 ? T_ : 1);
-    dDy_.alloc(m > 0 ? m : 1);
-    dRy_.alloc(m > 0 ? m : 1);
-    dDx_.alloc(n > 0 ? n : 1);
-    dRx_.alloc(n > 0 ? n : 1);
+    dZ_.alloc(2 * (T_ > 0 ? T_ : 1));
+    dDy_.alloc(2 * (m > 0 ? m : 1));
+    dRy_.alloc(2 * (m > 0 ? m : 1));
+    dDx_.alloc(2 * (n > 0 ? n : 1));
+    dRx_.alloc(2 * (n > 0 ? n : 1));
+    dIncons_.alloc(2);
     dPart_.alloc(8 * kRedBlocks);
     dScal_.alloc(16);
     IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hScal_), 16 * sizeof(double), hipHostMallocDefault));
@@ -1204,11 +1369,12 @@ static PlanView make_view(const KktPlan&, const DevBuf<int>& col0, const DevBuf<
 
 #define IPO_VIEW() with_scale(make_view(plan_, dcol0_, drowptr_, drows_, doff_, dunit_sup_, dunit_tile_, dtask_ptr_, \
                              dtask_pair_, dtask_i0_, dtask_i1_, dupd_src_, dupd_r0_, dupd_r1_, drelptr_, drel_, \
-                             dLx_, dDg_, dLive_, dFlags_), dDscale_.get(), pivot_tol_)
+                             dLx_, dDg_, dLive_, dFlags_), dDscale_.get(), pivot_tol_, dIncons_.get())
 
-static PlanView with_scale(PlanView v, double* dscale, double tau) {
+static PlanView with_scale(PlanView v, double* dscale, double tau, int* incons) {
     v.dscale = dscale;
     v.tau = tau;
+    v.incons = incons;
     return v;
 }
 
@@ -1342,77 +1508,52 @@ void KktDevice::ph_collect() {
     kev_used_ = 0;
 }
 
-void KktDevice::rawsolve(double* dz) {
+// Substitution sweeps for R right-hand sides stored at dz + r * K.
+template <int R>
+void KktDevice::sweep(double* dz, const double* epsp) {
     hipStream_t s = stream_;
     const PlanView pv = IPO_VIEW();
-    double* epsp = dScal_.get() + 4;
-    if (ndep_ > 0) {
-        // eps = epssol * max|z[0..n)| (ldlt.c:446: first n entries of the permuted vector)
-        RedJobs j{};
-        j.nj = 1; j.a[0] = dz; j.b[0] = nullptr; j.len[0] = n_; j.op[0] = 1;
-        launch_reduce(j, dPart_.get(), epsp, s);
-        hipLaunchKernelGGL(k_scale_scalar, dim3(1), dim3(1), 0, s, epsp, 1.0e-6);
-    } else {
-        IPO_HIP_CHECK(hipMemsetAsync(epsp, 0, sizeof(double), s));
-    }
+    const SweepVecs V{dz, static_cast<size_t>(T_), dYbuf_.get(), ybuf_stride_};
+    const size_t ps = partial_stride_;
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev2_, s));
     ph_begin(s);
     for (int l = 0; l < plan_.nlevels; l++) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         const int cb = chunk_ptr_[l], ce = chunk_ptr_[l + 1];
         if (ce > cb) {
-            hipLaunchKernelGGL(k_fwd_diag, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dyrow_ptr_.get(),
-                               dyrow_idx_.get(), dYbuf_.get(), dz, epsp);
-            hipLaunchKernelGGL(k_fwd_gemv, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(), cb,
-                               dYbuf_.get(), dz);
+            hipLaunchKernelGGL(k_fwd_diag<R>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
+                               dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+            hipLaunchKernelGGL(k_fwd_gemv<R>, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(), cb,
+                               V);
         } else {
-            hipLaunchKernelGGL(k_forward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dyrow_ptr_.get(),
-                               dyrow_idx_.get(), dYbuf_.get(), dz, epsp);
+            hipLaunchKernelGGL(k_forward<R>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
+                               dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
         }
     }
     if (plan_.nt > 0) {
         const TailView tv = tail_view();
-        const int nt = plan_.nt;
-        hipLaunchKernelGGL(k_tail_gather, dim3(ceil_div(nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(), dyrow_idx_.get(),
-                           dYbuf_.get(), dz);
-        if (plan_.ntb <= kChainMaxBlocks) {
-            hipLaunchKernelGGL(k_tail_fwd_chain, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, dz, epsp,
-                               dChainFlags_.get(), ++chain_epoch_);
-        } else {
-            for (int kb = 0; kb < plan_.ntb; kb++) {
-                const int below = nt - std::min(nt, (kb + 1) * kPanelCols);
-                hipLaunchKernelGGL(k_tail_fwd, dim3(std::max(1, ceil_div(below, 64))), dim3(NT), 0, s, pv, tv, kb, dz,
-                                   epsp);
-            }
-        }
+        hipLaunchKernelGGL(k_tail_gather<R>, dim3(ceil_div(plan_.nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(),
+                           dyrow_idx_.get(), V);
+        hipLaunchKernelGGL(k_tail_fwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
+                           dChainFlags_.get(), ++chain_epoch_);
     }
     ph_end(kPhForward, fwd_launches_, s);
     ph_begin(s);
     if (plan_.nt > 0) {
         const TailView tv = tail_view();
-        const int nt = plan_.nt;
-        if (plan_.ntb <= kChainMaxBlocks) {
-            hipLaunchKernelGGL(k_tail_bwd_chain, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, dz, epsp,
-                               dChainFlags_.get(), ++chain_epoch_);
-        } else {
-            hipLaunchKernelGGL(k_tail_dscale, dim3(ceil_div(nt, NT)), dim3(NT), 0, s, pv, tv, dz, epsp);
-            for (int kb = plan_.ntb - 1; kb >= 0; kb--) {
-                const int left = kb * kPanelCols;
-                hipLaunchKernelGGL(k_tail_bwd, dim3(std::max(1, ceil_div(left, 64))), dim3(NT), 0, s, pv, tv, kb, dz,
-                                   epsp);
-            }
-        }
+        hipLaunchKernelGGL(k_tail_bwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
+                           dChainFlags_.get(), ++chain_epoch_);
     }
     for (int l = plan_.nlevels - 1; l >= 0; l--) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         const int cb = chunk_ptr_[l], ce = chunk_ptr_[l + 1];
         if (ce > cb) {
-            hipLaunchKernelGGL(k_bwd_partial, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(), cb,
-                               dz, dPartial_.get());
-            hipLaunchKernelGGL(k_bwd_finish, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
-                               dsup_chunk0_.get(), dPartial_.get(), dz, epsp);
+            hipLaunchKernelGGL(k_bwd_partial<R>, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(),
+                               cb, V, dPartial_.get(), ps);
+            hipLaunchKernelGGL(k_bwd_finish<R>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
+                               dsup_chunk0_.get(), dPartial_.get(), ps, V, epsp);
         } else {
-            hipLaunchKernelGGL(k_backward, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, dz, epsp);
+            hipLaunchKernelGGL(k_backward<R>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, V, epsp);
         }
     }
     ph_end(kPhBackward, bwd_launches_, s);
@@ -1427,59 +1568,171 @@ void KktDevice::rawsolve(double* dz) {
         tm_.phase_count[kPhForward]++;
         tm_.phase_count[kPhBackward]++;
     }
-    tm_.rawsolves++;
 }
 
-int KktDevice::solve(const double* dE, const double* dD, double* dfy, double* dfx) {
+// Very large dense tails (more blocks than the chain kernels keep resident):
+// one right-hand side, per-block launches.
+void KktDevice::sweep_blocked(double* dz, const double* epsp) {
+    hipStream_t s = stream_;
+    const PlanView pv = IPO_VIEW();
+    const SweepVecs V{dz, static_cast<size_t>(T_), dYbuf_.get(), ybuf_stride_};
+    const size_t ps = partial_stride_;
+    for (int l = 0; l < plan_.nlevels; l++) {
+        const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
+        const int cb = chunk_ptr_[l], ce = chunk_ptr_[l + 1];
+        if (ce > cb) {
+            hipLaunchKernelGGL(k_fwd_diag<1>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
+                               dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+            hipLaunchKernelGGL(k_fwd_gemv<1>, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(), cb,
+                               V);
+        } else {
+            hipLaunchKernelGGL(k_forward<1>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
+                               dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+        }
+    }
+    const TailView tv = tail_view();
+    const int nt = plan_.nt;
+    hipLaunchKernelGGL(k_tail_gather<1>, dim3(ceil_div(nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(), dyrow_idx_.get(),
+                       V);
+    for (int kb = 0; kb < plan_.ntb; kb++) {
+        const int below = nt - std::min(nt, (kb + 1) * kPanelCols);
+        hipLaunchKernelGGL(k_tail_fwd, dim3(std::max(1, ceil_div(below, 64))), dim3(NT), 0, s, pv, tv, kb, dz, epsp);
+    }
+    hipLaunchKernelGGL(k_tail_dscale, dim3(ceil_div(nt, NT)), dim3(NT), 0, s, pv, tv, dz, epsp);
+    for (int kb = plan_.ntb - 1; kb >= 0; kb--) {
+        const int left = kb * kPanelCols;
+        hipLaunchKernelGGL(k_tail_bwd, dim3(std::max(1, ceil_div(left, 64))), dim3(NT), 0, s, pv, tv, kb, dz, epsp);
+    }
+    for (int l = plan_.nlevels - 1; l >= 0; l--) {
+        const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
+        const int cb = chunk_ptr_[l], ce = chunk_ptr_[l + 1];
+        if (ce > cb) {
+            hipLaunchKernelGGL(k_bwd_partial<1>, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(),
+                               cb, V, dPartial_.get(), ps);
+            hipLaunchKernelGGL(k_bwd_finish<1>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
+                               dsup_chunk0_.get(), dPartial_.get(), ps, V, epsp);
+        } else {
+            hipLaunchKernelGGL(k_backward<1>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, V, epsp);
+        }
+    }
+    IPO_HIP_CHECK(hipGetLastError());
+}
+
+// rawsolve (ldlt.c:433-505) of R right-hand sides at dz + r * K, in place.
+void KktDevice::rawsolve(double* dz, int R) {
+    hipStream_t s = stream_;
+    double* epsp = dScal_.get() + 4;        // eps of right-hand side r at epsp[r]
+    if (ndep_ > 0) {
+        // eps = epssol * max|z[0..n)| (ldlt.c:446: first n entries of the permuted vector)
+        RedJobs j{};
+        j.nj = R;
+        for (int r = 0; r < R; r++) { j.a[r] = dz + (size_t)r * T_; j.b[r] = nullptr; j.len[r] = n_; j.op[r] = 1; }
+        launch_reduce(j, dPart_.get(), epsp, s);
+        for (int r = 0; r < R; r++) hipLaunchKernelGGL(k_scale_scalar, dim3(1), dim3(1), 0, s, epsp + r, 1.0e-6);
+    } else {
+        IPO_HIP_CHECK(hipMemsetAsync(epsp, 0, R * sizeof(double), s));
+    }
+    if (plan_.nt > 0 && plan_.ntb > kChainMaxBlocks) {
+        for (int r = 0; r < R; r++) sweep_blocked(dz + (size_t)r * T_, epsp + r);
+    } else if (R == 2) {
+        sweep<2>(dz, epsp);
+    } else {
+        sweep<1>(dz, epsp);
+    }
+    tm_.rawsolves += R;
+}
+
+// Refined solves of R systems K [dy; dx] = [fy_r; fx_r] with the current
+// factor, in place (ldlt.c:327-425).  Each right-hand side runs the
+// reference's own refinement loop (first pass from the right-hand side,
+// further passes on the KKT residual while it exceeds 1e-10 (max|b| + 1)
+// and halves, the last correction undone if the residual grew); passes of
+// both systems share one sweep.  Returns the reference's consistency flag
+// of each system in ok[r].
+void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* const* dfy, double* const* dfx,
+                            int* ok) {
     hipStream_t s = stream_;
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev0_, s));
     const int m = m_, n = n_, T = T_;
-    IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get() + 1, 0, sizeof(int), s));
-    // maxbc = MAX(maxv(fx), maxv(fy)) + 1   (ldlt.c:367)
-    {
+    IPO_HIP_CHECK(hipMemsetAsync(dIncons_.get(), 0, 2 * sizeof(int), s));
+    {   // maxbc_r = MAX(maxv(fx_r), maxv(fy_r)) + 1   (ldlt.c:367)
         RedJobs j{};
-        j.nj = 2;
-        j.a[0] = dfx; j.b[0] = nullptr; j.len[0] = n; j.op[0] = 1;
-        j.a[1] = dfy; j.b[1] = nullptr; j.len[1] = m; j.op[1] = 1;
+        j.nj = 2 * R;
+        for (int r = 0; r < R; r++) {
+            j.a[2 * r] = dfx[r]; j.b[2 * r] = nullptr; j.len[2 * r] = n; j.op[2 * r] = 1;
+            j.a[2 * r + 1] = dfy[r]; j.b[2 * r + 1] = nullptr; j.len[2 * r + 1] = m; j.op[2 * r + 1] = 1;
+        }
         launch_reduce(j, dPart_.get(), dScal_.get(), s);
-        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 2 * R * sizeof(double), hipMemcpyDeviceToHost, s));
     }
     IPO_HIP_CHECK(hipStreamSynchronize(s));
-    const double maxbc = (hScal_[0] > hScal_[1] ? hScal_[0] : hScal_[1]) + 1;
-
-    double* z = dZ_.get();
-    double* dy = dDy_.get();
-    double* dx = dDx_.get();
-    double* ry = dRy_.get();
-    double* rx = dRx_.get();
-    int pass = 0;
-    double rs = HUGE_VAL, rs_old;
-    do {
-        hipLaunchKernelGGL(k_perm_in, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, dperm_.get(),
-                           pass == 0 ? dfy : ry, pass == 0 ? dfx : rx, z);
-        rawsolve(z);
-        hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), z, dy, dx,
-                           pass == 0 ? 0 : 1);
-        hipLaunchKernelGGL(k_kkt_residual, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dkAt_.get(), diAt_.get(), dAt_.get(),
-                           dkA_.get(), diA_.get(), dA_.get(), dE, dD, dfy, dfx, dy, dx, ry, rx, dPart_.get());
-        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), 1, 1u, dScal_.get());
-        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+    double maxbc[2], rs[2] = {HUGE_VAL, HUGE_VAL}, rs_old[2] = {HUGE_VAL, HUGE_VAL};
+    int pass[2] = {0, 0};
+    bool active[2] = {R > 0, R > 1};
+    for (int r = 0; r < R; r++) maxbc[r] = (hScal_[2 * r] > hScal_[2 * r + 1] ? hScal_[2 * r] : hScal_[2 * r + 1]) + 1;
+    auto zv = [&](int r) { return dZ_.get() + (size_t)r * T; };
+    auto dyv = [&](int r) { return dDy_.get() + (size_t)r * m; };
+    auto dxv = [&](int r) { return dDx_.get() + (size_t)r * n; };
+    auto ryv = [&](int r) { return dRy_.get() + (size_t)r * m; };
+    auto rxv = [&](int r) { return dRx_.get() + (size_t)r * n; };
+    while (active[0] || active[1]) {
+        for (int r = 0; r < R; r++)
+            if (active[r])
+                hipLaunchKernelGGL(k_perm_in, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, dperm_.get(),
+                                   pass[r] == 0 ? dfy[r] : ryv(r), pass[r] == 0 ? dfx[r] : rxv(r), zv(r));
+        if (active[0] && active[1]) rawsolve(zv(0), 2);
+        else rawsolve(zv(active[0] ? 0 : 1), 1);
+        int nq = 0;
+        for (int r = 0; r < R; r++) {
+            if (!active[r]) continue;
+            hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), zv(r), dyv(r),
+                               dxv(r), pass[r] == 0 ? 0 : 1);
+            hipLaunchKernelGGL(k_kkt_residual, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dkAt_.get(), diAt_.get(),
+                               dAt_.get(), dkA_.get(), diA_.get(), dA_.get(), dE, dD, dfy[r], dfx[r], dyv(r), dxv(r),
+                               ryv(r), rxv(r), dPart_.get() + (size_t)nq * kRedBlocks);
+            nq++;
+        }
+        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), nq, (1u << nq) - 1u,
+                           dScal_.get());
+        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), nq * sizeof(double), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
-        rs_old = rs;
-        rs = hScal_[0];
-        pass++;
-    } while (rs > 1.0e-10 * maxbc && rs < rs_old / 2);
-    if (rs > rs_old && pass > 1)
-        hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), z, dy, dx, 2);
-    IPO_HIP_CHECK(hipMemcpyAsync(dfy, dy, sizeof(double) * m, hipMemcpyDeviceToDevice, s));
-    IPO_HIP_CHECK(hipMemcpyAsync(dfx, dx, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-    IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 1, dFlags_.get() + 1, sizeof(int), hipMemcpyDeviceToHost, s));
+        int q = 0;
+        for (int r = 0; r < R; r++) {
+            if (!active[r]) continue;
+            rs_old[r] = rs[r];
+            rs[r] = hScal_[q++];
+            pass[r]++;
+            active[r] = rs[r] > 1.0e-10 * maxbc[r] && rs[r] < rs_old[r] / 2;
+        }
+    }
+    for (int r = 0; r < R; r++) {
+        if (rs[r] > rs_old[r] && pass[r] > 1)
+            hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), zv(r), dyv(r),
+                               dxv(r), 2);
+        IPO_HIP_CHECK(hipMemcpyAsync(dfy[r], dyv(r), sizeof(double) * m, hipMemcpyDeviceToDevice, s));
+        IPO_HIP_CHECK(hipMemcpyAsync(dfx[r], dxv(r), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    }
+    IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 2, dIncons_.get(), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
     IPO_HIP_CHECK(hipStreamSynchronize(s));
     if (timing_) { float ms = 0; IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_)); tm_.solve_ms += ms; }
-    tm_.solves++;
-    last_passes_ = pass;
-    return hFlags_[1] ? 0 : 1;
+    tm_.solves += R;
+    last_passes_ = pass[0] + pass[1];
+    for (int r = 0; r < R; r++) ok[r] = hFlags_[2 + r] ? 0 : 1;
+}
+
+int KktDevice::solve(const double* dE, const double* dD, double* dfy, double* dfx) {
+    int ok[1];
+    solve_multi(1, dE, dD, &dfy, &dfx, ok);
+    return ok[0];
+}
+
+int KktDevice::solve2(const double* dE, const double* dD, double* dfy1, double* dfx1, double* dfy2, double* dfx2) {
+    double* fy[2] = {dfy1, dfy2};
+    double* fx[2] = {dfx1, dfx2};
+    int ok[2];
+    solve_multi(2, dE, dD, fy, fx, ok);
+    return ok[0] && ok[1];
 }
 
 void KktDevice::download_factor(double* lx, double* d) const {

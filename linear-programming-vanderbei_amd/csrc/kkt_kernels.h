@@ -35,6 +35,7 @@ struct PlanView {
     const int* sign; // node class per new index: -1 y-node, +1 x-node
     double* dscale;  // sum of |terms| that formed each pivot (zero-pivot test)
     double tau;      // pivot d is "zero" when |d| <= tau * dscale
+    int* incons;     // [r]: right-hand side r met a dropped column with |z| > eps (ldlt.c:462)
 };
 
 // value of v in lane j (j wave-uniform), via two v_readlane_b32
