@@ -150,6 +150,7 @@ class KktDevice {
     std::vector<int> ck_ptr_, sp_ptr_;
     DevBuf<int> dck_u_, dck_b_, dck_e_, dck_part_, dsp_u_, dsp_p0_, dsp_n_;
     DevBuf<double> dPartialTile_;
+    DevBuf<TaskSrc> dusrc_, dtsrc_;   // per gather task: source panel descriptor
     DevBuf<int> dChainFlags_;    // dense-tail sweep chains: per block, epoch of the last completed sweep
     int chain_epoch_ = 0;      // forward-sweep update values, one per row of every R_s
     DevBuf<int> dtail_task_ptr_, dkslot_, dkslot_ptr_, dtail_kslot_, dtail_kslot_ptr_;

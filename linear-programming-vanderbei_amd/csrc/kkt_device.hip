@@ -77,25 +77,35 @@ k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __rest
 typedef double double4_t __attribute__((ext_vector_type(4)));
 constexpr int KS = kSlab;
 
-__device__ __forceinline__ void stage_slab(const PlanView& p, const TailTask* __restrict__ tasks,
-                                           const int* __restrict__ kslot, int base, int wv, int lane,
-                                           double (&ra)[KS / 4], double (&rb)[KS / 4]) {
+// What a k-slot needs, resolved once per slot (wave-uniform): the source
+// column (rows of R_d), its d_k, and the task's row / column masks.
+struct SlotMeta {
+    uint64_t rmask, cmask;
+    const double* col;
+    const double* dk;
+    int rbase, cbase;
+};
+
+__device__ __forceinline__ void slot_meta(const PlanView& p, const TailTask* __restrict__ tasks,
+                                          const TaskSrc* __restrict__ srcs, int sl, SlotMeta& m) {
+    if (sl < 0) { m.rmask = m.cmask = 0; m.col = p.Lx; m.dk = p.dg; m.rbase = m.cbase = 0; return; }
+    const int t = sl >> 6, kl = sl & 63;
+    const TailTask tk = tasks[t];
+    const TaskSrc sd = srcs[t];
+    m.rmask = tk.rmask;
+    m.cmask = tk.cmask;
+    m.rbase = tk.rbase;
+    m.cbase = tk.cbase;
+    m.col = p.Lx + sd.colbase + (size_t)kl * sd.hd;
+    m.dk = p.dg + sd.cd0 + kl;
+}
+
+__device__ __forceinline__ void slot_vals(const SlotMeta& m, int lane, double& ra, double& rb) {
     const uint64_t below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int j = 0; j < KS / 4; j++) {
-        const int sl = __builtin_amdgcn_readfirstlane(kslot[base + wv * (KS / 4) + j]);
-        ra[j] = 0.0;
-        rb[j] = 0.0;
-        if (sl < 0) continue;
-        const TailTask tk = tasks[sl >> 6];
-        const int kl = sl & 63;
-        const int d = tk.src;
-        const int cd0 = p.col0[d], ncd = p.col0[d + 1] - cd0;
-        const int hd = ncd + (p.rowptr[d + 1] - p.rowptr[d]);
-        const double* __restrict__ col = p.Lx + p.off[d] + ncd + (size_t)kl * hd;
-        if ((tk.rmask >> lane) & 1ull) ra[j] = col[tk.rbase + __popcll(tk.rmask & below)];
-        if ((tk.cmask >> lane) & 1ull) rb[j] = p.dg[cd0 + kl] * col[tk.cbase + __popcll(tk.cmask & below)];
-    }
+    ra = 0.0;
+    rb = 0.0;
+    if ((m.rmask >> lane) & 1ull) ra = m.col[m.rbase + __popcll(m.rmask & below)];
+    if ((m.cmask >> lane) & 1ull) rb = *m.dk * m.col[m.cbase + __popcll(m.cmask & below)];
 }
 
 // Output tile of one gather unit: a 64-row tile of a sparse panel
@@ -139,10 +149,12 @@ __device__ __forceinline__ GatherTile unit_tile(const PlanView& p, const TailVie
 // MFMA accumulation of slots [kb, ke) into this thread's 16 tile entries
 // (acc[a][b][i] = entry (wr + 16a + (lane>>4) + 4i, wc + 16b + (lane&15)))
 // and, for lanes on a diagonal entry, the |terms| of that entry (dabs).
-__device__ void gather_acc(const PlanView& p, const TailTask* __restrict__ tasks, const int* __restrict__ kslot,
-                           int kb, int ke, int dcol, bool has_diag, double4_t (&acc)[2][2], double& dabs) {
+__device__ void gather_acc(const PlanView& p, const TailTask* __restrict__ tasks, const TaskSrc* __restrict__ srcs,
+                           const int* __restrict__ kslot, int kb, int ke, int dcol, bool has_diag,
+                           double4_t (&acc)[2][2], double& dabs) {
     __shared__ double As[2][TR][KS + 1];
     __shared__ double Bs[2][TR][KS + 1];
+    __shared__ int ks[kMaxChunkSlots];
     const int tid = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
@@ -152,15 +164,36 @@ __device__ void gather_acc(const PlanView& p, const TailTask* __restrict__ tasks
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     dabs = 0.0;
+    const int nk = ke - kb, nslab = nk / KS;
+    for (int i = tid; i < nk; i += NT) ks[i] = kslot[kb + i];
+    __syncthreads();
+    // three-stage pipeline: slot metadata two slabs ahead, values one ahead
     double ra[KS / 4], rb[KS / 4];
-    const int nslab = (ke - kb) / KS;
-    stage_slab(p, tasks, kslot, kb, wv, lane, ra, rb);
+    SlotMeta mn[KS / 4];
+#pragma unroll
+    for (int j = 0; j < KS / 4; j++) slot_meta(p, tasks, srcs, __builtin_amdgcn_readfirstlane(ks[wv * (KS / 4) + j]), mn[j]);
+#pragma unroll
+    for (int j = 0; j < KS / 4; j++) slot_vals(mn[j], lane, ra[j], rb[j]);
+    if (nslab > 1) {
+#pragma unroll
+        for (int j = 0; j < KS / 4; j++)
+            slot_meta(p, tasks, srcs, __builtin_amdgcn_readfirstlane(ks[KS + wv * (KS / 4) + j]), mn[j]);
+    }
 #pragma unroll
     for (int j = 0; j < KS / 4; j++) { As[0][lane][wv * (KS / 4) + j] = ra[j]; Bs[0][lane][wv * (KS / 4) + j] = rb[j]; }
     __syncthreads();
     for (int sb = 0; sb < nslab; sb++) {
         const int cur = sb & 1;
-        if (sb + 1 < nslab) stage_slab(p, tasks, kslot, kb + (sb + 1) * KS, wv, lane, ra, rb);
+        if (sb + 1 < nslab) {
+#pragma unroll
+            for (int j = 0; j < KS / 4; j++) slot_vals(mn[j], lane, ra[j], rb[j]);
+            if (sb + 2 < nslab) {
+#pragma unroll
+                for (int j = 0; j < KS / 4; j++)
+                    slot_meta(p, tasks, srcs, __builtin_amdgcn_readfirstlane(ks[(sb + 2) * KS + wv * (KS / 4) + j]),
+                              mn[j]);
+            }
+        }
 #pragma unroll
         for (int kk = 0; kk < KS; kk += 4) {
             double av[2], bv[2];
@@ -221,7 +254,8 @@ __device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], 
 // partial tile (thread-fragment order) and dabs at partial slot ck_part[c].
 // tail >= 0: units are dense-tail tiles.
 __global__ void __launch_bounds__(NT)
-k_update(PlanView p, TailView tv, int tail, const TailTask* __restrict__ tasks, const int* __restrict__ kslot,
+k_update(PlanView p, TailView tv, int tail, const TailTask* __restrict__ tasks, const TaskSrc* __restrict__ srcs,
+         const int* __restrict__ kslot,
          const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
          const int* __restrict__ ck_part, int c0, double* __restrict__ partial) {
     const int c = c0 + blockIdx.x;
@@ -232,7 +266,7 @@ k_update(PlanView p, TailView tv, int tail, const TailTask* __restrict__ tasks, 
     const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
     double4_t acc[2][2];
     double dabs;
-    gather_acc(p, tasks, kslot, kb, ke, dcol, has_diag, acc, dabs);
+    gather_acc(p, tasks, srcs, kslot, kb, ke, dcol, has_diag, acc, dabs);
     if (pi < 0) {
         gather_store(g, acc, dabs, has_diag, dcol);
         return;
@@ -1201,7 +1235,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             for (int u = u0; u < u1; u++) sumk += kptr[u + 1] - kptr[u];
             // aim at >= 512 workgroups per launch, chunks of 64..512 slots
             long kmax = (sumk / 512 + kSlab - 1) / kSlab * kSlab;
-            kmax = std::max<long>(64, std::min<long>(512, kmax));
+            kmax = std::max<long>(64, std::min<long>(kMaxChunkSlots, kmax));
             int np = 0;
             for (int u = u0; u < u1; u++) {
                 const int kb = kptr[u], ke = kptr[u + 1];
@@ -1292,6 +1326,21 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             work_flops[ph] = 2.0 * (lxs + tail_tri);
             work_bytes[ph] = 8.0 * (lxs + tail_tri) + 8.0 * 2 * T_ + (ph == kPhForward ? 12.0 : 12.0) * nrowsR;
         }
+    }
+    {   // per-task source descriptors for the gather
+        auto build = [&](const std::vector<TailTask>& ts, DevBuf<TaskSrc>& dst) {
+            std::vector<TaskSrc> v(ts.size());
+            for (size_t t = 0; t < ts.size(); t++) {
+                const int d = ts[t].src, ncd = plan_.col0[d + 1] - plan_.col0[d];
+                v[t].colbase = plan_.off[d] + ncd;
+                v[t].hd = ncd + (plan_.rowptr[d + 1] - plan_.rowptr[d]);
+                v[t].cd0 = plan_.col0[d];
+            }
+            dst.upload(v, s);
+            IPO_HIP_CHECK(hipStreamSynchronize(s));
+        };
+        build(plan_.utasks, dusrc_);
+        if (plan_.nt > 0) build(plan_.tail_tasks, dtsrc_);
     }
     dutasks_.upload(reinterpret_cast<const uint64_t*>(plan_.utasks.data()), plan_.utasks.size() * 4, s);
     if (plan_.nt > 0) {
@@ -1466,7 +1515,8 @@ int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, i
     const TailTask* tasks = tail < 0 ? reinterpret_cast<const TailTask*>(dutasks_.get())
                                      : reinterpret_cast<const TailTask*>(dtail_tasks_.get());
     const int* kslot = tail < 0 ? dkslot_.get() : dtail_kslot_.get();
-    hipLaunchKernelGGL(k_update, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, tasks, kslot, dck_u_.get(), dck_b_.get(),
+    const TaskSrc* srcs = tail < 0 ? dusrc_.get() : dtsrc_.get();
+    hipLaunchKernelGGL(k_update, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, tasks, srcs, kslot, dck_u_.get(), dck_b_.get(),
                        dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get());
     const int s0 = sp_ptr_[group], s1 = sp_ptr_[group + 1];
     if (s1 > s0)

@@ -50,6 +50,15 @@ struct TailTask {
     int src, rbase, cbase, pad;
 };
 
+// Where a gather task's source panel lives: Lx + colbase + k * hd is column
+// k of its row set R_d; d_k = dg[cd0 + k].
+struct TaskSrc {
+    int64_t colbase;
+    int hd, cd0;
+};
+
+constexpr int kMaxChunkSlots = 512;   // largest split-K chunk of the gather
+
 struct KktPlan {
     int m = 0, n = 0, T = 0;
     std::vector<int> perm, iperm;
