@@ -298,7 +298,29 @@ k_update_reduce(PlanView p, TailView tv, int tail, const int* __restrict__ sp_u,
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     double dabs = 0.0;
-    for (int j = 0; j < np; j++) {
+    // loads of four chunks in flight, sums still in chunk order
+    int j = 0;
+    for (; j + 4 <= np; j += 4) {
+        double v[4][17];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const double* src = partial + (size_t)(p0 + j + u) * (TR * TR + 4 * TR);
+#pragma unroll
+            for (int e = 0; e < 16; e++) v[u][e] = src[e * NT + tid];
+            v[u][16] = src[TR * TR + tid];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) acc[a][b][i] += v[u][(a * 2 + b) * 4 + i];
+            dabs += v[u][16];
+        }
+    }
+    for (; j < np; j++) {
         const double* src = partial + (size_t)(p0 + j) * (TR * TR + 4 * TR);
 #pragma unroll
         for (int a = 0; a < 2; a++)
