@@ -123,6 +123,23 @@ void   ipo_hip_kkt_set_epsdiag(ipo_hip_kkt *k, double epsdiag);
 int ipo_hip_symbolic(int m, int n, const int *kA, const int *iA, int *perm, long *lnz, double *narth,
                      int *denwin, int *pdf, int *nsup, int *nlevels);
 
+/* Synthetic LPs in solver() form (BASELINE configs[3] and configs[4],
+ * SURVEY.md §8(d); not part of the reference): feasible and bounded by
+ * construction from an interior point x*, y*, w*, z* in U[0.5,1.5]
+ * (b = A x* + w*, c = A' y* - z*).  Pass kA = NULL to query sizes only;
+ * otherwise kA[n+1], iA[nz], A[nz], b[m], c[n] are filled, and xs/zs (n),
+ * ys/ws (m) when non-NULL.  band = 0: uniform rows; band > 0: rows from a
+ * window of that width around floor(j m / n).  Returns 0, or -1 on bad
+ * sizes (ipo_hip_last_error). */
+int ipo_hip_synth_random(int m, int n, int per_col, int band, unsigned long long seed, int *nz, int *kA, int *iA,
+                         double *A, double *b, double *c, double *xs, double *ys, double *ws, double *zs);
+/* nblocks diagonal blocks (mb x nb, banded random per block) + nlink linking
+ * rows with link_nz nonzeros each; block k owns rows [k mb, (k+1) mb) and
+ * columns [k nb, (k+1) nb), linking rows come last. */
+int ipo_hip_synth_block_angular(int nblocks, int mb, int nb, int per_col, int band, int nlink, int link_nz,
+                                unsigned long long seed, int *m, int *n, int *nz, int *kA, int *iA, double *A,
+                                double *b, double *c, double *xs, double *ys, double *ws, double *zs);
+
 int ipo_hip_device_count(void);
 const char *ipo_hip_last_error(void);
 const char *ipo_hip_version(void);

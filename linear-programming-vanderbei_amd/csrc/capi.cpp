@@ -13,6 +13,7 @@
 #include "ipm.h"
 #include "kkt_device.h"
 #include "lp_io.h"
+#include "synth.h"
 
 namespace {
 
@@ -443,5 +444,58 @@ int ipo_hip_device_count(void) {
 
 const char* ipo_hip_last_error(void) { return g_err.c_str(); }
 const char* ipo_hip_version(void) { return "ipo-hip 0.1 (gfx950)"; }
+
+}  // extern "C"
+
+namespace {
+void synth_out(const ipo::SynthLP& o, int* kA, int* iA, double* A, double* b, double* c, double* xs, double* ys,
+               double* ws, double* zs) {
+    std::copy(o.kA.begin(), o.kA.end(), kA);
+    std::copy(o.iA.begin(), o.iA.end(), iA);
+    std::copy(o.A.begin(), o.A.end(), A);
+    std::copy(o.b.begin(), o.b.end(), b);
+    std::copy(o.c.begin(), o.c.end(), c);
+    if (xs) std::copy(o.xs.begin(), o.xs.end(), xs);
+    if (ys) std::copy(o.ys.begin(), o.ys.end(), ys);
+    if (ws) std::copy(o.ws.begin(), o.ws.end(), ws);
+    if (zs) std::copy(o.zs.begin(), o.zs.end(), zs);
+}
+}  // namespace
+
+extern "C" {
+
+int ipo_hip_synth_random(int m, int n, int per_col, int band, unsigned long long seed, int* nz, int* kA, int* iA,
+                         double* A, double* b, double* c, double* xs, double* ys, double* ws, double* zs) {
+    try {
+        if (nz) *nz = static_cast<int>(static_cast<long long>(n) * per_col);
+        if (!kA) return 0;
+        ipo::SynthLP o;
+        ipo::synth_random(m, n, per_col, band, seed, o);
+        synth_out(o, kA, iA, A, b, c, xs, ys, ws, zs);
+        return 0;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
+
+int ipo_hip_synth_block_angular(int nblocks, int mb, int nb, int per_col, int band, int nlink, int link_nz,
+                                unsigned long long seed, int* m, int* n, int* nz, int* kA, int* iA, double* A,
+                                double* b, double* c, double* xs, double* ys, double* ws, double* zs) {
+    try {
+        if (m) *m = nblocks * mb + nlink;
+        if (n) *n = nblocks * nb;
+        if (nz) *nz = static_cast<int>(static_cast<long long>(nblocks) * nb * per_col +
+                                       static_cast<long long>(nlink) * link_nz);
+        if (!kA) return 0;
+        ipo::SynthLP o;
+        ipo::synth_block_angular(nblocks, mb, nb, per_col, band, nlink, link_nz, seed, o);
+        synth_out(o, kA, iA, A, b, c, xs, ys, ws, zs);
+        return 0;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
 
 }  // extern "C"

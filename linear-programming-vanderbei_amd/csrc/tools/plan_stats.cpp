@@ -5,13 +5,24 @@
 #include <algorithm>
 #include "../kkt_plan.h"
 #include "../lp_io.h"
+#include "../synth.h"
+#include <cstdlib>
 
 int main(int argc, char** argv) {
-    if (argc < 2) { std::fprintf(stderr, "usage: plan_stats file.mps\n"); return 1; }
+    if (argc < 2) { std::fprintf(stderr, "usage: plan_stats file.mps | synth m n band | blockang K mb nb l lnz\n"); return 1; }
+    ipo::SolverForm s;
+    if (std::string(argv[1]) == "synth" || std::string(argv[1]) == "blockang") {
+        ipo::SynthLP o;
+        if (argv[1][0] == 's') ipo::synth_random(std::atoi(argv[2]), std::atoi(argv[3]), 4, std::atoi(argv[4]), 20251121, o);
+        else ipo::synth_block_angular(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), 4, 256,
+                                      std::atoi(argv[5]), std::atoi(argv[6]), 20251121, o);
+        s.m = o.m; s.n = o.n; s.nz = o.kA[o.n]; s.kA = o.kA; s.iA = o.iA; s.A = o.A;
+        argc = 2;
+    } else {
     ipo::MpsProblem p; std::string err;
     if (ipo::read_mps(argv[1], p, &err)) { std::fprintf(stderr, "read error: %s\n", err.c_str()); return 1; }
-    ipo::SolverForm s;
     if (ipo::to_solver_form(p, s)) { std::printf("free variable -> status 3\n"); return 0; }
+    }
     std::vector<int> kat, iat; std::vector<double> at;
     ipo::csc_transpose(s.m, s.n, s.kA.data(), s.iA.data(), s.A.data(), kat, iat, at);
     auto t0 = std::chrono::steady_clock::now();

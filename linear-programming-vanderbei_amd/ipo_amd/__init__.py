@@ -74,6 +74,7 @@ EXPORTED = [
     "ipo_hip_device_count", "ipo_hip_last_error", "ipo_hip_version",
     "ipo_hip_ctx_create", "ipo_hip_ctx_run", "ipo_hip_ctx_download", "ipo_hip_ctx_destroy",
     "ipo_hip_ctx_setup_seconds", "ipo_hip_kkt_set_epsdiag",
+    "ipo_hip_synth_random", "ipo_hip_synth_block_angular",
 ]
 
 _P = C.c_void_p
@@ -135,6 +136,10 @@ def lib() -> C.CDLL:
     L.ipo_hip_ctx_destroy.restype = None
     L.ipo_hip_ctx_setup_seconds.argtypes = [_P]
     L.ipo_hip_ctx_setup_seconds.restype = _D
+    L.ipo_hip_synth_random.argtypes = [_I, _I, _I, _I, C.c_ulonglong, C.POINTER(_I)] + [_P] * 9
+    L.ipo_hip_synth_random.restype = _I
+    L.ipo_hip_synth_block_angular.argtypes = [_I] * 7 + [C.c_ulonglong] + [C.POINTER(_I)] * 3 + [_P] * 9
+    L.ipo_hip_synth_block_angular.restype = _I
     L.ipo_hip_device_count.restype = _I
     L.ipo_hip_last_error.restype = C.c_char_p
     L.ipo_hip_version.restype = C.c_char_p
@@ -379,3 +384,51 @@ def symbolic(m, n, kA, iA) -> dict:
         raise IpoHipError("symbolic: " + last_error())
     return dict(perm=perm, lnz=lnz.value, narth=narth.value, denwin=denwin.value, pdf=pdf.value, nsup=nsup.value,
                 nlevels=nlev.value)
+
+
+# ----------------------------------------------------------------- synthetic LPs
+SYNTH_SEED = 20251121
+
+
+@dataclass
+class SynthProblem(SolverForm):
+    """A synthetic LP plus the interior point it was generated from."""
+    xs: np.ndarray = None
+    ys: np.ndarray = None
+    ws: np.ndarray = None
+    zs: np.ndarray = None
+    blocks: dict = None
+
+
+def _synth_arrays(m, n, nz):
+    return (np.zeros(n + 1, np.int32), np.zeros(nz, np.int32), np.zeros(nz), np.zeros(m), np.zeros(n),
+            np.zeros(n), np.zeros(m), np.zeros(m), np.zeros(n))
+
+
+def synth_random(m, n, per_col=4, band=0, seed=SYNTH_SEED) -> SynthProblem:
+    """BASELINE configs[3]: random sparse LP (band=0 uniform rows, band>0 banded)."""
+    nz = C.c_int(0)
+    L = lib()
+    if L.ipo_hip_synth_random(m, n, per_col, band, seed, C.byref(nz), *([None] * 9)):
+        raise IpoHipError("synth_random: " + last_error())
+    arrs = _synth_arrays(m, n, nz.value)
+    kA, iA, A, b, c, xs, ys, ws, zs = arrs
+    if L.ipo_hip_synth_random(m, n, per_col, band, seed, C.byref(nz), *[_ptr(a) for a in arrs]):
+        raise IpoHipError("synth_random: " + last_error())
+    return SynthProblem(m, n, kA, iA, A, b, c, 0.0, xs, ys, ws, zs)
+
+
+def synth_block_angular(nblocks=8, mb=25000, nb=100000, per_col=4, band=256, nlink=512, link_nz=2000,
+                        seed=SYNTH_SEED) -> SynthProblem:
+    """BASELINE configs[4]: block-angular LP, linking rows last."""
+    m, n, nz = C.c_int(0), C.c_int(0), C.c_int(0)
+    L = lib()
+    args = (nblocks, mb, nb, per_col, band, nlink, link_nz, seed, C.byref(m), C.byref(n), C.byref(nz))
+    if L.ipo_hip_synth_block_angular(*args, *([None] * 9)):
+        raise IpoHipError("synth_block_angular: " + last_error())
+    arrs = _synth_arrays(m.value, n.value, nz.value)
+    kA, iA, A, b, c, xs, ys, ws, zs = arrs
+    if L.ipo_hip_synth_block_angular(*args, *[_ptr(a) for a in arrs]):
+        raise IpoHipError("synth_block_angular: " + last_error())
+    return SynthProblem(m.value, n.value, kA, iA, A, b, c, 0.0, xs, ys, ws, zs,
+                        dict(nblocks=nblocks, mb=mb, nb=nb, nlink=nlink))

@@ -113,3 +113,32 @@ class OracleKkt:
             lib().orc_kkt_destroy(self.h)
         except Exception:
             pass
+
+
+class _OrcRun(C.Structure):
+    _fields_ = [("trace", C.c_void_p), ("max_iter", C.c_int), ("iters", C.c_int), ("t_setup", C.c_double),
+                ("t_total", C.c_double), ("final_mu", C.c_double), ("final_pobj", C.c_double),
+                ("final_dobj", C.c_double), ("final_pinf", C.c_double), ("final_dinf", C.c_double)]
+
+
+def solve_arrays(form, method="hsd", max_iter=200):
+    """orc_hsd / orc_intpt / orc_hsdls on a solver()-form problem (silent).
+    Returns dict(status, iters, x, y, w, z, final_*)."""
+    L = lib()
+    fn = {"hsd": L.orc_hsd, "intpt": L.orc_intpt, "hsdls": L.orc_hsdls}[method]
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_int] * 3 + [C.c_void_p] * 5 + [C.c_double] + [C.c_void_p] * 4 + [C.POINTER(_OrcRun)]
+    m, n = form.m, form.n
+    kA = np.ascontiguousarray(form.kA, np.int32)
+    iA = np.ascontiguousarray(form.iA, np.int32)
+    A = np.ascontiguousarray(form.A, np.float64)
+    b = np.ascontiguousarray(form.b, np.float64)
+    c = np.ascontiguousarray(form.c, np.float64)
+    x, z = np.zeros(n + m), np.zeros(n)
+    y, w = np.zeros(n + m), np.zeros(m)
+    run = _OrcRun(None, max_iter, 0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0)
+    st = fn(m, n, int(kA[-1]), iA.ctypes.data, kA.ctypes.data, A.ctypes.data, b.ctypes.data, c.ctypes.data,
+            float(form.f), x.ctypes.data, y.ctypes.data, w.ctypes.data, z.ctypes.data, C.byref(run))
+    return dict(status=st, iters=run.iters, x=x[:n], y=y[:m], w=w, z=z, final_mu=run.final_mu,
+                final_pobj=run.final_pobj, final_dobj=run.final_dobj, final_pinf=run.final_pinf,
+                final_dinf=run.final_dinf)
