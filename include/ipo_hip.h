@@ -94,6 +94,31 @@ void ipo_hip_ctx_download(ipo_hip_ctx *ctx, double *x, double *y, double *w, dou
 void ipo_hip_ctx_destroy(ipo_hip_ctx *ctx);
 double ipo_hip_ctx_setup_seconds(const ipo_hip_ctx *ctx);
 
+/* ---- block-angular sharding (not in the reference) --------
+ * One process per GPU.  Rank k passes its LOCAL problem: the rows and
+ * columns of its diagonal blocks plus a replica of the nlink linking rows,
+ * which must be its last nlink rows (ipo_amd.shard_block_angular builds it);
+ * m_global, n_global, nz_global describe the whole LP (mu's denominator and
+ * the trace).  The linking rows form the dense tail of every shard's KKT
+ * factor and are the only place the shards meet: one allreduce of the
+ * nlink x nlink tail per factorisation, nlink-vectors per substitution sweep
+ * and refinement pass, a few scalars per iteration.  Transport: RCCL
+ * (rccl_id = the 128-byte ncclUniqueId rank 0 got from
+ * ipo_hip_rccl_unique_id, distributed by the caller; select the device
+ * with ipo_hip_set_device first) or, with rccl_id == NULL, the host
+ * callback fn (device data staged through pinned host memory; op 0 = sum,
+ * 1 = max, 2 = min; returns 0 on success).  nranks == 1: one process, the
+ * linking rows in the tail, no exchange.  Run with ipo_hip_ctx_run /
+ * _download / _destroy; all ranks call them together (collectives).
+ * Returns NULL on error (ipo_hip_last_error). */
+typedef int (*ipo_hip_allreduce_fn)(void *user, double *buf, long n, int op);
+int ipo_hip_set_device(int device);
+int ipo_hip_rccl_unique_id(void *out128);
+ipo_hip_ctx *ipo_hip_ctx_create_shard(int m, int n, const int *kA, const int *iA, const double *A,
+                                      const double *b, const double *c, double f, int nlink,
+                                      int m_global, int n_global, long nz_global, int nranks, int rank,
+                                      const void *rccl_id, ipo_hip_allreduce_fn fn, void *user);
+
 /* Read an MPS file, normalise it like solvelp() (src/common/solve.c:28-205)
  * and solve it; prints exactly what `ipo file.mps` prints (main.c:16-58)
  * minus the .out file.  Returns the status (3 = free variable). */
@@ -122,6 +147,11 @@ void   ipo_hip_kkt_set_epsdiag(ipo_hip_kkt *k, double epsdiag);
 /* Host-only symbolic analysis (no GPU needed): reference ordering stats. */
 int ipo_hip_symbolic(int m, int n, const int *kA, const int *iA, int *perm, long *lnz, double *narth,
                      int *denwin, int *pdf, int *nsup, int *nlevels);
+/* Same with the last nforced rows (linking rows) forced to the end of the
+ * order and forming the dense tail (block-angular sharding); colcount[T]
+ * = strict-lower nonzeros per column of L in the new order. */
+int ipo_hip_symbolic_forced(int m, int n, const int *kA, const int *iA, int nforced, int *perm, int *colcount,
+                            long *lnz, int *tail_c0, int *nsup, int *nlevels);
 
 /* Synthetic LPs in solver() form (BASELINE configs[3] and configs[4],
  * SURVEY.md §8(d); not part of the reference): feasible and bounded by

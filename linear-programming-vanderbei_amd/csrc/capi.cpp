@@ -139,6 +139,7 @@ LuState* g_lu = nullptr;
 }  // namespace
 
 struct ipo_hip_ctx {
+    std::unique_ptr<ipo::Exchange> xch;          // sharded contexts; outlives the solver (declared first)
     std::unique_ptr<ipo::IpmSolver> solver;
 };
 
@@ -199,6 +200,52 @@ void ipo_hip_ctx_download(ipo_hip_ctx* ctx, double* x, double* y, double* w, dou
 void ipo_hip_ctx_destroy(ipo_hip_ctx* ctx) { delete ctx; }
 
 double ipo_hip_ctx_setup_seconds(const ipo_hip_ctx* ctx) { return ctx->solver->setup_seconds(); }
+
+int ipo_hip_set_device(int device) {
+    const hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        set_err(std::string("hipSetDevice: ") + hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int ipo_hip_rccl_unique_id(void* out128) {
+    try {
+        ipo::rccl_unique_id(out128);
+        return 0;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
+
+ipo_hip_ctx* ipo_hip_ctx_create_shard(int m, int n, const int* kA, const int* iA, const double* A, const double* b,
+                                      const double* c, double f, int nlink, int m_global, int n_global,
+                                      long nz_global, int nranks, int rank, const void* rccl_id,
+                                      ipo_hip_allreduce_fn fn, void* user) {
+    try {
+        if (nlink < 0 || nlink > m) throw std::invalid_argument("shard: nlink out of range");
+        if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("shard: bad rank / nranks");
+        auto ctx = std::make_unique<ipo_hip_ctx>();
+        if (nranks > 1) {
+            if (rccl_id) ctx->xch.reset(ipo::make_rccl_exchange(rccl_id, nranks, rank));
+            else if (fn) ctx->xch.reset(ipo::make_host_exchange(nranks, rank, fn, user));
+            else throw std::invalid_argument("shard: nranks > 1 needs an RCCL id or a host allreduce callback");
+        }
+        ipo::ShardSpec sp;
+        sp.nforced = nlink;
+        sp.xch = ctx->xch.get();
+        sp.m_global = m_global;
+        sp.n_global = n_global;
+        sp.nz_global = nz_global;
+        ctx->solver = std::make_unique<ipo::IpmSolver>(m, n, kA, iA, A, b, c, f, nullptr, &sp);
+        return ctx.release();
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return nullptr;
+    }
+}
 
 int ipo_hip_run_mps(const char* path, int method, FILE* out, int timing, ipo_hip_stats* stats) {
     if (out) {
@@ -427,6 +474,32 @@ int ipo_hip_symbolic(int m, int n, const int* kA, const int* iA, int* perm, long
         if (narth) *narth = P.narth;
         if (denwin) *denwin = P.denwin;
         if (pdf) *pdf = P.pdf;
+        if (nsup) *nsup = P.nsup;
+        if (nlevels) *nlevels = P.nlevels;
+        return 0;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
+
+int ipo_hip_symbolic_forced(int m, int n, const int* kA, const int* iA, int nforced, int* perm, int* colcount,
+                            long* lnz, int* tail_c0, int* nsup, int* nlevels) {
+    try {
+        if (nforced < 0 || nforced > m) throw std::invalid_argument("nforced out of range");
+        std::vector<int> kat, iat;
+        std::vector<double> at, a(kA[n], 1.0);
+        ipo::csc_transpose(m, n, kA, iA, a.data(), kat, iat, at);
+        ipo::KktPlan P = ipo::build_kkt_plan(m, n, kA, iA, kat.data(), iat.data(), nforced);
+        if (perm) std::memcpy(perm, P.perm.data(), sizeof(int) * P.T);
+        if (colcount) {
+            for (int s = 0; s < P.nsup; s++)
+                for (int j = P.col0[s]; j < P.col0[s + 1]; j++)
+                    colcount[j] = (P.col0[s + 1] - 1 - j) + (P.rowptr[s + 1] - P.rowptr[s]);
+            for (int j = P.tail_c0; j < P.T; j++) colcount[j] = P.T - 1 - j;
+        }
+        if (lnz) *lnz = P.lnz;
+        if (tail_c0) *tail_c0 = P.tail_c0;
         if (nsup) *nsup = P.nsup;
         if (nlevels) *nlevels = P.nlevels;
         return 0;

@@ -66,4 +66,9 @@ k_reduce_jobs(RedJobs jobs, double* __restrict__ part);
 extern bool g_ordered_reductions;
 void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st);
 
+// Linking-row products of the sharded solve (exchange.h): out[i - mrow] =
+// sum_k At[k] x[iAt[k]] for rows mrow <= i < m (CSR of A), one wave per row.
+void launch_link_ax(int mrow, int m, const int* kAt, const int* iAt, const double* At, const double* x, double* out,
+                    hipStream_t st);
+
 }  // namespace ipo

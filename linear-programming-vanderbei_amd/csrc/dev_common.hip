@@ -77,6 +77,24 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
     if (threadIdx.x == 0) out[j] = s;
 }
 
+__global__ void __launch_bounds__(256)
+k_link_ax(int mrow, int m, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
+          const double* __restrict__ x, double* __restrict__ out) {
+    const int i = mrow + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i >= m) return;
+    double s = 0.0;
+    for (int k = kAt[i] + lane; k < kAt[i + 1]; k += 64) s += At[k] * x[iAt[k]];
+    s = wave_sum(s);
+    if (lane == 0) out[i - mrow] = s;
+}
+
+void launch_link_ax(int mrow, int m, const int* kAt, const int* iAt, const double* At, const double* x, double* out,
+                    hipStream_t st) {
+    if (m <= mrow) return;
+    hipLaunchKernelGGL(k_link_ax, dim3((m - mrow + 3) / 4), dim3(256), 0, st, mrow, m, kAt, iAt, At, x, out);
+    IPO_HIP_CHECK(hipGetLastError());
+}
+
 bool g_ordered_reductions = true;
 
 void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st) {

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <memory>
 
+#include "exchange.h"
 #include "hip_util.h"
 #include "kkt_device.h"
 
@@ -38,12 +39,26 @@ struct IpmResult {
     long refine_passes = 0;
 };
 
+// One shard of a block-angular LP (not in the reference).
+// The local problem holds this shard's diagonal blocks (rows, columns) and a
+// replica of the nforced linking rows, numbered last.  Column quantities
+// (x, z) are disjoint between shards, block-row quantities (y, w) too, and
+// the linking-row values are replicated bitwise: every shard computes them
+// from the same allreduced inputs.  Sums count linking rows on rank 0 only.
+// nforced > 0 without an Exchange: one process, linking rows in the tail.
+struct ShardSpec {
+    int nforced = 0;              // linking rows = the last nforced local rows
+    Exchange* xch = nullptr;      // not owned
+    int m_global = 0, n_global = 0;
+    long nz_global = 0;
+};
+
 // Problem uploaded to HBM once; run() iterates from the reference's start
 // point and can be called repeatedly (the bench times run()).
 class IpmSolver {
   public:
     IpmSolver(int m, int n, const int* kA, const int* iA, const double* A, const double* b, const double* c,
-              double f, hipStream_t stream = nullptr);
+              double f, hipStream_t stream = nullptr, const ShardSpec* shard = nullptr);
     ~IpmSolver();
     int run(const IpmOptions& opt, IpmResult* res);
     // copy x (n), y (m), w (m), z (n) of the last run to the host
@@ -56,16 +71,28 @@ class IpmSolver {
     int run_intpt(const IpmOptions& opt, IpmResult* res);
     int run_hsdls(const IpmOptions& opt, IpmResult* res);
     void reduce(const struct RedJobs& j, int nout);
+    // sharded solve: linking-row products A_link x summed over the shards
+    // into lax_ (no-op unsharded), and the cross-shard reduction of scalars
+    void link_ax(const double* x);
+    void xsum(double* d, size_t n, RedOp op) { if (xch_) xch_->allreduce(d, n, op, stream_); }
+    const double* lax() const { return xch_ ? lax_.get() : nullptr; }
+    int mrow() const { return xch_ ? m_ - nforced_ : m_; }   // rows below are shard-local
+    void print_dims(FILE* tr) const;
 
     int m_, n_;
     double f_;
     hipStream_t stream_;
     bool own_stream_ = false;
     double t_setup_ = 0.0;
+    int nforced_ = 0;
+    Exchange* xch_ = nullptr;
+    int mcnt_ = 0;               // rows this shard counts in sums (linking rows on rank 0 only)
+    int mg_ = 0, ng_ = 0;        // global sizes (mu's denominator, the trace)
+    long nzg_ = 0;
     std::unique_ptr<KktDevice> kkt_;
     DevBuf<double> b_, c_, x_, y_, w_, z_;
     DevBuf<double> rho_, sig_, D_, E_, fx_, fy_, gx_, gy_, dx_, dy_, dz_, dw_;
-    DevBuf<double> part_, scal_;
+    DevBuf<double> part_, scal_, lax_;
     double* hs_ = nullptr;       // pinned scalars
     bool full_trace_ = false;    // IPO_HIP_TRACE_FULL: full-precision scalars per iteration on stderr
 };

@@ -3,11 +3,18 @@
 // Fused O(m+n) kernels (HBM-bound; coalesced CSR/CSC gathers, one pass per
 // phase) + the KKT factor/solve of kkt_device.hip.  Per iteration the host
 // reads back only the scalars the reference prints or branches on.
+//
+// Sharded (block-angular, ipm.h ShardSpec): the same kernels run on the
+// shard's local problem; rows >= mrow (the replicated linking rows) take
+// their A x from lax (A_link x summed over the shards), rows >= mcnt are
+// left out of the shard's partial sums, and every scalar the host reads is
+// allreduced before it is read.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "dev_common.h"
 #include "ipm.h"
@@ -36,15 +43,18 @@ k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict
                 const double* __restrict__ b, const double* __restrict__ c, const double* __restrict__ x,
                 const double* __restrict__ y, const double* __restrict__ w, const double* __restrict__ z, double phi,
                 double delta, double mu, double* __restrict__ E, double* __restrict__ D, double* __restrict__ fy,
-                double* __restrict__ fx, double* __restrict__ gy, double* __restrict__ gx, double* __restrict__ part) {
+                double* __restrict__ fx, double* __restrict__ gy, double* __restrict__ gx, double* __restrict__ part,
+                int mrow, int mcnt, const double* __restrict__ lax) {
     __shared__ double sh[4];
     double sr = 0.0, ss = 0.0;
     for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
         if (i < m) {
             double ax = 0.0;
-            for (int k = kAt[i]; k < kAt[i + 1]; k++) ax += At[k] * x[iAt[k]];
+            if (i >= mrow) ax = lax[i - mrow];      // linking row of a shard: summed over the shards
+            else
+                for (int k = kAt[i]; k < kAt[i + 1]; k++) ax += At[k] * x[iAt[k]];
             const double r1 = ax - b[i] * phi + w[i];
-            sr += r1 * r1;
+            if (i < mcnt) sr += r1 * r1;
             const double rho = -(1 - delta) * r1 + w[i] - delta * mu / y[i];
             E[i] = w[i] / y[i];
             fy[i] = rho;
@@ -169,16 +179,19 @@ k_pf_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict_
                const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
                const double* __restrict__ b, const double* __restrict__ c, const double* __restrict__ x,
                const double* __restrict__ y, const double* __restrict__ w, const double* __restrict__ z,
-               double* __restrict__ rho, double* __restrict__ sig, double* __restrict__ part) {
+               double* __restrict__ rho, double* __restrict__ sig, double* __restrict__ part, int mrow, int mcnt,
+               const double* __restrict__ lax) {
     __shared__ double sh[4];
     double sr = 0.0, ss = 0.0;
     for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
         if (i < m) {
             double ax = 0.0;
-            for (int k = kAt[i]; k < kAt[i + 1]; k++) ax += At[k] * x[iAt[k]];
+            if (i >= mrow) ax = lax[i - mrow];      // linking row of a shard: summed over the shards
+            else
+                for (int k = kAt[i]; k < kAt[i + 1]; k++) ax += At[k] * x[iAt[k]];
             const double r = b[i] - ax - w[i];
             rho[i] = r;
-            sr += r * r;
+            if (i < mcnt) sr += r * r;
         } else {
             const int j = i - m;
             double aty = 0.0;
@@ -260,14 +273,30 @@ const char* kIntptHeader =
 }  // namespace
 
 IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A, const double* b, const double* c,
-                     double f, hipStream_t stream)
+                     double f, hipStream_t stream, const ShardSpec* shard)
     : m_(m), n_(n), f_(f), stream_(stream) {
     const double t0 = now_s();
+    mg_ = m;
+    ng_ = n;
+    nzg_ = kA[n];
+    mcnt_ = m;
+    if (shard) {
+        if (shard->nforced < 0 || shard->nforced > m) throw std::invalid_argument("shard: nforced out of range");
+        nforced_ = shard->nforced;
+        xch_ = shard->xch;
+        if (xch_) {
+            mg_ = shard->m_global;
+            ng_ = shard->n_global;
+            nzg_ = shard->nz_global;
+            if (xch_->rank() != 0) mcnt_ = m - nforced_;   // linking rows are counted on rank 0
+        }
+    }
     if (!stream_) {
         IPO_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         own_stream_ = true;
     }
-    kkt_ = std::make_unique<KktDevice>(m, n, kA, iA, A, stream_);
+    kkt_ = std::make_unique<KktDevice>(m, n, kA, iA, A, stream_, nforced_);
+    kkt_->set_exchange(xch_);
     const size_t mm = m > 0 ? m : 1, nn = n > 0 ? n : 1;
     b_.upload(b, m, stream_);
     c_.upload(c, n, stream_);
@@ -277,6 +306,7 @@ IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A
     if (n == 0) c_.alloc(1);
     part_.alloc(8 * kRedBlocks);
     scal_.alloc(16);
+    lax_.alloc(nforced_ > 0 ? nforced_ : 1);
     IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hs_), 16 * sizeof(double), hipHostMallocDefault));
     IPO_HIP_CHECK(hipStreamSynchronize(stream_));
     t_setup_ = now_s() - t0;
@@ -290,9 +320,18 @@ IpmSolver::~IpmSolver() {
 
 void IpmSolver::reduce(const RedJobs& j, int nout) {
     launch_reduce(j, part_.get(), scal_.get(), stream_);
+    xsum(scal_.get(), nout, RedOp::Sum);
     IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), nout * sizeof(double), hipMemcpyDeviceToHost, stream_));
     IPO_HIP_CHECK(hipStreamSynchronize(stream_));
 }
+
+void IpmSolver::link_ax(const double* x) {
+    if (!xch_ || nforced_ == 0) return;
+    launch_link_ax(m_ - nforced_, m_, kkt_->kAt(), kkt_->iAt(), kkt_->At(), x, lax_.get(), stream_);
+    xsum(lax_.get(), nforced_, RedOp::Sum);
+}
+
+void IpmSolver::print_dims(FILE* tr) const { std::fprintf(tr, "m = %d,n = %d,nz = %ld\n", mg_, ng_, nzg_); }
 
 void IpmSolver::download(double* x, double* y, double* w, double* z) const {
     if (x) x_.download(x, n_, stream_);
@@ -330,7 +369,7 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
     hipLaunchKernelGGL(k_fill, dim3(ceil_div(m, NT)), dim3(NT), 0, s, m, 1.0, y_.get());
     double phi = 1.0, psi = 1.0;
     if (tr) {
-        std::fprintf(tr, "m = %d,n = %d,nz = %d\n", m, n, kkt_->plan().amap.empty() ? 0 : (int)kkt_->plan().amap.size());
+        print_dims(tr);
         std::fputs(kHsdHeader, tr);
         std::fflush(tr);
     }
@@ -340,11 +379,11 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
         RedJobs j{};
         j.nj = 4;
         j.a[0] = z_.get(); j.b[0] = x_.get(); j.len[0] = n; j.op[0] = 0;
-        j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = m; j.op[1] = 0;
+        j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = mcnt_; j.op[1] = 0;
         j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
-        j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = m; j.op[3] = 0;
+        j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = mcnt_; j.op[3] = 0;
         reduce(j, 4);
-        const double mu = (hs_[0] + hs_[1] + phi * psi) / (n + m + 1);
+        const double mu = (hs_[0] + hs_[1] + phi * psi) / (ng_ + mg_ + 1);
         const double delta = (iter % 2 == 0) ? 0.0 : 1.0;
         const double pobj = hs_[2], dobj = hs_[3];
         if (mu < 1.0e-12) {
@@ -354,10 +393,13 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
             else { if (tr) std::fprintf(tr, "Trouble in river city \n"); status = 4; }
             break;
         }
+        link_ax(x_.get());
         hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(NT), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
                            K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), phi, delta, mu,
-                           E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get());
+                           E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get(), mrow(), mcnt_,
+                           lax());
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get());
+        xsum(scal_.get(), 2, RedOp::Sum);
         IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         const double normr = std::sqrt(hs_[0]) / phi;
@@ -382,9 +424,9 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
         RedJobs q{};
         q.nj = 4;
         q.a[0] = c_.get(); q.b[0] = fx_.get(); q.len[0] = n; q.op[0] = 0;
-        q.a[1] = b_.get(); q.b[1] = fy_.get(); q.len[1] = m; q.op[1] = 0;
+        q.a[1] = b_.get(); q.b[1] = fy_.get(); q.len[1] = mcnt_; q.op[1] = 0;
         q.a[2] = c_.get(); q.b[2] = gx_.get(); q.len[2] = n; q.op[2] = 0;
-        q.a[3] = b_.get(); q.b[3] = gy_.get(); q.len[3] = m; q.op[3] = 0;
+        q.a[3] = b_.get(); q.b[3] = gy_.get(); q.len[3] = mcnt_; q.op[3] = 0;
         reduce(q, 4);
         const double dphi = (hs_[0] - hs_[1] + gamma) / (hs_[2] - hs_[3] - psi / phi);
         const double dpsi = delta * mu / phi - psi - (psi / phi) * dphi;
@@ -393,6 +435,7 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
                            gx_.get(), fy_.get(), gy_.get(), x_.get(), z_.get(), y_.get(), w_.get(), D_.get(), E_.get(),
                            dx_.get(), dz_.get(), dy_.get(), dw_.get(), part_.get());
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 1, 1u, scal_.get());
+        xsum(scal_.get(), 1, RedOp::Max);
         IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         double theta = hs_[0];
@@ -427,7 +470,7 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
     hipLaunchKernelGGL(k_fill, dim3(ceil_div(m, NT)), dim3(NT), 0, s, m, 1.0, y_.get());
     double phi = 1.0, psi = 1.0;
     if (tr) {
-        std::fprintf(tr, "m = %d,n = %d,nz = %d\n", m, n, (int)kkt_->plan().amap.size());
+        print_dims(tr);
         std::fputs(kHsdHeader, tr);
         std::fflush(tr);
     }
@@ -438,11 +481,11 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
         RedJobs j{};
         j.nj = 4;
         j.a[0] = z_.get(); j.b[0] = x_.get(); j.len[0] = n; j.op[0] = 0;
-        j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = m; j.op[1] = 0;
+        j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = mcnt_; j.op[1] = 0;
         j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
-        j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = m; j.op[3] = 0;
+        j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = mcnt_; j.op[3] = 0;
         reduce(j, 4);
-        const double mu = (hs_[0] + hs_[1] + phi * psi) / (n + m + 1);
+        const double mu = (hs_[0] + hs_[1] + phi * psi) / (ng_ + mg_ + 1);
         const double pobj = hs_[2], dobj = hs_[3];
         if (mu < 1.0e-12) {                                   // hsdls.c:131-153
             if (phi > 1.0e-12) status = 0;
@@ -451,10 +494,13 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
             else status = 7;
             break;
         }
+        link_ax(x_.get());
         hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(NT), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
                            K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), phi, delta, mu,
-                           E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get());
+                           E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get(), mrow(), mcnt_,
+                           lax());
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get());
+        xsum(scal_.get(), 2, RedOp::Sum);
         IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         const double normr = std::sqrt(hs_[0]) / phi;
@@ -477,9 +523,9 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
         RedJobs q{};
         q.nj = 4;
         q.a[0] = c_.get(); q.b[0] = fx_.get(); q.len[0] = n; q.op[0] = 0;
-        q.a[1] = b_.get(); q.b[1] = fy_.get(); q.len[1] = m; q.op[1] = 0;
+        q.a[1] = b_.get(); q.b[1] = fy_.get(); q.len[1] = mcnt_; q.op[1] = 0;
         q.a[2] = c_.get(); q.b[2] = gx_.get(); q.len[2] = n; q.op[2] = 0;
-        q.a[3] = b_.get(); q.b[3] = gy_.get(); q.len[3] = m; q.op[3] = 0;
+        q.a[3] = b_.get(); q.b[3] = gy_.get(); q.len[3] = mcnt_; q.op[3] = 0;
         reduce(q, 4);
         const double dphi = (hs_[0] - hs_[1] + gamma) / (hs_[2] - hs_[3] - psi / phi);
         const double dpsi = delta * mu / phi - psi - (psi / phi) * dphi;
@@ -488,6 +534,7 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
                            gx_.get(), fy_.get(), gy_.get(), x_.get(), z_.get(), y_.get(), w_.get(), D_.get(), E_.get(),
                            dx_.get(), dz_.get(), dy_.get(), dw_.get(), part_.get());
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 1, 1u, scal_.get());
+        xsum(scal_.get(), 1, RedOp::Max);
         IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         double theta = 1.0;
@@ -521,24 +568,27 @@ int IpmSolver::run_intpt(const IpmOptions& opt, IpmResult* res) {
     const double delta = 0.02, r = 0.9;
     double normr0 = HUGE_VAL, norms0 = HUGE_VAL;
     if (tr) {
-        std::fprintf(tr, "m = %d,n = %d,nz = %d\n", m, n, (int)kkt_->plan().amap.size());
+        print_dims(tr);
         std::fputs(kIntptHeader, tr);
         std::fflush(tr);
     }
     KktDevice& K = *kkt_;
     int status = 5, iter;
     for (iter = 0; iter < opt.max_iter; iter++) {
+        link_ax(x_.get());
         hipLaunchKernelGGL(k_pf_residuals, dim3(kRedBlocks), dim3(NT), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
                            K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), rho_.get(),
-                           sig_.get(), part_.get());
+                           sig_.get(), part_.get(), mrow(), mcnt_, lax());
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get() + 8);
         RedJobs j{};
         j.nj = 4;
         j.a[0] = z_.get(); j.b[0] = x_.get(); j.len[0] = n; j.op[0] = 0;
-        j.a[1] = y_.get(); j.b[1] = w_.get(); j.len[1] = m; j.op[1] = 0;
+        j.a[1] = y_.get(); j.b[1] = w_.get(); j.len[1] = mcnt_; j.op[1] = 0;
         j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
-        j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = m; j.op[3] = 0;
+        j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = mcnt_; j.op[3] = 0;
         launch_reduce(j, part_.get(), scal_.get(), s);
+        xsum(scal_.get(), 4, RedOp::Sum);
+        xsum(scal_.get() + 8, 2, RedOp::Sum);
         IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 10 * sizeof(double), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         // intpt.c:47 keeps the printed quantities in single precision
@@ -556,7 +606,7 @@ int IpmSolver::run_intpt(const IpmOptions& opt, IpmResult* res) {
         if (normr < 1.0e-6 && norms < 1.0e-6 && gamma < 1.0e-6) { status = 0; break; }
         if (normr > 10 * normr0) { status = 2; break; }
         if (norms > 10 * norms0) { status = 4; break; }
-        const double mu = delta * gamma / (n + m);
+        const double mu = delta * gamma / (ng_ + mg_);
         hipLaunchKernelGGL(k_pf_rhs, dim3(gv), dim3(NT), 0, s, m, n, mu, x_.get(), z_.get(), y_.get(), w_.get(),
                            rho_.get(), sig_.get(), D_.get(), E_.get(), dx_.get(), dy_.get());
         K.factor(E_.get(), D_.get());
@@ -565,6 +615,7 @@ int IpmSolver::run_intpt(const IpmOptions& opt, IpmResult* res) {
         hipLaunchKernelGGL(k_pf_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, mu, x_.get(), z_.get(), y_.get(),
                            w_.get(), D_.get(), E_.get(), dx_.get(), dy_.get(), dz_.get(), dw_.get(), part_.get());
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 1, 1u, scal_.get());
+        xsum(scal_.get(), 1, RedOp::Max);
         IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         double theta = hs_[0];

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "hip_util.h"
+#include "exchange.h"
 #include "kkt_plan.h"
 
 namespace ipo {
@@ -46,12 +47,18 @@ class KktDevice {
   public:
     // A is the solver's m x n matrix (CSC).  The plan (ordering, supernodes)
     // is computed here on the host.  kA/iA/A must outlive nothing: copied.
-    KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream);
+    // nforced > 0: the last nforced rows (linking rows of a block-angular
+    // shard) form the dense tail (kkt_plan.h); with an Exchange set, the
+    // tail Schur complement, the tail right-hand sides and the refinement
+    // residual of those rows are summed over the shards (exchange.h).
+    KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream, int nforced = 0);
     ~KktDevice();
     KktDevice(const KktDevice&) = delete;
     KktDevice& operator=(const KktDevice&) = delete;
 
     const KktPlan& plan() const { return plan_; }
+    void set_exchange(Exchange* x) { xch_ = x; }
+    int nforced() const { return nforced_; }
     int m() const { return m_; }
     int n() const { return n_; }
     hipStream_t stream() const { return stream_; }
@@ -96,6 +103,8 @@ class KktDevice {
     template <int R>
     void sweep(double* dz, const double* epsp);
     void sweep_blocked(double* dz, const double* epsp);
+    void tail_rhs_begin(double* dz, int R);
+    void tail_rhs_end(double* dz, int R);
     size_t ybuf_stride_ = 1, partial_stride_ = 1;
     DevBuf<int> dIncons_;          // per right-hand side: inconsistent-system flag
     int launch_gather(const struct PlanView& pv, const TailView& tv, int tail, int group, hipStream_t s);
@@ -103,6 +112,11 @@ class KktDevice {
     void launch_reduce_maxabs2(const double* a, int na, const double* b, int nb, double* dst);
 
     int m_, n_, T_;
+    int nforced_ = 0;
+    Exchange* xch_ = nullptr;      // not owned
+    DevBuf<double> dLinkAx_;       // [2 * nforced] linking-row products A_link dx per right-hand side
+    bool shard_minor() const { return xch_ && xch_->rank() != 0; }   // holds replicas of the linking rows
+    void xsum(double* d, size_t n, RedOp op) { if (xch_) xch_->allreduce(d, n, op, stream_); }
     hipStream_t stream_;
     KktPlan plan_;
     double epsdiag_ = 1.0e-14;     // ldlt.c:31, grows x10 (ldlt.c:301-305)

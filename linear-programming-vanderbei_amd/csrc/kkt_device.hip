@@ -52,11 +52,13 @@ k_assemble_A(int nz, const double* __restrict__ A, const int64_t* __restrict__ a
 __global__ void __launch_bounds__(NT)
 k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __restrict__ E,
                 const double* __restrict__ D, double eps, const int64_t* __restrict__ dslot,
-                double* __restrict__ Lx, int* __restrict__ live, double* __restrict__ dscale) {
+                double* __restrict__ Lx, int* __restrict__ live, double* __restrict__ dscale, int tail_from) {
     const int v = blockIdx.x * NT + threadIdx.x;
     if (v >= T) return;
     const int old = perm[v];
-    const double a = old < m ? -ref_max(E[old], eps) : ref_max(D[old - m], eps);
+    // columns >= tail_from: replicated linking rows of a non-leading shard,
+    // whose diagonal enters the summed tail once (from shard 0)
+    const double a = v >= tail_from ? 0.0 : old < m ? -ref_max(E[old], eps) : ref_max(D[old - m], eps);
     Lx[dslot[v]] = a;
     dscale[v] = fabs(a);
     live[v] = 1;
@@ -1142,13 +1144,16 @@ k_kkt_residual(int m, int n, const int* __restrict__ kAt, const int* __restrict_
                const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
                const double* __restrict__ E, const double* __restrict__ D, const double* __restrict__ fy,
                const double* __restrict__ fx, const double* __restrict__ dy, const double* __restrict__ dx,
-               double* __restrict__ ry, double* __restrict__ rx, double* __restrict__ part) {
+               double* __restrict__ ry, double* __restrict__ rx, double* __restrict__ part, int mrow,
+               const double* __restrict__ axl) {
     __shared__ double sh[4];
     double mx = 0.0;
     for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
         if (i < m) {
             double s = 0.0;
-            for (int k = kAt[i]; k < kAt[i + 1]; k++) s += At[k] * dx[iAt[k]];
+            if (i >= mrow) s = axl[i - mrow];      // linking row: product summed over the shards
+            else
+                for (int k = kAt[i]; k < kAt[i + 1]; k++) s += At[k] * dx[iAt[k]];
             const double r = fy[i] - (s - E[i] * dy[i]);
             ry[i] = r;
             mx = fmax(mx, ref_abs(r));
@@ -1176,16 +1181,18 @@ k_min_abs_partial(const double* __restrict__ d, int T, double* __restrict__ part
 }
 
 __global__ void k_scale_scalar(double* e, double f) { e[0] *= f; }
+__global__ void k_flag_to_scalar(const int* f, double* d) { d[0] = static_cast<double>(f[0]); }
 
 }  // namespace
 
 // ======================================================================
-KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream)
-    : m_(m), n_(n), T_(m + n), stream_(stream) {
+KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream, int nforced)
+    : m_(m), n_(n), T_(m + n), nforced_(nforced), stream_(stream) {
     std::vector<int> kat, iat;
     std::vector<double> at;
     csc_transpose(m, n, kA, iA, A, kat, iat, at);
-    plan_ = build_kkt_plan(m, n, kA, iA, kat.data(), iat.data());
+    plan_ = build_kkt_plan(m, n, kA, iA, kat.data(), iat.data(), nforced);
+    if (nforced > 0) dLinkAx_.alloc(2 * static_cast<size_t>(nforced));
     const int nz = kA[n];
     hipStream_t s = stream_;
     dkA_.upload(kA, n + 1, s);
@@ -1470,7 +1477,7 @@ void KktDevice::factor(const double* dE, const double* dD) {
     IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get(), 0, 2 * sizeof(int), s));
     if (nz > 0) hipLaunchKernelGGL(k_assemble_A, dim3(ceil_div(nz, NT)), dim3(NT), 0, s, nz, dA_.get(), damap_.get(), dLx_.get());
     hipLaunchKernelGGL(k_assemble_diag, dim3(ceil_div(T_, NT)), dim3(NT), 0, s, T_, m_, dperm_.get(), dE, dD, epsdiag_,
-                       ddslot_.get(), dLx_.get(), dLive_.get(), dDscale_.get());
+                       ddslot_.get(), dLx_.get(), dLive_.get(), dDscale_.get(), shard_minor() ? plan_.tail_c0 : T_);
     const TailView tv = tail_view();
     for (int l = 0; l < plan_.nlevels; l++) {
         const int u0 = plan_.unit_level_ptr[l], u1 = plan_.unit_level_ptr[l + 1];
@@ -1492,6 +1499,9 @@ void KktDevice::factor(const double* dE, const double* dD) {
         ph_begin(s);
         const int nl = launch_gather(pv, tv, 0, plan_.nlevels, s);
         ph_end(kPhGather, nl, s);
+        // shards: S = sum of every shard's assembled + gathered tail (exchange.h)
+        xsum(tv.S, static_cast<size_t>(plan_.nt) * plan_.nt, RedOp::Sum);
+        xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
         for (int kb = 0; kb < plan_.ntb; kb++) {
             const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
             ph_begin(s);
@@ -1513,7 +1523,11 @@ void KktDevice::factor(const double* dE, const double* dD) {
     // min |d| over the factor (ldlt.c:293-306) and the dependent-pivot count
     hipLaunchKernelGGL(k_min_abs_partial, dim3(kRedBlocks), dim3(NT), 0, s, dDg_.get(), T_, dPart_.get());
     hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), 1, 1u, dScal_.get());
-    IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+    if (xch_) {   // every shard must take the same eps_diag / dependent-pivot decisions
+        hipLaunchKernelGGL(k_flag_to_scalar, dim3(1), dim3(1), 0, s, dFlags_.get(), dScal_.get() + 1);
+        xsum(dScal_.get(), 2, RedOp::Max);
+    }
+    IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
     IPO_HIP_CHECK(hipMemcpyAsync(hFlags_, dFlags_.get(), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
     IPO_HIP_CHECK(hipStreamSynchronize(s));
@@ -1525,7 +1539,7 @@ void KktDevice::factor(const double* dE, const double* dD) {
         for (int ph : {kPhGather, kPhDiag, kPhTrsm, kPhSyrk}) tm_.phase_count[ph]++;
     }
     tm_.factors++;
-    ndep_ = hFlags_[0];
+    ndep_ = xch_ ? static_cast<int>(hScal_[1]) : hFlags_[0];
     if (-hScal_[0] < 1.0e-14) epsdiag_ *= 10;
 }
 
@@ -1604,8 +1618,10 @@ void KktDevice::sweep(double* dz, const double* epsp) {
     }
     if (plan_.nt > 0) {
         const TailView tv = tail_view();
+        tail_rhs_begin(dz, R);
         hipLaunchKernelGGL(k_tail_gather<R>, dim3(ceil_div(plan_.nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(),
                            dyrow_idx_.get(), V);
+        tail_rhs_end(dz, R);
         hipLaunchKernelGGL(k_tail_fwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
                            dChainFlags_.get(), ++chain_epoch_);
     }
@@ -1664,8 +1680,10 @@ void KktDevice::sweep_blocked(double* dz, const double* epsp) {
     }
     const TailView tv = tail_view();
     const int nt = plan_.nt;
+    tail_rhs_begin(dz, 1);
     hipLaunchKernelGGL(k_tail_gather<1>, dim3(ceil_div(nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(), dyrow_idx_.get(),
                        V);
+    tail_rhs_end(dz, 1);
     for (int kb = 0; kb < plan_.ntb; kb++) {
         const int below = nt - std::min(nt, (kb + 1) * kPanelCols);
         hipLaunchKernelGGL(k_tail_fwd, dim3(std::max(1, ceil_div(below, 64))), dim3(NT), 0, s, pv, tv, kb, dz, epsp);
@@ -1690,6 +1708,17 @@ void KktDevice::sweep_blocked(double* dz, const double* epsp) {
     IPO_HIP_CHECK(hipGetLastError());
 }
 
+// Sharded sweeps: the tail rows' right-hand side enters once (shard 0), and
+// after the gather each shard holds its own blocks' contributions: sum them.
+void KktDevice::tail_rhs_begin(double* dz, int R) {
+    if (!shard_minor()) return;
+    for (int r = 0; r < R; r++)
+        IPO_HIP_CHECK(hipMemsetAsync(dz + (size_t)r * T_ + plan_.tail_c0, 0, sizeof(double) * plan_.nt, stream_));
+}
+void KktDevice::tail_rhs_end(double* dz, int R) {
+    for (int r = 0; r < R; r++) xsum(dz + (size_t)r * T_ + plan_.tail_c0, plan_.nt, RedOp::Sum);
+}
+
 // rawsolve (ldlt.c:433-505) of R right-hand sides at dz + r * K, in place.
 void KktDevice::rawsolve(double* dz, int R) {
     hipStream_t s = stream_;
@@ -1701,6 +1730,7 @@ void KktDevice::rawsolve(double* dz, int R) {
         for (int r = 0; r < R; r++) { j.a[r] = dz + (size_t)r * T_; j.b[r] = nullptr; j.len[r] = n_; j.op[r] = 1; }
         launch_reduce(j, dPart_.get(), epsp, s);
         for (int r = 0; r < R; r++) hipLaunchKernelGGL(k_scale_scalar, dim3(1), dim3(1), 0, s, epsp + r, 1.0e-6);
+        xsum(epsp, R, RedOp::Max);
     } else {
         IPO_HIP_CHECK(hipMemsetAsync(epsp, 0, R * sizeof(double), s));
     }
@@ -1735,6 +1765,7 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
             j.a[2 * r + 1] = dfy[r]; j.b[2 * r + 1] = nullptr; j.len[2 * r + 1] = m; j.op[2 * r + 1] = 1;
         }
         launch_reduce(j, dPart_.get(), dScal_.get(), s);
+        xsum(dScal_.get(), 2 * R, RedOp::Max);
         IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 2 * R * sizeof(double), hipMemcpyDeviceToHost, s));
     }
     IPO_HIP_CHECK(hipStreamSynchronize(s));
@@ -1759,13 +1790,20 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
             if (!active[r]) continue;
             hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), zv(r), dyv(r),
                                dxv(r), pass[r] == 0 ? 0 : 1);
+            const int mrow = xch_ ? m - nforced_ : m;
+            double* axl = dLinkAx_.get() + (size_t)r * nforced_;
+            if (xch_) {
+                launch_link_ax(mrow, m, dkAt_.get(), diAt_.get(), dAt_.get(), dxv(r), axl, s);
+                xsum(axl, nforced_, RedOp::Sum);
+            }
             hipLaunchKernelGGL(k_kkt_residual, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dkAt_.get(), diAt_.get(),
                                dAt_.get(), dkA_.get(), diA_.get(), dA_.get(), dE, dD, dfy[r], dfx[r], dyv(r), dxv(r),
-                               ryv(r), rxv(r), dPart_.get() + (size_t)nq * kRedBlocks);
+                               ryv(r), rxv(r), dPart_.get() + (size_t)nq * kRedBlocks, mrow, axl);
             nq++;
         }
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), nq, (1u << nq) - 1u,
                            dScal_.get());
+        xsum(dScal_.get(), nq, RedOp::Max);
         IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), nq * sizeof(double), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         int q = 0;

@@ -37,9 +37,18 @@ struct KktOrdering {
     double narth = 0.0;            // reference op count (ldlt.c:1243-1248)
 };
 
-// ldlt.c:638-858 (inv_sym) + ldlt.c:860-1262 (lltsym), method _MD, dense = 3
+// ldlt.c:638-858 (inv_sym) + ldlt.c:860-1262 (lltsym), method _MD, dense = 3.
+//
+// nforced > 0 (not in the reference; block-angular sharding, SURVEY.md
+// §8(e)): the last nforced y-nodes (rows m-nforced..m-1, the linking rows)
+// are left out of the minimum-degree graph and placed last in natural
+// order, and the factor's dense tail is exactly those rows -- the role the
+// reference's tier penalty (ldlt.c:994-999) plays for its dense window.
+// Every other column's pattern is then independent of the rest of the
+// problem, so blocks that share only the linking rows factor apart and meet
+// in the tail.  nforced = 0 is the reference ordering, unchanged.
 KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
-                                    const int* kAt, const int* iAt);
+                                    const int* kAt, const int* iAt, int nforced = 0);
 
 // One gather task into a 64x64 tile of the dense tail: the tail rows of
 // source panel `src` whose positions inside the tile's row block (rmask)
@@ -134,6 +143,7 @@ struct KktPlan {
     double bytes_update = 0.0;      // algorithmic bytes of k_update per factorisation
 };
 
-KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt);
+KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
+                       int nforced = 0);
 
 }  // namespace ipo

@@ -5,6 +5,7 @@
 #include "kkt_plan.h"
 
 #include <algorithm>
+#include <iterator>
 #include <cmath>
 #include <stdexcept>
 
@@ -45,10 +46,65 @@ struct KeyHeap {
     }
 };
 
+// Forced tail (kkt_plan.h): the free columns [0, Tfree) are ordered and
+// their free-row pattern is known; the forced rows (y-nodes mf..m-1) go
+// last in natural order.  No path between two free nodes runs through a
+// forced node (those come later), so the free pattern is unchanged and the
+// forced part of column s is  F(s) = adjF(s) U (F(c) of every etree child c),
+// the standard row-merge rule restricted to the forced rows.
+void add_forced_tail(KktOrdering& o, int m, const int* kA, const int* iA, int nforced) {
+    const int T = o.T, Tfree = T - nforced, mf = m - nforced;
+    for (int k = 0; k < nforced; k++) {
+        o.perm[Tfree + k] = mf + k;
+        o.iperm[mf + k] = Tfree + k;
+    }
+    std::vector<std::vector<int>> F(Tfree);
+    for (int s = 0; s < Tfree; s++) {
+        const int v = o.perm[s];
+        std::vector<int>& f = F[s];
+        if (v >= m) {                                   // x-node: its forced rows
+            std::vector<int> a;
+            for (int k = kA[v - m]; k < kA[v - m + 1]; k++)
+                if (iA[k] >= mf) a.push_back(Tfree + iA[k] - mf);
+            std::sort(a.begin(), a.end());
+            std::vector<int> u;
+            std::set_union(f.begin(), f.end(), a.begin(), a.end(), std::back_inserter(u));
+            f.swap(u);
+        }
+        // parent: first free row below, else the first forced row
+        int par = -1;
+        if (o.Lp[s + 1] > o.Lp[s]) par = o.Li[o.Lp[s]];
+        if (par >= 0 && par < Tfree) {
+            std::vector<int>& g = F[par];
+            std::vector<int> u;
+            std::set_union(g.begin(), g.end(), f.begin(), f.end(), std::back_inserter(u));
+            g.swap(u);
+        }
+    }
+    std::vector<int> Lp(T + 1, 0), Li;
+    size_t tot = static_cast<size_t>(o.Lp[Tfree]);
+    for (int s = 0; s < Tfree; s++) tot += F[s].size();
+    tot += static_cast<size_t>(nforced) * (nforced - 1) / 2;
+    Li.reserve(tot);
+    for (int s = 0; s < Tfree; s++) {
+        Li.insert(Li.end(), o.Li.begin() + o.Lp[s], o.Li.begin() + o.Lp[s + 1]);
+        Li.insert(Li.end(), F[s].begin(), F[s].end());
+        std::vector<int>().swap(F[s]);
+        Lp[s + 1] = static_cast<int>(Li.size());
+    }
+    for (int k = 0; k < nforced; k++) {                 // dense lower triangle
+        for (int r = Tfree + k + 1; r < T; r++) Li.push_back(r);
+        Lp[Tfree + k + 1] = static_cast<int>(Li.size());
+    }
+    o.Lp.swap(Lp);
+    o.Li.swap(Li);
+    o.denwin = Tfree;
+}
+
 }  // namespace
 
 KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
-                                    const int* kAt, const int* iAt) {
+                                    const int* kAt, const int* iAt, int nforced) {
     KktOrdering o;
     o.m = m; o.n = n; o.T = m + n;
     const int T = o.T;
@@ -70,16 +126,20 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
     o.pdf = (3 * fill_y_first <= fill_x_first) ? 1 : 2;
 
     // adjacency of K, y-node r lists its x-nodes (column order), x-node c its rows
+    // forced rows (y-nodes mf..m-1, see kkt_plan.h) stay out of the graph
+    const int mf = m - nforced;
     std::vector<std::vector<int>> nb(T);
     std::vector<int> tier(T);
-    for (int r = 0; r < m; r++) {
+    for (int r = 0; r < mf; r++) {
         nb[r].reserve(kAt[r + 1] - kAt[r]);
         for (int k = kAt[r]; k < kAt[r + 1]; k++) nb[r].push_back(m + iAt[k]);
         tier[r] = o.pdf == 1 ? 0 : 1;
     }
+    for (int r = mf; r < m; r++) tier[r] = 0;
     for (int c = 0; c < n; c++) {
         nb[m + c].reserve(kA[c + 1] - kA[c]);
-        for (int k = kA[c]; k < kA[c + 1]; k++) nb[m + c].push_back(iA[k]);
+        for (int k = kA[c]; k < kA[c + 1]; k++)
+            if (iA[k] < mf) nb[m + c].push_back(iA[k]);
         tier[m + c] = o.pdf == 1 ? 1 : 0;
     }
     // the reference's dense-column threshold always evaluates to 3 for ipo
@@ -93,6 +153,7 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
         if (d > dense_deg && tier[v] == 0) tier[v] = 1;
         key[v] = d + tier[v] * penalty;
     }
+    for (int r = mf; r < m; r++) key[r] = 4 * penalty;    // never chosen before the free nodes
     KeyHeap hp;
     hp.key = &key;
     hp.slot.assign(T + 1, 0);
@@ -111,7 +172,8 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
     lrows.reserve(static_cast<size_t>(kA[n]) * 2);
 
     int stamp = 0, step = 0, denwin = T;
-    while (step < T) {
+    const int Tfree = T - nforced;
+    while (step < Tfree) {
         const int piv = hp.slot[1];
         const int dg = static_cast<int>(nb[piv].size());
         if (dg >= T - 1 - step) denwin = step;
@@ -187,15 +249,16 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
     o.denwin = denwin;
     o.Li.resize(lrows.size());
     for (size_t k = 0; k < lrows.size(); k++) o.Li[k] = iperm[lrows[k]];
-    for (int v = 0; v < T; v++) std::sort(o.Li.begin() + o.Lp[v], o.Li.begin() + o.Lp[v + 1]);
+    for (int v = 0; v < Tfree; v++) std::sort(o.Li.begin() + o.Lp[v], o.Li.begin() + o.Lp[v + 1]);
+    if (nforced > 0) add_forced_tail(o, m, kA, iA, nforced);
     double na = 0.0;
     for (int v = 0; v < T; v++) { double c = o.Lp[v + 1] - o.Lp[v]; na += c * c; }
     o.narth = na + 3.0 * o.Lp[T] + T;
     return o;
 }
 
-KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt) {
-    KktOrdering o = order_tiered_min_degree(m, n, kA, iA, kAt, iAt);
+KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced) {
+    KktOrdering o = order_tiered_min_degree(m, n, kA, iA, kAt, iAt, nforced);
     KktPlan P;
     P.m = m; P.n = n; P.T = o.T;
     const int T = o.T;
@@ -211,8 +274,12 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
     // ---- dense tail: the maximal suffix of columns whose L column is full
     //      (the reference's dense window, ldlt.c:1027 / :587-590)
     int tc = T;
-    while (tc > 0 && cnt[tc - 1] == T - tc) tc--;
-    if (T - tc < kTailMin) tc = T;
+    if (nforced > 0) {
+        tc = T - nforced;               // the tail is exactly the forced rows
+    } else {
+        while (tc > 0 && cnt[tc - 1] == T - tc) tc--;
+        if (T - tc < kTailMin) tc = T;
+    }
     P.tail_c0 = tc;
     P.nt = T - tc;
     P.ntb = (P.nt + kTileRows - 1) / kTileRows;

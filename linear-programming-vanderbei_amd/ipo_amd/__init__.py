@@ -74,8 +74,12 @@ EXPORTED = [
     "ipo_hip_device_count", "ipo_hip_last_error", "ipo_hip_version",
     "ipo_hip_ctx_create", "ipo_hip_ctx_run", "ipo_hip_ctx_download", "ipo_hip_ctx_destroy",
     "ipo_hip_ctx_setup_seconds", "ipo_hip_kkt_set_epsdiag",
-    "ipo_hip_synth_random", "ipo_hip_synth_block_angular",
+    "ipo_hip_synth_random", "ipo_hip_synth_block_angular", "ipo_hip_symbolic_forced",
+    "ipo_hip_set_device", "ipo_hip_rccl_unique_id", "ipo_hip_ctx_create_shard",
 ]
+
+# int (*)(void *user, double *buf, long n, int op)  -- ipo_hip_allreduce_fn
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_long, C.c_int)
 
 _P = C.c_void_p
 _I = C.c_int
@@ -140,6 +144,15 @@ def lib() -> C.CDLL:
     L.ipo_hip_synth_random.restype = _I
     L.ipo_hip_synth_block_angular.argtypes = [_I] * 7 + [C.c_ulonglong] + [C.POINTER(_I)] * 3 + [_P] * 9
     L.ipo_hip_synth_block_angular.restype = _I
+    L.ipo_hip_symbolic_forced.argtypes = [_I, _I, _P, _P, _I, _P, _P, C.POINTER(C.c_long), C.POINTER(_I),
+                                          C.POINTER(_I), C.POINTER(_I)]
+    L.ipo_hip_symbolic_forced.restype = _I
+    L.ipo_hip_set_device.argtypes = [_I]
+    L.ipo_hip_set_device.restype = _I
+    L.ipo_hip_rccl_unique_id.argtypes = [_P]
+    L.ipo_hip_rccl_unique_id.restype = _I
+    L.ipo_hip_ctx_create_shard.argtypes = [_I, _I, _P, _P, _P, _P, _P, _D, _I, _I, _I, C.c_long, _I, _I, _P, _P, _P]
+    L.ipo_hip_ctx_create_shard.restype = _P
     L.ipo_hip_device_count.restype = _I
     L.ipo_hip_last_error.restype = C.c_char_p
     L.ipo_hip_version.restype = C.c_char_p
@@ -371,6 +384,63 @@ class Context:
             pass
 
 
+def set_device(device: int) -> None:
+    """hipSetDevice for the library's calls from this thread (one process per GPU)."""
+    if lib().ipo_hip_set_device(int(device)):
+        raise IpoHipError("set_device: " + last_error())
+
+
+def rccl_unique_id() -> bytes:
+    """128-byte ncclUniqueId for a sharded solve; rank 0 creates it, the caller distributes it."""
+    buf = C.create_string_buffer(128)
+    if lib().ipo_hip_rccl_unique_id(buf):
+        raise IpoHipError("rccl_unique_id: " + last_error())
+    return buf.raw
+
+
+class ShardContext(Context):
+    """One shard of a block-angular LP on this process's GPU (ipo_hip_ctx_create_shard).
+
+    `local` is the shard's problem from :func:`shard_block_angular` (its
+    ``blocks`` carry nlink and the global sizes).  Exchange between the
+    nranks shards: RCCL when `rccl_id` (rank 0's :func:`rccl_unique_id`) is
+    given, else `host_allreduce(buf, op)`, called with a float64 numpy view of
+    the staged data to reduce in place over all ranks (op 0 sum, 1 max,
+    2 min).  nranks == 1: one process, linking rows in the dense tail.
+    run() / solution() / close() as for :class:`Context`; every rank must
+    call run() together."""
+
+    def __init__(self, local, nranks: int = 1, rank: int = 0, rccl_id: bytes = None, host_allreduce=None):
+        require_gpu()
+        self.p = local
+        self.nranks, self.rank = nranks, rank
+        bl = local.blocks or {}
+        self._keep = [np.ascontiguousarray(local.kA, np.int32), np.ascontiguousarray(local.iA, np.int32),
+                      np.ascontiguousarray(local.A, np.float64), np.ascontiguousarray(local.b, np.float64),
+                      np.ascontiguousarray(local.c, np.float64)]
+        self._cb = None
+        cb = None
+        if rccl_id is None and host_allreduce is not None:
+            def _allreduce(user, buf, n, op):
+                try:
+                    host_allreduce(np.ctypeslib.as_array(buf, shape=(n,)), op)
+                    return 0
+                except Exception:       # noqa: BLE001 -- reported through the C side's failure path
+                    import traceback
+                    traceback.print_exc()
+                    return 1
+            self._cb = ALLREDUCE_FN(_allreduce)
+            cb = C.cast(self._cb, C.c_void_p)
+        uid = C.create_string_buffer(bytes(rccl_id), 128) if rccl_id is not None else None
+        self.h = lib().ipo_hip_ctx_create_shard(
+            local.m, local.n, *[_ptr(a) for a in self._keep], float(local.f), int(bl.get("nlink", 0)),
+            int(bl.get("m_global", local.m)), int(bl.get("n_global", local.n)), int(bl.get("nz_global", local.nz)),
+            nranks, rank, uid, cb, None)
+        if not self.h:
+            raise IpoHipError("shard ctx create: " + last_error())
+        self.setup_seconds = lib().ipo_hip_ctx_setup_seconds(self.h)
+
+
 def symbolic(m, n, kA, iA) -> dict:
     """Host-only symbolic analysis (reference ordering); no GPU needed."""
     kA = np.ascontiguousarray(kA, np.int32)
@@ -384,6 +454,20 @@ def symbolic(m, n, kA, iA) -> dict:
         raise IpoHipError("symbolic: " + last_error())
     return dict(perm=perm, lnz=lnz.value, narth=narth.value, denwin=denwin.value, pdf=pdf.value, nsup=nsup.value,
                 nlevels=nlev.value)
+
+
+def symbolic_forced(m, n, kA, iA, nforced) -> dict:
+    """Host-only symbolic analysis with the last `nforced` rows forced into the dense tail."""
+    kA = np.ascontiguousarray(kA, np.int32)
+    iA = np.ascontiguousarray(iA, np.int32)
+    perm = np.zeros(m + n, np.int32)
+    cc = np.zeros(m + n, np.int32)
+    lnz, tc, nsup, nlev = C.c_long(), C.c_int(), C.c_int(), C.c_int()
+    rc = lib().ipo_hip_symbolic_forced(m, n, _ptr(kA), _ptr(iA), nforced, _ptr(perm), _ptr(cc), C.byref(lnz),
+                                       C.byref(tc), C.byref(nsup), C.byref(nlev))
+    if rc:
+        raise IpoHipError("symbolic_forced: " + last_error())
+    return dict(perm=perm, colcount=cc, lnz=lnz.value, tail_c0=tc.value, nsup=nsup.value, nlevels=nlev.value)
 
 
 # ----------------------------------------------------------------- synthetic LPs
@@ -432,3 +516,49 @@ def synth_block_angular(nblocks=8, mb=25000, nb=100000, per_col=4, band=256, nli
         raise IpoHipError("synth_block_angular: " + last_error())
     return SynthProblem(m.value, n.value, kA, iA, A, b, c, 0.0, xs, ys, ws, zs,
                         dict(nblocks=nblocks, mb=mb, nb=nb, nlink=nlink))
+
+
+def shard_block_angular(p: SynthProblem, nshards: int, k: int) -> SynthProblem:
+    """Local LP of shard k of a block-angular problem.
+
+    Shard k owns the diagonal blocks [k B/nshards, (k+1) B/nshards) -- their
+    rows and columns -- plus a replica of every linking row, numbered after
+    its own rows.  Its A is the column slice restricted to those rows; b of
+    the linking rows and every linking-row quantity are replicated on all
+    shards.  Returns the local problem (blocks: row/column offsets in the
+    global problem)."""
+    B = p.blocks["nblocks"]
+    mb, nb, nl = p.blocks["mb"], p.blocks["nb"], p.blocks["nlink"]
+    if B % nshards:
+        raise IpoHipError(f"{B} blocks do not split evenly over {nshards} shards")
+    per = B // nshards
+    r0, r1 = k * per * mb, (k + 1) * per * mb
+    c0, c1 = k * per * nb, (k + 1) * per * nb
+    mloc = r1 - r0 + nl
+    kA = (p.kA[c0:c1 + 1] - p.kA[c0]).astype(np.int32)
+    rows = p.iA[p.kA[c0]:p.kA[c1]]
+    iA = np.where(rows >= B * mb, rows - B * mb + (r1 - r0), rows - r0).astype(np.int32)
+    A = p.A[p.kA[c0]:p.kA[c1]].copy()
+    b = np.concatenate([p.b[r0:r1], p.b[B * mb:]])
+    c = p.c[c0:c1].copy()
+    ys = np.concatenate([p.ys[r0:r1], p.ys[B * mb:]]) if p.ys is not None else None
+    ws = np.concatenate([p.ws[r0:r1], p.ws[B * mb:]]) if p.ws is not None else None
+    return SynthProblem(mloc, c1 - c0, kA, iA, A, b, c, 0.0,
+                        p.xs[c0:c1].copy() if p.xs is not None else None, ys, ws,
+                        p.zs[c0:c1].copy() if p.zs is not None else None,
+                        dict(nblocks=per, mb=mb, nb=nb, nlink=nl, row0=r0, col0=c0, shard=k, nshards=nshards,
+                             m_global=p.m, n_global=p.n, nz_global=p.nz))
+
+
+def assemble_block_angular(parts):
+    """Global (x, y, w, z) of a sharded solve from every shard's (blocks, (x, y, w, z)).
+
+    Columns and block rows concatenate in shard order; the linking rows are
+    replicated on every shard and taken from shard 0."""
+    parts = sorted(parts, key=lambda t: t[0]["shard"])
+    nl = parts[0][0]["nlink"]
+    x = np.concatenate([s[0] for _, s in parts])
+    z = np.concatenate([s[3] for _, s in parts])
+    y = np.concatenate([s[1][:len(s[1]) - nl] for _, s in parts] + [parts[0][1][1][len(parts[0][1][1]) - nl:]])
+    w = np.concatenate([s[2][:len(s[2]) - nl] for _, s in parts] + [parts[0][1][2][len(parts[0][1][2]) - nl:]])
+    return x, y, w, z

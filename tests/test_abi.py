@@ -12,6 +12,7 @@ def declared_functions():
     with open(os.path.join(REPO, "include", "ipo_hip.h")) as fh:
         text = fh.read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"typedef[^;]*;", "", text)          # function-pointer typedefs are not symbols
     names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", text)
     return sorted(set(n for n in names if n not in ("if", "while", "sizeof")))
 
