@@ -19,7 +19,16 @@ Also reported:
                    solver's stream; "phases" lists every phase the same way;
   cpu_baseline  -- the CPU oracle (oracle/, a single-threaded restatement of
                    the reference's ipo) timed on this host over a bounded
-                   sample of the same workload (rank 0, N = 1).
+                   sample of the same workload (rank 0, N = 1);
+  block_angular -- BASELINE configs[4]: the synthetic
+                   block-angular LP (8 diagonal blocks of 25,000 x 100,000,
+                   banded, + 512 linking rows of 2,000 nonzeros) solved by
+                   HSD with its blocks sharded over the N ranks, one shard
+                   per GPU, RCCL allreduce of the linking-row tail (N = 1:
+                   the same algorithm in one process).  Strong scaling (the
+                   problem is fixed); not part of `value`.  A watchdog
+                   prints the line with this leg marked "timeout" if it
+                   does not finish within --ba-timeout seconds.
 """
 import argparse
 import ctypes as C
@@ -27,6 +36,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -83,6 +93,18 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def bcast_bytes(self, data, n):
+        """rank 0's n bytes on every rank"""
+        if not self.dist:
+            return data
+        t = self.torch.zeros(n, dtype=self.torch.uint8)
+        if self.rank == 0:
+            t.copy_(self.torch.frombuffer(bytearray(data), dtype=self.torch.uint8))
+        if self.backend == "nccl":
+            t = t.cuda()
+        self.dist.broadcast(t, 0)
+        return bytes(t.cpu().numpy().tobytes())
+
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
@@ -98,6 +120,60 @@ def timed_replicas(d: Dist, run_step_block, sync):
     d.barrier()
     dt = time.perf_counter() - t0
     return res, d.max(dt)
+
+
+BA_WORKLOAD = ("synthetic block-angular LP, BASELINE configs[4]: 8 blocks of 25,000 x 100,000 (banded width 256, "
+               "4 nnz/column) + 512 linking rows x 2,000 nnz, seed 20251121, hsd")
+
+
+def block_angular_leg(d, args, sync):
+    """BASELINE configs[4] sharded over the ranks; see the module docstring."""
+    import ipo_amd
+    t0 = time.perf_counter()
+    p = ipo_amd.synth_block_angular()                  # configs[4] sizes
+    nb = p.blocks["nblocks"]
+    if nb % d.world:
+        return {"workload": BA_WORKLOAD, "error": f"{nb} blocks do not split over {d.world} ranks"}
+    loc = ipo_amd.shard_block_angular(p, d.world, d.rank)
+    dims = {"m": p.m, "n": p.n, "nz": p.nz}
+    del p
+    t_gen = time.perf_counter() - t0
+    uid = None
+    if d.world > 1:
+        ipo_amd.set_device(d.local)
+        uid = d.bcast_bytes(ipo_amd.rccl_unique_id() if d.rank == 0 else None, 128)
+    ctx = ipo_amd.ShardContext(loc, d.world, d.rank, rccl_id=uid)
+    try:
+        if args.warmup > 0:
+            ctx.run("hsd", max_iter=args.warmup)
+        (status, st, _), el = timed_replicas(d, lambda: ctx.run("hsd", max_iter=args.ba_steps), sync)
+        setup = d.max(ctx.setup_seconds)
+    finally:
+        ctx.close()
+    iters = st["iters"]
+    return {"workload": BA_WORKLOAD, "value": iters / el, "unit": "iterations/s", "scaling": "strong",
+            "n_gpus": d.world, "parallelism": f"shard{d.world}" if d.world > 1 else "one process",
+            "exchange": "RCCL allreduce over xGMI" if d.world > 1 else "none (linking rows in the dense tail)",
+            "ms_per_iteration": 1e3 * el / max(iters, 1), "iterations": iters,
+            "status": ipo_amd.STATUS_TEXT.get(status, status), "final_mu": st["final_mu"],
+            "final_pobj": st["final_pobj"], "final_dobj": st["final_dobj"], **dims,
+            "m_local": loc.m, "n_local": loc.n, "nlink": loc.blocks["nlink"], "lnz_local": st["lnz"],
+            "setup_s": setup, "generate_s": t_gen}
+
+
+def with_watchdog(seconds, fn, on_timeout):
+    """fn() under a watchdog thread: after `seconds` it calls on_timeout() and ends the process."""
+    done = threading.Event()
+
+    def dog():
+        if not done.wait(seconds):
+            on_timeout()
+            os._exit(0)
+    threading.Thread(target=dog, daemon=True).start()
+    try:
+        return fn()
+    finally:
+        done.set()
 
 
 def pmc_traffic(phase):
@@ -146,6 +222,10 @@ def main():
     ap.add_argument("--problem", default="dfl001")
     ap.add_argument("--cpu-iters", type=int, default=3, help="HSD iterations of the CPU oracle sample (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip the instrumented second solve (no roofline)")
+    ap.add_argument("--block-angular", choices=["on", "off"], default="on",
+                    help="also run BASELINE configs[4] sharded over the ranks (reported under block_angular)")
+    ap.add_argument("--ba-steps", type=int, default=200, help="MAX_ITER of the block-angular solve")
+    ap.add_argument("--ba-timeout", type=float, default=600.0, help="watchdog for the block-angular leg (s)")
     args = ap.parse_args()
 
     d = Dist()
@@ -238,9 +318,21 @@ def main():
             out["config"]["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
         except Exception as e:  # the GPU number stands on its own
             out["cpu_baseline"] = {"error": str(e)}
+    ctx.close()
+    if args.block_angular == "on":
+        def on_timeout():
+            if d.rank == 0:
+                out["block_angular"] = {"workload": BA_WORKLOAD, "error": f"timeout after {args.ba_timeout:.0f} s"}
+                print(json.dumps(out), flush=True)
+
+        def leg():
+            try:
+                return block_angular_leg(d, args, sync)
+            except Exception as e:  # noqa: BLE001 -- the headline number stands on its own
+                return {"workload": BA_WORKLOAD, "error": repr(e)}
+        out["block_angular"] = with_watchdog(args.ba_timeout, leg, on_timeout)
     if d.rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
     d.close()
 
 

@@ -228,10 +228,19 @@ ipo_hip_ctx* ipo_hip_ctx_create_shard(int m, int n, const int* kA, const int* iA
         if (nlink < 0 || nlink > m) throw std::invalid_argument("shard: nlink out of range");
         if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("shard: bad rank / nranks");
         auto ctx = std::make_unique<ipo_hip_ctx>();
-        if (nranks > 1) {
-            if (rccl_id) ctx->xch.reset(ipo::make_rccl_exchange(rccl_id, nranks, rank));
-            else if (fn) ctx->xch.reset(ipo::make_host_exchange(nranks, rank, fn, user));
-            else throw std::invalid_argument("shard: nranks > 1 needs an RCCL id or a host allreduce callback");
+        // IPO_HIP_SHARD_RCCL=1 with one rank and no transport given: a
+        // one-rank RCCL communicator, so the RCCL path runs on a single GPU
+        const bool rccl1 = nranks == 1 && !rccl_id && !fn && std::getenv("IPO_HIP_SHARD_RCCL");
+        if (rccl1) {
+            char id[128];
+            ipo::rccl_unique_id(id);
+            ctx->xch.reset(ipo::make_rccl_exchange(id, 1, 0));
+        } else if (rccl_id) {
+            ctx->xch.reset(ipo::make_rccl_exchange(rccl_id, nranks, rank));
+        } else if (fn) {
+            ctx->xch.reset(ipo::make_host_exchange(nranks, rank, fn, user));
+        } else if (nranks > 1) {
+            throw std::invalid_argument("shard: nranks > 1 needs an RCCL id or a host allreduce callback");
         }
         ipo::ShardSpec sp;
         sp.nforced = nlink;

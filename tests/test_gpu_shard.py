@@ -136,3 +136,33 @@ def test_forced_tail_single_process_matches_oracle():
                 assert pr_ < 1e-6 and du < 1e-6 and gap < 1e-6, (pr_, du, gap)
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+def test_rccl_exchange_one_rank_matches_host_exchange(monkeypatch):
+    """The RCCL transport (exchange.cpp) on a one-rank communicator against
+    the host-callback transport on one rank: both take every sharded code
+    path (summed linking-row products, allreduced tail and scalars) and a
+    one-rank allreduce is the identity, so the two solves must agree
+    bitwise -- this runs the RCCL calls of bench.py's multi-GPU leg on the
+    single-GPU box."""
+    p = ipo_amd.synth_block_angular(*DIMS)
+    loc = ipo_amd.shard_block_angular(p, 1, 0)
+    runs = []
+    for transport in ("host", "rccl"):
+        if transport == "rccl":
+            monkeypatch.setenv("IPO_HIP_SHARD_RCCL", "1")
+            ctx = ipo_amd.ShardContext(loc)
+        else:
+            ctx = ipo_amd.ShardContext(loc, 1, 0, host_allreduce=lambda buf, op: None)
+        try:
+            st, stats, text = ctx.run("hsd", trace=True)
+            runs.append((st, stats["iters"], text, ctx.solution()))
+        finally:
+            ctx.close()
+    (s0, i0, t0, sol0), (s1, i1, t1, sol1) = runs
+    assert s0 == s1 == 0 and i0 == i1 and t0 == t1
+    for a, b in zip(sol0, sol1):
+        assert np.array_equal(a, b)
+    o = oracle_lib.solve_arrays(p, "hsd")
+    assert abs(i0 - o["iters"]) <= 1
