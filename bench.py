@@ -225,7 +225,7 @@ def main():
     ap.add_argument("--block-angular", choices=["on", "off"], default="on",
                     help="also run BASELINE configs[4] sharded over the ranks (reported under block_angular)")
     ap.add_argument("--ba-steps", type=int, default=200, help="MAX_ITER of the block-angular solve")
-    ap.add_argument("--ba-timeout", type=float, default=600.0, help="watchdog for the block-angular leg (s)")
+    ap.add_argument("--ba-timeout", type=float, default=300.0, help="watchdog for the block-angular leg (s)")
     args = ap.parse_args()
 
     d = Dist()
