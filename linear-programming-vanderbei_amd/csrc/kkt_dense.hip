@@ -308,7 +308,174 @@ k_trsm(PlanView p, int u0, TailView tv, int kb) {
     solve_rows(DiagCtx{p.dscale, p.dg, p.live, p.flags, p.sign, p.tau}, panel, ld, nc, c0, rlo, rhi, wbuf, ldw, wrow0);
 }
 
+// ------------------------------------------------------------ fused panel
+// Diagonal block and the rows below it in one launch: the fast path of
+// k_diag + k_trsm.  Workgroup j of a panel (512 threads, 8 waves) holds
+//   half 0 (waves 0-3): panel rows 0..63 -- the diagonal block and, on a
+//          sparse panel with nc < 64, the first rows of R_s -- factored
+//          right-looking as factor_diag_fast does it;
+//   half 1 (waves 4-7): panel rows 64 (j + 1) .. 64 (j + 1) + 63, solved
+//          against the diagonal block column by column while it is factored.
+// Thread (row = lane, part q0 = wave & 3) keeps the entries (row, 4q + q0).
+// Every workgroup of a panel factors the diagonal block redundantly (same
+// data, same code, bitwise the same result), so no workgroup waits for
+// another; workgroup 0 stores it.  One barrier per column: before it the
+// pivot wave of half 0 publishes l(., k) and l(., k) d_k, and the half-1
+// wave owning column k publishes its rows' a(row, k); after it every half-1
+// wave forms l(row, k) = a(row, k) / d_k itself.  Per entry the operations
+// and their order are those of factor_diag_fast and solve_rows (reference
+// form l = w / d, w -= l (l11 d)), so the factor is bitwise the one of the
+// two-kernel path.  A pivot that fails the zero test stops every workgroup
+// of the panel before it writes anything and raises flags[1]: the host then
+// redoes the whole factorisation with k_diag / k_trsm, which own the
+// dependent-pivot rule (ldlt.c:600-614).
+constexpr int PNT = 512;
+
+__global__ void __launch_bounds__(PNT)
+k_panel(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j, int f0, TailView tv, int kb) {
+    __shared__ double colk[2][PC];        // l(r, k) of half 0's rows
+    __shared__ double cold[2][PC];        // l(c, k) d_k
+    __shared__ double acol[2][PC];        // a(row, k) of half 1's rows
+    __shared__ int tinys[2];
+    __shared__ double dv[PC];
+    __shared__ double B[PC][PC + 1];
+    double* panel;
+    double* wbuf = nullptr;
+    int ld, nc, h, c0, j;
+    if (fu_sup) {
+        const int s = fu_sup[f0 + blockIdx.x];
+        j = fu_j[f0 + blockIdx.x];
+        c0 = p.col0[s];
+        nc = p.col0[s + 1] - c0;
+        h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+        ld = h;
+        panel = p.Lx + p.off[s];
+    } else {
+        const int k0 = kb * PC;
+        j = blockIdx.x;
+        nc = min(PC, tv.nt - k0);
+        h = tv.nt - k0;
+        ld = tv.nt;
+        c0 = tv.tc + k0;
+        panel = tv.S + k0 + (size_t)k0 * tv.nt;
+        wbuf = tv.W;                      // rows relative to the block column, ld nt
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q0 = wv & 3;
+    const bool h1 = wv >= 4;
+    const int h0 = min(PC, h);                      // half 0's rows
+    const int row = h1 ? TR * (j + 1) + lane : lane;
+    const bool rok = h1 ? row < h : row < h0;
+    double a[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int c = 4 * q + q0;
+        const bool ok = rok && c < nc && c <= row;
+        const double t = panel[ok ? row + (size_t)c * ld : 0];
+        a[q] = ok ? t : 0.0;
+    }
+    double dsc = (!h1 && lane < nc && (lane & 3) == q0) ? p.dscale[c0 + lane] : 0.0;
+    bool tiny = false;
+#pragma unroll
+    for (int qk = 0; qk < 16; qk++) {
+        for (int pk = 0; pk < 4; pk++) {
+            const int k = 4 * qk + pk;
+            if (k >= nc || tiny) break;
+            const int buf = k & 1;
+            if (q0 == pk) {
+                if (!h1) {
+                    const double dk = lane_bcast(a[qk], k);
+                    const double dsk = lane_bcast(dsc, k);
+                    const bool tz = fabs(dk) <= p.tau * dsk;      // uniform in the wave
+                    const bool below = !tz && lane > k && lane < h0;
+                    const double l = below ? a[qk] / dk : 0.0;
+                    if (below) a[qk] = l;
+                    colk[buf][lane] = l;
+                    cold[buf][lane] = l * dk;
+                    if (lane == 0) { tinys[buf] = tz; dv[k] = dk; }
+                } else {
+                    acol[buf][lane] = a[qk];
+                }
+            }
+            __syncthreads();
+            if (tinys[buf]) { tiny = true; break; }
+            // a(row, c) -= l(row, k) (l(c, k) d_k) for c > k.  Entries right of
+            // the diagonal (c > row) and columns >= nc are updated too: nothing
+            // reads or stores them.
+            double lr;
+            bool act;
+            if (!h1) {
+                act = lane > k && lane < h0;
+                lr = act ? colk[buf][lane] : 0.0;
+            } else {
+                act = rok;
+                lr = act ? acol[buf][lane] / dv[k] : 0.0;
+                if (act && q0 == pk) a[qk] = lr;
+            }
+            if (act) {
+                double ck[16];
+#pragma unroll
+                for (int q = qk; q < 16; q++) ck[q] = cold[buf][4 * q + q0];
+                if (q0 > pk) a[qk] = a[qk] - lr * ck[qk];     // column 4 qk + q0 > k
+#pragma unroll
+                for (int q = qk + 1; q < 16; q++) a[q] = a[q] - lr * ck[q];
+                // |term| of the diagonal entry, kept by the owner of column lane
+                if (!h1 && (lane & 3) == q0) dsc = dsc + fabs(lr * cold[buf][lane]);
+            }
+        }
+    }
+    if (tiny) {
+        if (tid == 0) atomicOr(&p.flags[1], 1);
+        return;
+    }
+    // half 1: its rows of L21 (and W = L21 D on the dense tail)
+    if (h1 && rok) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int c = 4 * q + q0;
+            if (c < nc) {
+                panel[row + (size_t)c * ld] = a[q];
+                if (wbuf) wbuf[row + (size_t)c * ld] = a[q] * dv[c];
+            }
+        }
+    }
+    if (j != 0) return;
+    // workgroup 0, half 0: rows of R_s inside the first 64 rows, then L11'
+    // into the upper slot through an LDS transpose, D and mark
+    if (!h1 && lane >= nc && lane < h0) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int c = 4 * q + q0;
+            if (c < nc) {
+                panel[lane + (size_t)c * ld] = a[q];
+                if (wbuf) wbuf[lane + (size_t)c * ld] = a[q] * dv[c];
+            }
+        }
+    }
+    __syncthreads();
+    if (!h1) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) B[lane][4 * q + q0] = a[q];
+    }
+    __syncthreads();
+    if (!h1) {
+        for (int rr = q0; rr < nc; rr += 4)
+            if (lane < rr) panel[lane + (size_t)rr * ld] = B[rr][lane];
+    }
+    if (tid < nc) { p.dg[c0 + tid] = dv[tid]; p.live[c0 + tid] = 1; }
+}
+
 }  // namespace
+
+void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,
+                  int kb, hipStream_t s) {
+    if (fu_sup) {
+        if (count > 0) hipLaunchKernelGGL(k_panel, dim3(count), dim3(PNT), 0, s, pv, fu_sup, fu_j, f0, tv, -1);
+    } else {
+        const int h = tv.nt - kb * PC;
+        hipLaunchKernelGGL(k_panel, dim3(std::max(1, (h + TR - 1) / TR - 1)), dim3(PNT), 0, s, pv, nullptr, nullptr, 0,
+                           tv, kb);
+    }
+}
 
 void launch_diag(const PlanView& pv, const int* level_sups, int q0, int count, const TailView& tv, int kb,
                  hipStream_t s) {

@@ -41,6 +41,7 @@ struct KktTimers {
     double solve_ms = 0.0;    // accumulated device time of solve()
     double sweep_ms = 0.0;    // forward + backward substitution sweeps (timing mode)
     long factors = 0, solves = 0, rawsolves = 0;
+    long panel_redos = 0;     // factorisations redone without the fused panel kernels
 };
 
 class KktDevice {
@@ -157,6 +158,10 @@ class KktDevice {
     DevBuf<int> dupd_src_, dupd_r0_, dupd_r1_, drel_, dlevel_sups_;
     DevBuf<int> dyrow_ptr_, dyrow_idx_;
     DevBuf<double> dYbuf_;
+    std::vector<int> fu_ptr_;             // per level: fused panel units [fu_ptr_[l], fu_ptr_[l+1])
+    DevBuf<int> dfu_sup_, dfu_j_;         // fused panel unit -> supernode, tile pair index
+    bool use_panel_ = true;               // fused diagonal-block + panel kernels (IPO_HIP_PANEL=0: off)
+    bool factor_pass(const double* dE, const double* dD, bool fused);
     std::vector<int> chunk_ptr_;          // per level: solve chunks [chunk_ptr_[l], chunk_ptr_[l+1])
     DevBuf<int> dchunk_sup_, dchunk_r0_, dsup_chunk0_;
     DevBuf<double> dPartial_;    // backward partial sums, one 64-vector per chunk

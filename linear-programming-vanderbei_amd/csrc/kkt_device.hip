@@ -233,6 +233,20 @@ __device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], 
     __shared__ double dred[4][TR];
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
+    // every load before the first store: the compiler cannot tell that the
+    // 16 entries are distinct and would otherwise serialise 16 round trips
+    double old[2][2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int rr = wr + a * 16 + (lane >> 4) + 4 * i;
+                const int cc = wc + b * 16 + (lane & 15);
+                const bool ok = rr < g.nrow && cc < g.ncol && g.row0 + rr >= g.col0 + cc;
+                old[a][b][i] = ok ? g.out[rr + (size_t)cc * g.ld] : 0.0;
+            }
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -242,7 +256,7 @@ __device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], 
                 const int rr = wr + a * 16 + (lane >> 4) + 4 * i;
                 const int cc = wc + b * 16 + (lane & 15);
                 if (rr >= g.nrow || cc >= g.ncol || g.row0 + rr < g.col0 + cc) continue;
-                g.out[rr + (size_t)cc * g.ld] -= acc[a][b][i];
+                g.out[rr + (size_t)cc * g.ld] = old[a][b][i] - acc[a][b][i];
             }
     if (g.dscale_col) {
         dred[wv][lane] = dabs;
@@ -368,12 +382,26 @@ k_tail_syrk(PlanView p, TailView tv, int kb) {
     const int nt = tv.nt;
     const int tid = threadIdx.x;
     const double* Lcol = tv.S + (size_t)k0 * nt;      // column k0 of S
-    // W rows are stored relative to the block column: W[(row - k0) + k * nt]
-    for (int idx = tid; idx < TR * PC; idx += NT) {
-        const int rr = idx % TR, k = idx / TR;
-        const int ra = bi * TR + rr, rb = bj * TR + rr;
-        As[rr][k] = (k < nc && ra < nt) ? Lcol[ra + (size_t)k * nt] : 0.0;
-        Bs[rr][k] = (k < nc && rb < nt) ? tv.W[(rb - k0) + (size_t)k * nt] : 0.0;
+    // W rows are stored relative to the block column: W[(row - k0) + k * nt].
+    // All 32 loads of a thread are issued before its first LDS store.
+    {
+        double va[TR * PC / NT], vb[TR * PC / NT];
+#pragma unroll
+        for (int u = 0; u < TR * PC / NT; u++) {
+            const int idx = tid + u * NT, rr = idx % TR, k = idx / TR;
+            const int ra = bi * TR + rr, rb = bj * TR + rr;
+            const bool oka = k < nc && ra < nt, okb = k < nc && rb < nt;
+            const double x = Lcol[oka ? ra + (size_t)k * nt : 0];
+            const double y = tv.W[okb ? (rb - k0) + (size_t)k * nt : 0];
+            va[u] = oka ? x : 0.0;
+            vb[u] = okb ? y : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < TR * PC / NT; u++) {
+            const int idx = tid + u * NT;
+            As[idx % TR][idx / TR] = va[u];
+            Bs[idx % TR][idx / TR] = vb[u];
+        }
     }
     __syncthreads();
     const int wv = tid >> 6, lane = tid & 63;
@@ -390,14 +418,30 @@ k_tail_syrk(PlanView p, TailView tv, int kb) {
             for (int b = 0; b < 2; b++) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
     }
     const bool diag_tile = bi == bj;
+    double old[2][2][4];      // all loads before the first store (see gather_store)
+#pragma unroll
     for (int a = 0; a < 2; a++)
+#pragma unroll
         for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int rr = wr + a * 16 + (lane >> 4) + 4 * i;
+                const int cc = wc + b * 16 + (lane & 15);
+                const int rg = bi * TR + rr, cg = bj * TR + cc;
+                const bool ok = rg < nt && cg < nt && !(diag_tile && cc > rr);
+                old[a][b][i] = ok ? tv.S[rg + (size_t)cg * nt] : 0.0;
+            }
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int rr = wr + a * 16 + (lane >> 4) + 4 * i;
                 const int cc = wc + b * 16 + (lane & 15);
                 const int rg = bi * TR + rr, cg = bj * TR + cc;
                 if (rg >= nt || cg >= nt || (diag_tile && cc > rr)) continue;
-                tv.S[rg + (size_t)cg * nt] -= acc[a][b][i];
+                tv.S[rg + (size_t)cg * nt] = old[a][b][i] - acc[a][b][i];
             }
     if (diag_tile && tid < TR) {           // |terms| of the diagonal for the zero-pivot test
         const int rg = bi * TR + tid;
@@ -1222,6 +1266,24 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dupd_r1_.upload(plan_.upd_r1, s);
     drel_.upload(plan_.rel, s);
     dlevel_sups_.upload(plan_.level_sups, s);
+    {   // fused panel units (k_panel): per supernode max(1, tiles - 1) workgroups,
+        // workgroup j holding the diagonal block and 64-row tile j + 1
+        std::vector<int> fs, fj;
+        fu_ptr_.assign(plan_.nlevels + 1, 0);
+        for (int l = 0; l < plan_.nlevels; l++) {
+            for (int q = plan_.level_ptr[l]; q < plan_.level_ptr[l + 1]; q++) {
+                const int sp = plan_.level_sups[q];
+                const int h = plan_.col0[sp + 1] - plan_.col0[sp] + plan_.rowptr[sp + 1] - plan_.rowptr[sp];
+                const int nw = std::max(1, ceil_div(h, kTileRows) - 1);
+                for (int j = 0; j < nw; j++) { fs.push_back(sp); fj.push_back(j); }
+            }
+            fu_ptr_[l + 1] = static_cast<int>(fs.size());
+        }
+        dfu_sup_.upload(fs, s);
+        dfu_j_.upload(fj, s);
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        if (const char* e = std::getenv("IPO_HIP_PANEL")) use_panel_ = std::atoi(e) != 0;
+    }
     {   // solve chunks: levels holding a panel with more than kChunkRows rows below
         // its diagonal block are solved in 64-row chunks (two launches each way)
         constexpr int kChunkRows = 128;
@@ -1346,6 +1408,10 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         work_flops[kPhGather] = gf; work_bytes[kPhGather] = gb;
         work_flops[kPhDiag] = df; work_bytes[kPhDiag] = db;
         work_flops[kPhTrsm] = tf; work_bytes[kPhTrsm] = tb;
+        if (use_panel_) {   // k_panel does both: the diag phase carries the trsm work
+            work_flops[kPhDiag] += tf; work_bytes[kPhDiag] += tb;
+            work_flops[kPhTrsm] = work_bytes[kPhTrsm] = 0;
+        }
         work_flops[kPhSyrk] = sf; work_bytes[kPhSyrk] = sb;
         // a sweep reads every factor entry once (sparse panels + the tail's
         // lower triangle) and the vector / update values it touches
@@ -1395,7 +1461,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dLive_.alloc(T_ > 0 ? T_ : 1);
     dDscale_.alloc(T_ > 0 ? T_ : 1);
     if (const char* e = std::getenv("IPO_HIP_PIVTOL")) pivot_tol_ = std::atof(e);
-    // flags: [0] ndep, [1] inconsistent, [2..2+T) node class sign per new index
+    // flags: [0] ndep, [1] fused panel bail-out, [2..2+T) node class sign per new index
     dFlags_.alloc(2 + T_);
     {
         std::vector<int> fl(2 + T_, 0);
@@ -1469,6 +1535,21 @@ TailView KktDevice::tail_view() const {
 }
 
 void KktDevice::factor(const double* dE, const double* dD) {
+    // fast path: fused diagonal-block + panel kernels; a pivot that fails
+    // the zero test makes them stop unwritten, and the factorisation is
+    // redone with the per-phase kernels, which own the dependent-pivot rule
+    if (!factor_pass(dE, dD, use_panel_)) {
+        tm_.panel_redos++;
+        factor_pass(dE, dD, false);
+    }
+    tm_.factors++;
+    ndep_ = xch_ ? static_cast<int>(hScal_[1]) : hFlags_[0];
+    if (-hScal_[0] < 1.0e-14) epsdiag_ *= 10;
+}
+
+// One numeric factorisation; returns false when fused kernels bailed out
+// (nothing of the result may then be used).
+bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
     hipStream_t s = stream_;
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev0_, s));
     const PlanView pv = IPO_VIEW();
@@ -1489,11 +1570,16 @@ void KktDevice::factor(const double* dE, const double* dD) {
         }
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         ph_begin(s);
-        launch_diag(pv, dlevel_sups_.get(), q0, q1 - q0, tv, 0, s);
-        ph_end(kPhDiag, 1, s);
-        ph_begin(s);
-        launch_trsm(pv, u0, u1 - u0, tv, 0, s);
-        ph_end(kPhTrsm, 1, s);
+        if (fused) {
+            launch_panel(pv, dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], fu_ptr_[l + 1] - fu_ptr_[l], tv, -1, s);
+            ph_end(kPhDiag, 1, s);
+        } else {
+            launch_diag(pv, dlevel_sups_.get(), q0, q1 - q0, tv, 0, s);
+            ph_end(kPhDiag, 1, s);
+            ph_begin(s);
+            launch_trsm(pv, u0, u1 - u0, tv, 0, s);
+            ph_end(kPhTrsm, 1, s);
+        }
     }
     if (plan_.nt > 0) {
         ph_begin(s);
@@ -1504,14 +1590,21 @@ void KktDevice::factor(const double* dE, const double* dD) {
         xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
         for (int kb = 0; kb < plan_.ntb; kb++) {
             const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
-            ph_begin(s);
-            launch_diag(pv, nullptr, 0, 1, tv, kb, s);
-            ph_end(kPhDiag, 1, s);
             const int below = plan_.nt - k0 - nc;
+            ph_begin(s);
+            if (fused) {
+                launch_panel(pv, nullptr, nullptr, 0, 0, tv, kb, s);
+                ph_end(kPhDiag, 1, s);
+            } else {
+                launch_diag(pv, nullptr, 0, 1, tv, kb, s);
+                ph_end(kPhDiag, 1, s);
+                if (below > 0) {
+                    ph_begin(s);
+                    launch_trsm(pv, 0, -1, tv, kb, s);
+                    ph_end(kPhTrsm, 1, s);
+                }
+            }
             if (below > 0) {
-                ph_begin(s);
-                launch_trsm(pv, 0, -1, tv, kb, s);
-                ph_end(kPhTrsm, 1, s);
                 const int nb = plan_.ntb - kb - 1;
                 ph_begin(s);
                 hipLaunchKernelGGL(k_tail_syrk, dim3(nb * (nb + 1) / 2), dim3(NT), 0, s, pv, tv, kb);
@@ -1520,14 +1613,16 @@ void KktDevice::factor(const double* dE, const double* dD) {
         }
     }
     IPO_HIP_CHECK(hipGetLastError());
-    // min |d| over the factor (ldlt.c:293-306) and the dependent-pivot count
+    // min |d| over the factor (ldlt.c:293-306), the dependent-pivot count
+    // and the fused kernels' bail-out flag
     hipLaunchKernelGGL(k_min_abs_partial, dim3(kRedBlocks), dim3(NT), 0, s, dDg_.get(), T_, dPart_.get());
     hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), 1, 1u, dScal_.get());
-    if (xch_) {   // every shard must take the same eps_diag / dependent-pivot decisions
+    if (xch_) {   // every shard must take the same eps_diag / dependent-pivot / redo decisions
         hipLaunchKernelGGL(k_flag_to_scalar, dim3(1), dim3(1), 0, s, dFlags_.get(), dScal_.get() + 1);
-        xsum(dScal_.get(), 2, RedOp::Max);
+        hipLaunchKernelGGL(k_flag_to_scalar, dim3(1), dim3(1), 0, s, dFlags_.get() + 1, dScal_.get() + 2);
+        xsum(dScal_.get(), 3, RedOp::Max);
     }
-    IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+    IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 3 * sizeof(double), hipMemcpyDeviceToHost, s));
     IPO_HIP_CHECK(hipMemcpyAsync(hFlags_, dFlags_.get(), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
     IPO_HIP_CHECK(hipStreamSynchronize(s));
@@ -1538,9 +1633,8 @@ void KktDevice::factor(const double* dE, const double* dD) {
         ph_collect();
         for (int ph : {kPhGather, kPhDiag, kPhTrsm, kPhSyrk}) tm_.phase_count[ph]++;
     }
-    tm_.factors++;
-    ndep_ = xch_ ? static_cast<int>(hScal_[1]) : hFlags_[0];
-    if (-hScal_[0] < 1.0e-14) epsdiag_ *= 10;
+    const bool bail = xch_ ? hScal_[2] > 0 : hFlags_[1] != 0;
+    return !(fused && bail);
 }
 
 // Gather launches of one level (tail < 0) or of the dense tail (group =

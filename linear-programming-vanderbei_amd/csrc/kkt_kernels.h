@@ -31,7 +31,7 @@ struct PlanView {
     double* Lx;
     double* dg;
     int* live;
-    int* flags;      // [0] dependent pivots, [1] inconsistent system
+    int* flags;      // [0] dependent pivots, [1] fused panel kernel bail-out
     const int* sign; // node class per new index: -1 y-node, +1 x-node
     double* dscale;  // sum of |terms| that formed each pivot (zero-pivot test)
     double tau;      // pivot d is "zero" when |d| <= tau * dscale
@@ -53,5 +53,11 @@ void launch_diag(const PlanView& pv, const int* level_sups, int q0, int count, c
 // L21 = A21 L11^-T D^-1 for factor units [u0, u0+count), or, with
 // count < 0, for the rows below block column kb of the dense tail.
 void launch_trsm(const PlanView& pv, int u0, int count, const TailView& tv, int kb, hipStream_t s);
+// Fused diagonal block + panel rows (the fast path of launch_diag +
+// launch_trsm): fused units [f0, f0+count) of a sparse level, or, with
+// fu_sup == nullptr, block column kb of the dense tail.  A pivot that fails
+// the zero test sets flags[1] and leaves the panel unwritten.
+void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,
+                  int kb, hipStream_t s);
 
 }  // namespace ipo
