@@ -334,8 +334,8 @@ constexpr int PNT = 512;
 __global__ void __launch_bounds__(PNT)
 k_panel(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j, int f0, TailView tv, int kb) {
     __shared__ double colk[2][PC];        // l(r, k) of half 0's rows
-    __shared__ double cold[2][PC];        // l(c, k) d_k
-    __shared__ double acol[2][PC];        // a(row, k) of half 1's rows
+    __shared__ double cold[3][PC];        // l(c, k) d_k
+    __shared__ double colk1[2][PC];       // l(row, k) of half 1's rows
     __shared__ int tinys[2];
     __shared__ double dv[PC];
     __shared__ double B[PC][PC + 1];
@@ -360,7 +360,9 @@ k_panel(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j
         panel = tv.S + k0 + (size_t)k0 * tv.nt;
         wbuf = tv.W;                      // rows relative to the block column, ld nt
     }
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q0 = wv & 3;
+    // wave index through readfirstlane: the compiler then knows it (and every
+    // branch on it) to be wave-uniform -- scalar branches instead of EXEC masks
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), q0 = wv & 3;
     const bool h1 = wv >= 4;
     const int h0 = min(PC, h);                      // half 0's rows
     const int row = h1 ? TR * (j + 1) + lane : lane;
@@ -374,52 +376,82 @@ k_panel(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j
         a[q] = ok ? t : 0.0;
     }
     double dsc = (!h1 && lane < nc && (lane & 3) == q0) ? p.dscale[c0 + lane] : 0.0;
+    // Software pipeline, one barrier per column k:
+    //  * half 0 publishes pivot k one iteration early: the wave owning
+    //    column k + 1 forms it right after its step-k update, in the same
+    //    straight-line code as the rest of that update (all waves compute it,
+    //    the owner publishes), so the division overlaps the update;
+    //  * half 1 lags one step: in iteration k it applies step k - 1 (with the
+    //    l(row, k - 1) its owner wave published) and the owner of column k
+    //    forms l(row, k) = a(row, k) / d_k for the next iteration.
+    // cold[] is read by half 0 in iteration k and by half 1 in k + 1 while
+    // pivot k + 2 is being written: three buffers.
     bool tiny = false;
+    if (!h1 && q0 == 0) {                 // pivot 0
+        const double dk = lane_bcast(a[0], 0);
+        const double dsk = lane_bcast(dsc, 0);
+        const bool tz = fabs(dk) <= p.tau * dsk;
+        const bool below = !tz && lane > 0 && lane < h0;
+        const double l = below ? a[0] / dk : 0.0;
+        if (below) a[0] = l;
+        colk[0][lane] = l;
+        cold[0][lane] = l * dk;
+        if (lane == 0) { tinys[0] = tz; dv[0] = dk; }
+    }
 #pragma unroll
     for (int qk = 0; qk < 16; qk++) {
         for (int pk = 0; pk < 4; pk++) {
             const int k = 4 * qk + pk;
             if (k >= nc || tiny) break;
-            const int buf = k & 1;
-            if (q0 == pk) {
-                if (!h1) {
-                    const double dk = lane_bcast(a[qk], k);
-                    const double dsk = lane_bcast(dsc, k);
-                    const bool tz = fabs(dk) <= p.tau * dsk;      // uniform in the wave
-                    const bool below = !tz && lane > k && lane < h0;
-                    const double l = below ? a[qk] / dk : 0.0;
-                    if (below) a[qk] = l;
-                    colk[buf][lane] = l;
-                    cold[buf][lane] = l * dk;
-                    if (lane == 0) { tinys[buf] = tz; dv[k] = dk; }
-                } else {
-                    acol[buf][lane] = a[qk];
-                }
-            }
             __syncthreads();
-            if (tinys[buf]) { tiny = true; break; }
-            // a(row, c) -= l(row, k) (l(c, k) d_k) for c > k.  Entries right of
-            // the diagonal (c > row) and columns >= nc are updated too: nothing
-            // reads or stores them.
-            double lr;
-            bool act;
+            const int b2 = k & 1, b3 = k % 3;
+            if (tinys[b2]) { tiny = true; break; }
+            const int kn = k + 1;
+            const bool own_next = kn < nc && q0 == (kn & 3);
             if (!h1) {
-                act = lane > k && lane < h0;
-                lr = act ? colk[buf][lane] : 0.0;
-            } else {
-                act = rok;
-                lr = act ? acol[buf][lane] / dv[k] : 0.0;
-                if (act && q0 == pk) a[qk] = lr;
-            }
-            if (act) {
+                // step k on rows > k.  Rows <= k read l = 0 and only touch
+                // entries right of their diagonal, which nothing reads.
+                const double lr = colk[b2][lane];
                 double ck[16];
 #pragma unroll
-                for (int q = qk; q < 16; q++) ck[q] = cold[buf][4 * q + q0];
-                if (q0 > pk) a[qk] = a[qk] - lr * ck[qk];     // column 4 qk + q0 > k
+                for (int q = qk; q < 16; q++) ck[q] = cold[b3][4 * q + q0];
+                a[qk] = q0 > pk ? a[qk] - lr * ck[qk] : a[qk];      // column 4 qk + q0 > k
 #pragma unroll
                 for (int q = qk + 1; q < 16; q++) a[q] = a[q] - lr * ck[q];
-                // |term| of the diagonal entry, kept by the owner of column lane
-                if (!h1 && (lane & 3) == q0) dsc = dsc + fabs(lr * cold[buf][lane]);
+                const double cr = cold[b3][lane];
+                dsc = (lane & 3) == q0 ? dsc + fabs(lr * cr) : dsc;   // |term| of the diagonal entry
+                // pivot k + 1 (column kn: register qk in wave pk + 1, or qk + 1 in wave 0)
+                const double an = pk < 3 ? a[qk] : a[qk < 15 ? qk + 1 : qk];
+                const int kl = kn < 64 ? kn : 63;
+                const double dk = lane_bcast(an, kl);
+                const double dsk = lane_bcast(dsc, kl);
+                const bool tz = fabs(dk) <= p.tau * dsk;
+                const bool below = !tz && lane > kn && lane < h0;
+                const double l = below ? an / dk : 0.0;
+                if (own_next) {
+                    if (pk < 3) a[qk] = below ? l : a[qk];
+                    else if (qk < 15) a[qk + 1] = below ? l : a[qk + 1];
+                    colk[b2 ^ 1][lane] = l;
+                    cold[kn % 3][lane] = l * dk;
+                    if (lane == 0) { tinys[b2 ^ 1] = tz; dv[kn] = dk; }
+                }
+            } else {
+                if (k > 0) {                  // step k - 1 on columns > k - 1
+                    const int bp = (k - 1) % 3;
+                    const double lr = colk1[b2 ^ 1][lane];
+                    double ck[16];
+#pragma unroll
+                    for (int q = qk; q < 16; q++) ck[q] = cold[bp][4 * q + q0];
+                    a[qk] = q0 >= pk ? a[qk] - lr * ck[qk] : a[qk];
+#pragma unroll
+                    for (int q = qk + 1; q < 16; q++) a[q] = a[q] - lr * ck[q];
+                }
+                // l(row, k) = a(row, k) / d_k by the owner of column k
+                const double l = rok ? a[qk] / dv[k] : 0.0;
+                if (q0 == pk) {
+                    a[qk] = l;
+                    colk1[b2][lane] = l;
+                }
             }
         }
     }

@@ -158,6 +158,17 @@ class KktDevice {
     DevBuf<int> dupd_src_, dupd_r0_, dupd_r1_, drel_, dlevel_sups_;
     DevBuf<int> dyrow_ptr_, dyrow_idx_;
     DevBuf<double> dYbuf_;
+    // sync-free top levels of the sweeps (k_fwd_sf / k_bwd_sf)
+    void build_sync_free_plan();
+    int sf_level_ = 0;                    // first level of the range (nlevels: none)
+    int nsf_f_ = 0, nsf_b_ = 0, sf_grid_ = 1;
+    int sf_fwd_epoch_ = 0, sf_bwd_epoch_ = 0;
+    size_t zpad_stride_ = 1;
+    std::vector<int> h_chunk0_;           // per supernode: first solve chunk (-1: not chunked)
+    DevBuf<int2> dsf_items_f_, dsf_items_b_;
+    DevBuf<int> dsf_need_, dsf_par_, dsf_zbase_, dsf_zpi_, dsf_fcnt_, dsf_fflag_, dsf_bcnt_, dsf_bflag_;
+    DevBuf<int> dybase_;                  // per supernode: first ybuf slot of its update values
+    DevBuf<double> dZpad_;                // padded z slices of the range, 2 right-hand sides
     std::vector<int> fu_ptr_;             // per level: fused panel units [fu_ptr_[l], fu_ptr_[l+1])
     DevBuf<int> dfu_sup_, dfu_j_;         // fused panel unit -> supernode, tile pair index
     bool use_panel_ = true;               // fused diagonal-block + panel kernels (IPO_HIP_PANEL=0: off)

@@ -39,6 +39,22 @@ constexpr int TR = kTileRows;     // 64
 constexpr int PC = kPanelCols;    // 64
 constexpr int NT = 256;           // threads per workgroup
 
+// sc1 (agent-scope relaxed atomic) accesses: they bypass the CU's L1, the
+// hand-off form of MI355X_MICROARCH.md for data one workgroup passes to
+// another inside a launch
+__device__ __forceinline__ void sc1_store(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double sc1_load(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a handed-off value (SC) or a plain one
+template <bool SC>
+__device__ __forceinline__ double ld_h(const double* p) {
+    if constexpr (SC) return sc1_load(p);
+    else return *p;
+}
+
 
 
 // ---------------------------------------------------------------- assembly
@@ -570,7 +586,7 @@ struct SweepVecs {
 // Forward, diagonal part of supernode s: subtract the y values of solved
 // descendants from its rows, solve L11.  Leaves z_s in zl[r] and in z.
 // 4 threads per row; partial sums combined as (p0 + p1) + (p2 + p3).
-template <int R>
+template <int R, bool SC = false>
 __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
                          const SweepVecs& V, const double (&eps)[R], double (*zl)[PC], double (*Ls)[PC + 1], int* lv) {
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
@@ -593,7 +609,8 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
 #pragma unroll
                 for (int r = 0; r < R; r++) {
                     const double* yb = V.y + r * V.ys;
-                    const double y0 = yb[i0], y1 = yb[i1], y2 = yb[i2], y3 = yb[i3];
+                    const double y0 = ld_h<SC>(yb + i0), y1 = ld_h<SC>(yb + i1), y2 = ld_h<SC>(yb + i2),
+                                 y3 = ld_h<SC>(yb + i3);
                     acc[r] += y0;
                     acc[r] += y1;
                     acc[r] += y2;
@@ -603,7 +620,7 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
             for (; e < e1; e += 4) {
                 const int i0 = yrow_idx[e];
 #pragma unroll
-                for (int r = 0; r < R; r++) acc[r] += V.y[r * V.ys + i0];
+                for (int r = 0; r < R; r++) acc[r] += ld_h<SC>(V.y + r * V.ys + i0);
             }
         }
 #pragma unroll
@@ -660,7 +677,7 @@ k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __r
             for (int r = 0; r < R; r++) acc[r] += l * zl[r][k];
         }
 #pragma unroll
-        for (int r = 0; r < R; r++) V.y[r * V.ys + p.rowptr[s] + i] = acc[r];
+        for (int r = 0; r < R; r++) V.y[r * V.ys + p.ybase[s] + i] = acc[r];
     }
 }
 
@@ -716,7 +733,7 @@ k_fwd_gemv(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict_
     if (wv == 0 && i < hb) {
 #pragma unroll
         for (int r = 0; r < R; r++)
-            V.y[r * V.ys + p.rowptr[s] + i] = ((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane];
+            V.y[r * V.ys + p.ybase[s] + i] = ((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane];
     }
 }
 
@@ -1001,12 +1018,6 @@ k_tail_bwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double
 constexpr int kChainMaxBlocks = 200;
 constexpr size_t kChainLds = 96 * 1024;
 
-__device__ __forceinline__ void sc1_store(double* p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double sc1_load(const double* p) {
-    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ void chain_wait(const int* flags, int j, int epoch) {
     if (threadIdx.x == 0)
         while (__hip_atomic_load(const_cast<int*>(flags + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch)
@@ -1153,6 +1164,248 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
         flag_bad<R>(p, bad);
     }
     chain_publish(flags, i, epoch);
+}
+
+// ------------------------------------------- sync-free sweeps, top levels
+// The narrow top of the elimination tree (levels >= sf_level_, a few
+// supernodes each) in one persistent launch per direction instead of one or
+// two launches per level.  One workgroup per CU (dynamic LDS); workgroup w
+// takes the work items w, w + G, ... in list order, and an item only waits
+// on items earlier in the list (descendants forward, ancestors backward), so
+// the grid always drains.  Items: (s, -1) a whole supernode, (s, -2) the
+// diagonal part (forward) / the finish (backward) of a chunked supernode,
+// (s, c >= 0) its 64-row chunk c.  Hand-offs follow MI355X_MICROARCH.md
+// (inter-workgroup visibility, table row 1): the producer writes the values
+// with sc1 stores, waits vmcnt(0), joins a barrier, and one lane adds to
+// the consumer's counter or stores a flag (agent scope); the consumer polls
+// from one lane, joins a barrier and reads the values with sc1 loads.  Each
+// handed-off value sits in 128-B lines of its own producer (padded ybuf
+// slices, the zpad mirror, per-chunk partials), written once per sweep, so
+// no consumer can have cached a line before its producer wrote it.  The
+// arithmetic per supernode is that of the per-level kernels (bitwise).
+struct SfView {
+    const int2* items;
+    int nitems;
+    int* cnt;           // per supernode: arrivals (forward: child y producers; backward: chunks)
+    int* flag;          // per supernode: epoch of its completed diagonal part (fwd) / finish (bwd)
+    const int* need;    // per supernode: forward arrivals per sweep
+    const int* parent;  // per supernode: parent inside the range, else -1
+    const int* zbase;   // per supernode: its padded z slice
+    const int* zpi;     // per column: padded z position, -1 outside the range
+    double* zpad;       // padded z slices of R right-hand sides
+    size_t zps;
+    int epoch;
+};
+
+__device__ __forceinline__ void sf_arrive(int* c) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
+         const int* __restrict__ chunk_r0, SweepVecs V, const double* __restrict__ epsp) {
+    extern __shared__ double lds_pad[];
+    __shared__ double zl[R][PC];
+    __shared__ double Ls[PC][PC + 1];
+    __shared__ int lv[PC];
+    __shared__ double red[R][4][64];
+    double eps[R];
+    load_eps<R>(epsp, eps);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) lds_pad[0] = 0.0;
+    for (int it = blockIdx.x; it < sf.nitems; it += gridDim.x) {
+        const int2 w = sf.items[it];
+        const int s = w.x, code = w.y;
+        const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+        const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
+        const int par = sf.parent[s];
+        const double* panel = p.Lx + p.off[s];
+        if (code < 0) {
+            chain_wait(sf.cnt, s, sf.epoch * sf.need[s]);
+            fwd_diag<R, true>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv);
+            if (code == -1) {       // y_s = L21 z_s, one row per thread (k_forward)
+                for (int i = tid; i < hb; i += NT) {
+                    const double* __restrict__ row = panel + nc + i;
+                    double acc[R];
+#pragma unroll
+                    for (int r = 0; r < R; r++) acc[r] = 0.0;
+#pragma unroll 8
+                    for (int k = 0; k < nc; k++) {
+                        const double l = row[(size_t)k * h];
+#pragma unroll
+                        for (int r = 0; r < R; r++) acc[r] += l * zl[r][k];
+                    }
+#pragma unroll
+                    for (int r = 0; r < R; r++) sc1_store(V.y + r * V.ys + p.ybase[s] + i, acc[r]);
+                }
+                if (par >= 0) sf_arrive(sf.cnt + par);
+                else __syncthreads();
+            } else {                // z_s for the chunk items
+                if (tid < nc) {
+#pragma unroll
+                    for (int r = 0; r < R; r++) sc1_store(sf.zpad + r * sf.zps + sf.zbase[s] + tid, zl[r][tid]);
+                }
+                chain_publish(sf.flag, s, sf.epoch);
+            }
+        } else {                    // y over one 64-row chunk (k_fwd_gemv)
+            chain_wait(sf.flag, s, sf.epoch);
+            if (tid < nc) {
+#pragma unroll
+                for (int r = 0; r < R; r++) zl[r][tid] = sc1_load(sf.zpad + r * sf.zps + sf.zbase[s] + tid);
+            }
+            __syncthreads();
+            const int i = chunk_r0[code] + lane, kq = wv * 16, nq = min(16, nc - kq);
+            double acc[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) acc[r] = 0.0;
+            if (i < hb && nq > 0) {
+                const double* __restrict__ row = panel + nc + i + (size_t)kq * h;
+                double t[16];
+#pragma unroll
+                for (int q = 0; q < 16; q++) t[q] = row[(size_t)min(q, nq - 1) * h];
+#pragma unroll
+                for (int q = 0; q < 16; q++)
+                    if (q < nq) {
+#pragma unroll
+                        for (int r = 0; r < R; r++) acc[r] += t[q] * zl[r][kq + q];
+                    }
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++) red[r][wv][lane] = acc[r];
+            __syncthreads();
+            if (wv == 0 && i < hb) {
+#pragma unroll
+                for (int r = 0; r < R; r++)
+                    sc1_store(V.y + r * V.ys + p.ybase[s] + i,
+                              ((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane]);
+            }
+            if (par >= 0) sf_arrive(sf.cnt + par);
+            else __syncthreads();
+        }
+    }
+}
+
+// z of row ri for the backward sweep: the padded mirror inside the range
+template <int R>
+__device__ __forceinline__ void sf_zrow(const SfView& sf, const SweepVecs& V, int ri, double (&zi)[R]) {
+    const int pi = sf.zpi[ri];
+#pragma unroll
+    for (int r = 0; r < R; r++) zi[r] = pi >= 0 ? sc1_load(sf.zpad + r * sf.zps + pi) : V.z[r * V.zs + ri];
+}
+
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __restrict__ sup_chunk0,
+         double* __restrict__ part, size_t ps, SweepVecs V, const double* __restrict__ epsp) {
+    extern __shared__ double lds_pad[];
+    __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L(j, r)
+    __shared__ int lv[PC];
+    __shared__ double xs[R][4][PC];
+    double eps[R];
+    load_eps<R>(epsp, eps);
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) lds_pad[0] = 0.0;
+    for (int it = blockIdx.x; it < sf.nitems; it += gridDim.x) {
+        const int2 w = sf.items[it];
+        const int s = w.x, code = w.y;
+        const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+        const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
+        const int par = sf.parent[s];
+        const double* panel = p.Lx + p.off[s];
+        const int* __restrict__ rows = p.rows + p.rowptr[s];
+        const int kq = wv * 16, nq = min(16, nc - kq);
+        if (code >= 0) {            // partial sums of one 64-row chunk (k_bwd_partial)
+            if (par >= 0) chain_wait(sf.flag, par, sf.epoch);
+            if (nq > 0) {
+                const int i = chunk_r0[code] + lane;
+                const bool okr = i < hb;
+                const int ic = okr ? i : 0;
+                double zi[R];
+                sf_zrow<R>(sf, V, rows[ic], zi);
+                const double* __restrict__ col = panel + nc + ic + (size_t)kq * h;
+                double t[16];
+#pragma unroll
+                for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, nq - 1) * h];
+#pragma unroll
+                for (int r = 0; r < R; r++)
+#pragma unroll
+                    for (int q = 0; q < 16; q++) {
+                        const double v = wave_sum((okr && q < nq) ? t[q] * zi[r] : 0.0);
+                        if (lane == 0 && q < nq) sc1_store(part + r * ps + (size_t)code * PC + kq + q, v);
+                    }
+            }
+            sf_arrive(sf.cnt + s);
+            continue;
+        }
+        if (code == -2) chain_wait(sf.cnt, s, sf.epoch * ((hb + 63) / 64));
+        else if (par >= 0) chain_wait(sf.flag, par, sf.epoch);
+        stage_l11(panel, h, nc, Ls);
+        if (tid < nc) lv[tid] = p.live[c0 + tid];
+        if (code == -2) {           // chunk partials in the order of k_bwd_finish
+            const int cf = sup_chunk0[s], nch = (hb + 63) / 64;
+            double x[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) x[r] = 0.0;
+            if (lane < nc)
+                for (int c = wv; c < nch; c += 4) {
+#pragma unroll
+                    for (int r = 0; r < R; r++) x[r] += sc1_load(part + r * ps + (size_t)(cf + c) * PC + lane);
+                }
+#pragma unroll
+            for (int r = 0; r < R; r++) xs[r][wv][lane] = x[r];
+        } else if (nq > 0) {        // L21' z_R over all rows (k_backward)
+            double acc[R][16];
+#pragma unroll
+            for (int r = 0; r < R; r++)
+#pragma unroll
+                for (int q = 0; q < 16; q++) acc[r][q] = 0.0;
+            for (int i = lane; i < hb; i += 64) {
+                double zi[R];
+                sf_zrow<R>(sf, V, rows[i], zi);
+                const double* __restrict__ col = panel + nc + i + (size_t)kq * h;
+                double t[16];
+#pragma unroll
+                for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, nq - 1) * h];
+#pragma unroll
+                for (int q = 0; q < 16; q++)
+                    if (q < nq) {
+#pragma unroll
+                        for (int r = 0; r < R; r++) acc[r][q] += t[q] * zi[r];
+                    }
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++)
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    const double t = wave_sum(acc[r][q]);
+                    if (lane == 0 && q < nq) xs[r][0][kq + q] = t;
+                }
+        }
+        __syncthreads();
+        if (wv == 0) {
+            int bad[R] = {};
+            double zr[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const double sub = code == -2 ? ((xs[r][0][lane] + xs[r][1][lane]) + xs[r][2][lane]) + xs[r][3][lane]
+                                              : xs[r][0][lane];
+                zr[r] = lane < nc ? dscale_rule(p, c0 + lane, V.z[r * V.zs + c0 + lane], eps[r], bad[r]) - sub : 0.0;
+            }
+            tri_upper<R>(zr, Ls, lv, nc, eps, bad);
+            if (lane < nc) {
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    V.z[r * V.zs + c0 + lane] = zr[r];
+                    sc1_store(sf.zpad + r * sf.zps + sf.zbase[s] + lane, zr[r]);
+                }
+            }
+            flag_bad<R>(p, bad);
+        }
+        chain_publish(sf.flag, s, sf.epoch);
+    }
 }
 
 // -------------------------------------------------------- refinement glue
@@ -1309,11 +1562,10 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         partial_stride_ = csup.empty() ? 1 : csup.size() * kPanelCols;
         dPartial_.alloc(2 * partial_stride_);
         IPO_HIP_CHECK(hipStreamSynchronize(s));   // csup / cr0 / chunk0 are stack vectors
+        h_chunk0_ = chunk0;
     }
     dyrow_ptr_.upload(plan_.yrow_ptr, s);
-    dyrow_idx_.upload(plan_.yrow_idx, s);
-    ybuf_stride_ = plan_.rowptr.back() > 0 ? static_cast<size_t>(plan_.rowptr.back()) : 1;
-    dYbuf_.alloc(2 * ybuf_stride_);
+    build_sync_free_plan();
     dkslot_.upload(plan_.kslot, s);
     dkslot_ptr_.upload(plan_.kslot_ptr, s);
     {   // gather chunks (split K): groups = sparse levels, then the dense tail
@@ -1361,8 +1613,8 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         IPO_HIP_CHECK(hipStreamSynchronize(s));
     }
     {   // launches per sweep and algorithmic work per phase occurrence
-        fwd_launches_ = bwd_launches_ = 0;
-        for (int l = 0; l < plan_.nlevels; l++) {
+        fwd_launches_ = bwd_launches_ = sf_level_ < plan_.nlevels ? 1 : 0;
+        for (int l = 0; l < sf_level_; l++) {
             const int k = chunk_ptr_[l + 1] > chunk_ptr_[l] ? 2 : 1;
             fwd_launches_ += k;
             bwd_launches_ += k;
@@ -1485,6 +1737,89 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     IPO_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+// Sync-free top levels (k_fwd_sf / k_bwd_sf): from sf_level_ up every level
+// is at most kSfWidth supernodes wide.  Their forward update values get
+// ybuf slices, and their z values zpad slices, of their own 128-B lines;
+// work items, per-supernode arrival counts and parents.  Called from the
+// constructor after the solve chunks are built.
+void KktDevice::build_sync_free_plan() {
+    constexpr int kSfWidth = 64;
+    hipStream_t s = stream_;
+    const KktPlan& P = plan_;
+    const int ns = P.nsup;
+    sf_level_ = P.nlevels;
+    while (sf_level_ > 0 && P.level_ptr[sf_level_] - P.level_ptr[sf_level_ - 1] <= kSfWidth) sf_level_--;
+    if (P.nlevels - sf_level_ < 2) sf_level_ = P.nlevels;
+    if (const char* e = std::getenv("IPO_HIP_SF"))
+        if (std::atoi(e) == 0) sf_level_ = P.nlevels;
+    auto chunked = [&](int sp) { const int l = P.level[sp]; return chunk_ptr_[l + 1] > chunk_ptr_[l]; };
+    auto nchunks = [&](int sp) { return (P.rowptr[sp + 1] - P.rowptr[sp] + 63) / 64; };
+    std::vector<int> ybase(ns + 1), zbase(ns, -1), zpi(T_ > 0 ? T_ : 1, -1), need(ns, 0), par(ns, -1);
+    size_t yend = P.rowptr.empty() ? 0 : P.rowptr.back(), zend = 0;
+    for (int sp = 0; sp < ns; sp++) {
+        if (P.level[sp] < sf_level_) { ybase[sp] = P.rowptr[sp]; continue; }
+        yend = (yend + 15) & ~size_t(15);
+        ybase[sp] = static_cast<int>(yend);
+        yend += P.rowptr[sp + 1] - P.rowptr[sp];
+        zend = (zend + 15) & ~size_t(15);
+        zbase[sp] = static_cast<int>(zend);
+        for (int c = P.col0[sp]; c < P.col0[sp + 1]; c++) zpi[c] = static_cast<int>(zend + c - P.col0[sp]);
+        zend += P.col0[sp + 1] - P.col0[sp];
+        const int pa = P.parent[sp];
+        if (pa >= 0) { par[sp] = pa; need[pa] += chunked(sp) ? nchunks(sp) : 1; }
+    }
+    ybase[ns] = static_cast<int>(yend);
+    std::vector<int> yidx(P.yrow_idx);
+    if (sf_level_ < P.nlevels) {       // update-value positions of the moved slices
+        std::vector<int> pos(yidx.empty() ? 1 : P.rowptr.back());
+        for (int sp = 0; sp < ns; sp++)
+            for (int i = P.rowptr[sp]; i < P.rowptr[sp + 1]; i++) pos[i] = ybase[sp] + (i - P.rowptr[sp]);
+        for (int& e : yidx) e = pos[e];
+    }
+    dyrow_idx_.upload(yidx, s);
+    dybase_.upload(ybase, s);
+    ybuf_stride_ = std::max<size_t>(yend, 1);
+    dYbuf_.alloc(2 * ybuf_stride_);
+    std::vector<int2> fi, bi;
+    for (int l = sf_level_; l < P.nlevels; l++)
+        for (int q = P.level_ptr[l]; q < P.level_ptr[l + 1]; q++) {
+            const int sp = P.level_sups[q];
+            if (!chunked(sp)) { fi.push_back(make_int2(sp, -1)); continue; }
+            fi.push_back(make_int2(sp, -2));
+            for (int c = 0; c < nchunks(sp); c++) fi.push_back(make_int2(sp, h_chunk0_[sp] + c));
+        }
+    for (int l = P.nlevels - 1; l >= sf_level_; l--)
+        for (int q = P.level_ptr[l]; q < P.level_ptr[l + 1]; q++) {
+            const int sp = P.level_sups[q];
+            if (!chunked(sp)) { bi.push_back(make_int2(sp, -1)); continue; }
+            for (int c = 0; c < nchunks(sp); c++) bi.push_back(make_int2(sp, h_chunk0_[sp] + c));
+            bi.push_back(make_int2(sp, -2));
+        }
+    nsf_f_ = static_cast<int>(fi.size());
+    nsf_b_ = static_cast<int>(bi.size());
+    if (sf_level_ < P.nlevels) {
+        dsf_items_f_.upload(fi, s);
+        dsf_items_b_.upload(bi, s);
+        dsf_need_.upload(need, s);
+        dsf_par_.upload(par, s);
+        dsf_zbase_.upload(zbase, s);
+        dsf_zpi_.upload(zpi, s);
+        zpad_stride_ = std::max<size_t>(zend, 1);
+        dZpad_.alloc(2 * zpad_stride_);
+        for (DevBuf<int>* b : {&dsf_fcnt_, &dsf_fflag_, &dsf_bcnt_, &dsf_bflag_}) {
+            b->alloc(ns);
+            IPO_HIP_CHECK(hipMemsetAsync(b->get(), 0, ns * sizeof(int), s));
+        }
+        int dev = 0;
+        IPO_HIP_CHECK(hipGetDevice(&dev));
+        IPO_HIP_CHECK(hipDeviceGetAttribute(&sf_grid_, hipDeviceAttributeMultiprocessorCount, dev));
+        for (const void* f : {reinterpret_cast<const void*>(&k_fwd_sf<1>), reinterpret_cast<const void*>(&k_fwd_sf<2>),
+                              reinterpret_cast<const void*>(&k_bwd_sf<1>), reinterpret_cast<const void*>(&k_bwd_sf<2>)})
+            IPO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
+    }
+    IPO_HIP_CHECK(hipStreamSynchronize(s));   // the host vectors above are locals
+}
+
 KktDevice::~KktDevice() {
     if (hScal_) (void)hipHostFree(hScal_);
     if (hFlags_) (void)hipHostFree(hFlags_);
@@ -1513,12 +1848,14 @@ static PlanView make_view(const KktPlan&, const DevBuf<int>& col0, const DevBuf<
 
 #define IPO_VIEW() with_scale(make_view(plan_, dcol0_, drowptr_, drows_, doff_, dunit_sup_, dunit_tile_, dtask_ptr_, \
                              dtask_pair_, dtask_i0_, dtask_i1_, dupd_src_, dupd_r0_, dupd_r1_, drelptr_, drel_, \
-                             dLx_, dDg_, dLive_, dFlags_), dDscale_.get(), pivot_tol_, dIncons_.get())
+                             dLx_, dDg_, dLive_, dFlags_), dDscale_.get(), pivot_tol_, dIncons_.get(), \
+                             dybase_.get())
 
-static PlanView with_scale(PlanView v, double* dscale, double tau, int* incons) {
+static PlanView with_scale(PlanView v, double* dscale, double tau, int* incons, const int* ybase) {
     v.dscale = dscale;
     v.tau = tau;
     v.incons = incons;
+    v.ybase = ybase;
     return v;
 }
 
@@ -1697,7 +2034,7 @@ void KktDevice::sweep(double* dz, const double* epsp) {
     const size_t ps = partial_stride_;
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev2_, s));
     ph_begin(s);
-    for (int l = 0; l < plan_.nlevels; l++) {
+    for (int l = 0; l < sf_level_; l++) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         const int cb = chunk_ptr_[l], ce = chunk_ptr_[l + 1];
         if (ce > cb) {
@@ -1709,6 +2046,12 @@ void KktDevice::sweep(double* dz, const double* epsp) {
             hipLaunchKernelGGL(k_forward<R>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
                                dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
         }
+    }
+    if (sf_level_ < plan_.nlevels) {      // the narrow top levels in one launch
+        const SfView sf{dsf_items_f_.get(), nsf_f_, dsf_fcnt_.get(), dsf_fflag_.get(), dsf_need_.get(), dsf_par_.get(),
+                        dsf_zbase_.get(), dsf_zpi_.get(), dZpad_.get(), zpad_stride_, ++sf_fwd_epoch_};
+        hipLaunchKernelGGL(k_fwd_sf<R>, dim3(std::min(sf_grid_, nsf_f_)), dim3(NT), kChainLds, s, pv, sf,
+                           dyrow_ptr_.get(), dyrow_idx_.get(), dchunk_r0_.get(), V, epsp);
     }
     if (plan_.nt > 0) {
         const TailView tv = tail_view();
@@ -1726,7 +2069,13 @@ void KktDevice::sweep(double* dz, const double* epsp) {
         hipLaunchKernelGGL(k_tail_bwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
                            dChainFlags_.get(), ++chain_epoch_);
     }
-    for (int l = plan_.nlevels - 1; l >= 0; l--) {
+    if (sf_level_ < plan_.nlevels) {
+        const SfView sf{dsf_items_b_.get(), nsf_b_, dsf_bcnt_.get(), dsf_bflag_.get(), dsf_need_.get(), dsf_par_.get(),
+                        dsf_zbase_.get(), dsf_zpi_.get(), dZpad_.get(), zpad_stride_, ++sf_bwd_epoch_};
+        hipLaunchKernelGGL(k_bwd_sf<R>, dim3(std::min(sf_grid_, nsf_b_)), dim3(NT), kChainLds, s, pv, sf,
+                           dchunk_r0_.get(), dsup_chunk0_.get(), dPartial_.get(), ps, V, epsp);
+    }
+    for (int l = sf_level_ - 1; l >= 0; l--) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         const int cb = chunk_ptr_[l], ce = chunk_ptr_[l + 1];
         if (ce > cb) {

@@ -36,6 +36,7 @@ struct PlanView {
     double* dscale;  // sum of |terms| that formed each pivot (zero-pivot test)
     double tau;      // pivot d is "zero" when |d| <= tau * dscale
     int* incons;     // [r]: right-hand side r met a dropped column with |z| > eps (ldlt.c:462)
+    const int* ybase; // per supernode: first ybuf slot of its forward update values
 };
 
 // value of v in lane j (j wave-uniform), via two v_readlane_b32
