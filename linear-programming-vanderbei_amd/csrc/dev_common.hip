@@ -35,46 +35,72 @@ k_finish_reduce(const double* __restrict__ part, int nq, unsigned maxmask, doubl
 }
 
 // dotprod() of linalg.c:17-25 in its own order: one running sum, i = 0..n-1.
-// One block per job; the products are independent (prefetched), only the
-// adds form the sequential chain.  Max-type jobs are order-free.
-__global__ void __launch_bounds__(64)
+// One 256-thread block per job: the products of a chunk are formed by the
+// whole block into LDS (eight loads in flight per thread), then one lane
+// adds them in index order with its LDS reads one 16-value batch ahead of
+// the adds, so that only the dependent adds remain on the chain.  Max-type
+// jobs are order-free.
+constexpr int kOrdThreads = 256;
+
+__global__ void __launch_bounds__(kOrdThreads)
 k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
     const int j = blockIdx.x;
     const double* a = jobs.a[j];
     const double* b = jobs.b[j];
     const int len = jobs.len[j];
     const int op = jobs.op[j];
+    const int tid = threadIdx.x;
     if (op != 0) {
-        __shared__ double sh[1];
+        __shared__ double sh[4];
         double acc = 0.0;
-        for (int i = threadIdx.x; i < len; i += 64) {
+        for (int i = tid; i < len; i += kOrdThreads) {
             if (op == 1) acc = fmax(acc, ref_abs(a[i]));
             else acc = fmax(acc, -a[i] / b[i]);
         }
-        acc = wave_max(acc);
-        if (threadIdx.x == 0) { sh[0] = acc; out[j] = acc; }
+        acc = block_max(acc, sh);
+        if (tid == 0) out[j] = acc;
         return;
     }
-    // products in parallel into LDS, then one lane adds them in index order
-    constexpr int CH = 4096;
-    __shared__ double prod[CH];
+    constexpr int CH = 8192;
+    __shared__ __attribute__((aligned(16))) double prod[CH + 16];   // + one batch of read-ahead
     double s = 0.0e0;
     for (int base = 0; base < len; base += CH) {
         const int cnt = min(CH, len - base);
         __syncthreads();
-        for (int i = threadIdx.x; i < cnt; i += 64) prod[i] = a[base + i] * b[base + i];
+        for (int i0 = 0; i0 < cnt; i0 += 8 * kOrdThreads) {
+            double pa[8], pb[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = i0 + u * kOrdThreads + tid;
+                pa[u] = i < cnt ? a[base + i] : 0.0;
+                pb[u] = i < cnt ? b[base + i] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = i0 + u * kOrdThreads + tid;
+                if (i < cnt) prod[i] = pa[u] * pb[u];
+            }
+        }
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
+            const double2* pp = reinterpret_cast<const double2*>(prod);
+            double2 cur[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) cur[u] = pp[u];
             int i = 0;
-            for (; i + 8 <= cnt; i += 8) {
-                const double p0 = prod[i], p1 = prod[i + 1], p2 = prod[i + 2], p3 = prod[i + 3];
-                const double p4 = prod[i + 4], p5 = prod[i + 5], p6 = prod[i + 6], p7 = prod[i + 7];
-                s += p0; s += p1; s += p2; s += p3; s += p4; s += p5; s += p6; s += p7;
+            for (; i + 16 <= cnt; i += 16) {
+                double2 nxt[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) nxt[u] = pp[(i + 16) / 2 + u];
+#pragma unroll
+                for (int u = 0; u < 8; u++) { s += cur[u].x; s += cur[u].y; }
+#pragma unroll
+                for (int u = 0; u < 8; u++) cur[u] = nxt[u];
             }
             for (; i < cnt; i++) s += prod[i];
         }
     }
-    if (threadIdx.x == 0) out[j] = s;
+    if (tid == 0) out[j] = s;
 }
 
 __global__ void __launch_bounds__(256)
@@ -99,7 +125,7 @@ bool g_ordered_reductions = true;
 
 void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st) {
     if (g_ordered_reductions) {
-        hipLaunchKernelGGL(k_reduce_ordered, dim3(jobs.nj), dim3(64), 0, st, jobs, out);
+        hipLaunchKernelGGL(k_reduce_ordered, dim3(jobs.nj), dim3(kOrdThreads), 0, st, jobs, out);
         IPO_HIP_CHECK(hipGetLastError());
         return;
     }

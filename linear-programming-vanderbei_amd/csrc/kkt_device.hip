@@ -586,24 +586,41 @@ struct SweepVecs {
 // Forward, diagonal part of supernode s: subtract the y values of solved
 // descendants from its rows, solve L11.  Leaves z_s in zl[r] and in z.
 // 4 threads per row; partial sums combined as (p0 + p1) + (p2 + p3).
-template <int R, bool SC = false>
+template <int R, bool SC = false, bool STAGED = false>
 __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
                          const SweepVecs& V, const double (&eps)[R], double (*zl)[PC], double (*Ls)[PC + 1], int* lv) {
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    stage_l11(p.Lx + p.off[s], h, nc, Ls);
-    if (tid < nc) lv[tid] = p.live[c0 + tid];
+    if (!STAGED) {              // else the caller staged L11 and the marks already
+        stage_l11(p.Lx + p.off[s], h, nc, Ls);
+        if (tid < nc) lv[tid] = p.live[c0 + tid];
+    }
     for (int base = 0; base < nc; base += blockDim.x >> 2) {
         const int k = base + (tid >> 2), part = tid & 3;
         double acc[R];
 #pragma unroll
         for (int r = 0; r < R; r++) acc[r] = 0.0;
         if (k < nc) {
-            // four entries in flight per thread: index loads first, then values
+            // eight, then four entries in flight per thread: index loads
+            // first, then values; one running sum per part in list order
             const int v = c0 + k;
             const int e1 = yrow_ptr[v + 1];
             int e = yrow_ptr[v] + part;
+            for (; e + 28 < e1; e += 32) {
+                int ix[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) ix[u] = yrow_idx[e + 4 * u];
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    const double* yb = V.y + r * V.ys;
+                    double yv[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) yv[u] = ld_h<SC>(yb + ix[u]);
+#pragma unroll
+                    for (int u = 0; u < 8; u++) acc[r] += yv[u];
+                }
+            }
             for (; e + 12 < e1; e += 16) {
                 const int i0 = yrow_idx[e], i1 = yrow_idx[e + 4], i2 = yrow_idx[e + 8], i3 = yrow_idx[e + 12];
 #pragma unroll
@@ -1224,8 +1241,10 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
         const int par = sf.parent[s];
         const double* panel = p.Lx + p.off[s];
         if (code < 0) {
+            stage_l11(panel, h, nc, Ls);      // the factor does not depend on the hand-off
+            if (tid < nc) lv[tid] = p.live[c0 + tid];
             chain_wait(sf.cnt, s, sf.epoch * sf.need[s]);
-            fwd_diag<R, true>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv);
+            fwd_diag<R, true, true>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv);
             if (code == -1) {       // y_s = L21 z_s, one row per thread (k_forward)
                 for (int i = tid; i < hb; i += NT) {
                     const double* __restrict__ row = panel + nc + i;
@@ -1318,17 +1337,18 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
         const int* __restrict__ rows = p.rows + p.rowptr[s];
         const int kq = wv * 16, nq = min(16, nc - kq);
         if (code >= 0) {            // partial sums of one 64-row chunk (k_bwd_partial)
+            const int i = chunk_r0[code] + lane;
+            const bool okr = i < hb;
+            const int ic = okr ? i : 0;
+            const int ri = rows[ic];
+            double t[16];             // the factor tile is loaded before the wait
+            const double* __restrict__ col = panel + nc + ic + (size_t)(nq > 0 ? kq : 0) * h;
+#pragma unroll
+            for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, max(nq, 1) - 1) * h];
             if (par >= 0) chain_wait(sf.flag, par, sf.epoch);
             if (nq > 0) {
-                const int i = chunk_r0[code] + lane;
-                const bool okr = i < hb;
-                const int ic = okr ? i : 0;
                 double zi[R];
-                sf_zrow<R>(sf, V, rows[ic], zi);
-                const double* __restrict__ col = panel + nc + ic + (size_t)kq * h;
-                double t[16];
-#pragma unroll
-                for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, nq - 1) * h];
+                sf_zrow<R>(sf, V, ri, zi);
 #pragma unroll
                 for (int r = 0; r < R; r++)
 #pragma unroll
@@ -1340,10 +1360,10 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             sf_arrive(sf.cnt + s);
             continue;
         }
+        stage_l11(panel, h, nc, Ls);          // the factor does not depend on the hand-off
+        if (tid < nc) lv[tid] = p.live[c0 + tid];
         if (code == -2) chain_wait(sf.cnt, s, sf.epoch * ((hb + 63) / 64));
         else if (par >= 0) chain_wait(sf.flag, par, sf.epoch);
-        stage_l11(panel, h, nc, Ls);
-        if (tid < nc) lv[tid] = p.live[c0 + tid];
         if (code == -2) {           // chunk partials in the order of k_bwd_finish
             const int cf = sup_chunk0[s], nch = (hb + 63) / 64;
             double x[R];
