@@ -53,6 +53,11 @@ def per_kernel(db, counter):
     return acc
 
 
+def base(k):
+    """kernel name without 'void ' and template arguments (the PHASE_KERNELS names)"""
+    return re.sub(r"<.*>", "", k.replace("void ", "")).strip()
+
+
 fetch = per_kernel(os.path.join(src, f"{tag}_pmc_fetch", "run_results.db"), "FETCH_SIZE")
 write = per_kernel(os.path.join(src, f"{tag}_pmc_write", "run_results.db"), "WRITE_SIZE")
 kern = {}
@@ -65,7 +70,8 @@ for k in sorted(set(fetch) | set(write)):
     kern[k]["hbm_bytes_per_launch"] = kern[k]["fetch_bytes_per_launch"] + kern[k]["write_bytes_per_launch"]
 phases = {}
 for ph, names in PHASE_KERNELS.items():
-    ks = [k for k in re.split(r"[|+]", names) if k in kern]
+    want = set(re.split(r"[|+]", names))
+    ks = [k for k in kern if base(k) in want]
     tot = sum(kern[k]["hbm_bytes_per_launch"] * kern[k]["launches"] for k in ks)
     nl = sum(kern[k]["launches"] for k in ks)
     if nl:
