@@ -405,20 +405,25 @@ k_panel(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j
             if (k >= nc || tiny) break;
             __syncthreads();
             const int b2 = k & 1, b3 = k % 3;
-            if (tinys[b2]) { tiny = true; break; }
+            // every LDS read of the step is issued before the zero-pivot
+            // branch: one LDS round trip per column instead of two.  Half 1
+            // applies step k - 1 (cold buffer (k - 1) mod 3).
+            const double lr = h1 ? colk1[b2 ^ 1][lane] : colk[b2][lane];
+            double ck[16];
+#pragma unroll
+            for (int q = qk; q < 16; q++) ck[q] = cold[h1 ? (k + 2) % 3 : b3][4 * q + q0];
+            const double cr = cold[b3][lane];
+            const double dvk = dv[k];
+            const int tzk = tinys[b2];
+            if (tzk) { tiny = true; break; }
             const int kn = k + 1;
             const bool own_next = kn < nc && q0 == (kn & 3);
             if (!h1) {
                 // step k on rows > k.  Rows <= k read l = 0 and only touch
                 // entries right of their diagonal, which nothing reads.
-                const double lr = colk[b2][lane];
-                double ck[16];
-#pragma unroll
-                for (int q = qk; q < 16; q++) ck[q] = cold[b3][4 * q + q0];
                 a[qk] = q0 > pk ? a[qk] - lr * ck[qk] : a[qk];      // column 4 qk + q0 > k
 #pragma unroll
                 for (int q = qk + 1; q < 16; q++) a[q] = a[q] - lr * ck[q];
-                const double cr = cold[b3][lane];
                 dsc = (lane & 3) == q0 ? dsc + fabs(lr * cr) : dsc;   // |term| of the diagonal entry
                 // pivot k + 1 (column kn: register qk in wave pk + 1, or qk + 1 in wave 0)
                 const double an = pk < 3 ? a[qk] : a[qk < 15 ? qk + 1 : qk];
@@ -437,17 +442,12 @@ k_panel(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j
                 }
             } else {
                 if (k > 0) {                  // step k - 1 on columns > k - 1
-                    const int bp = (k - 1) % 3;
-                    const double lr = colk1[b2 ^ 1][lane];
-                    double ck[16];
-#pragma unroll
-                    for (int q = qk; q < 16; q++) ck[q] = cold[bp][4 * q + q0];
                     a[qk] = q0 >= pk ? a[qk] - lr * ck[qk] : a[qk];
 #pragma unroll
                     for (int q = qk + 1; q < 16; q++) a[q] = a[q] - lr * ck[q];
                 }
                 // l(row, k) = a(row, k) / d_k by the owner of column k
-                const double l = rok ? a[qk] / dv[k] : 0.0;
+                const double l = rok ? a[qk] / dvk : 0.0;
                 if (q0 == pk) {
                     a[qk] = l;
                     colk1[b2][lane] = l;
