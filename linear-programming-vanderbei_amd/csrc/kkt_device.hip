@@ -1059,6 +1059,11 @@ k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
     __shared__ double red[R][4][64];
     const int nt = tv.nt, tc = tv.tc, i = blockIdx.x, k0 = i * PC, nc = min(PC, nt - k0);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // the own block's right-hand side and eps do not depend on the chain
+    double eps[R], zown[R];
+    load_eps<R>(epsp, eps);
+#pragma unroll
+    for (int r = 0; r < R; r++) zown[r] = (wv == 0 && lane < nc) ? V.z[r * V.zs + tc + k0 + lane] : 0.0;
     if (tid == 0) lds_pad[0] = 0.0;
     stage_l11(tv.S + k0 + (size_t)k0 * nt, nt, nc, Ls);
     if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
@@ -1089,14 +1094,11 @@ k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
     for (int r = 0; r < R; r++) red[r][wv][lane] = acc[r];
     __syncthreads();
     if (wv == 0) {
-        double eps[R];
-        load_eps<R>(epsp, eps);
         int bad[R] = {};
         double zr[R];
 #pragma unroll
         for (int r = 0; r < R; r++)
-            zr[r] = lane < nc ? V.z[r * V.zs + tc + k0 + lane] -
-                                    (((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane])
+            zr[r] = lane < nc ? zown[r] - (((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane])
                               : 0.0;
         tri_lower<R>(zr, Ls, lv, nc, eps, bad);
         if (lane < nc) {
@@ -1127,6 +1129,14 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
     stage_l11(tv.S + k0 + (size_t)k0 * nt, nt, nc, Ls);
     if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
     const int kq = wv * 16, nq = min(16, nc - kq);
+    // D^{-1} z of the own block does not depend on the chain: formed first
+    double eps[R], zd[R];
+    int bad[R] = {};
+    load_eps<R>(epsp, eps);
+#pragma unroll
+    for (int r = 0; r < R; r++)
+        zd[r] = (wv == 0 && lane < nc) ? dscale_rule(p, tc + k0 + lane, V.z[r * V.zs + tc + k0 + lane], eps[r], bad[r])
+                                       : 0.0;
     double acc[R][16];
 #pragma unroll
     for (int r = 0; r < R; r++)
@@ -1164,15 +1174,9 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
     }
     __syncthreads();
     if (wv == 0) {
-        double eps[R];
-        load_eps<R>(epsp, eps);
-        int bad[R] = {};
         double zr[R];
 #pragma unroll
-        for (int r = 0; r < R; r++)
-            zr[r] = lane < nc ? dscale_rule(p, tc + k0 + lane, V.z[r * V.zs + tc + k0 + lane], eps[r], bad[r]) -
-                                    (i < ntb - 1 ? xs[r][lane] : 0.0)
-                              : 0.0;
+        for (int r = 0; r < R; r++) zr[r] = lane < nc ? zd[r] - (i < ntb - 1 ? xs[r][lane] : 0.0) : 0.0;
         tri_upper<R>(zr, Ls, lv, nc, eps, bad);
         if (lane < nc) {
 #pragma unroll
