@@ -799,8 +799,9 @@ k_backward(PlanView p, const int* __restrict__ level_sups, int q0, SweepVecs V, 
         for (int r = 0; r < R; r++)
 #pragma unroll
             for (int q = 0; q < 16; q++) {
+                if (q >= nq) break;           // columns of the wave beyond nc: no reduction
                 const double t = wave_sum(acc[r][q]);
-                if (lane == 0 && q < nq) xs[r][kq + q] = t;
+                if (lane == 0) xs[r][kq + q] = t;
             }
     }
     __syncthreads();
@@ -848,8 +849,9 @@ k_bwd_partial(PlanView p, const int* __restrict__ chunk_sup, const int* __restri
     for (int r = 0; r < R; r++)
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            const double v = wave_sum((okr && q < nq) ? t[q] * zi[r] : 0.0);
-            if (lane == 0 && q < nq) part[r * ps + (size_t)c * PC + kq + q] = v;
+            if (q >= nq) break;
+            const double v = wave_sum(okr ? t[q] * zi[r] : 0.0);
+            if (lane == 0) part[r * ps + (size_t)c * PC + kq + q] = v;
         }
 }
 
@@ -1167,7 +1169,7 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
 #pragma unroll
         for (int r = 0; r < R; r++)
 #pragma unroll
-            for (int q = 0; q < 16; q++) {
+            for (int q = 0; q < 16; q++) {   // all 16 in one block: the reductions overlap
                 const double v = wave_sum(acc[r][q]);
                 if (lane == 0 && q < nq) xs[r][kq + q] = v;
             }
@@ -1357,8 +1359,9 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
                 for (int r = 0; r < R; r++)
 #pragma unroll
                     for (int q = 0; q < 16; q++) {
-                        const double v = wave_sum((okr && q < nq) ? t[q] * zi[r] : 0.0);
-                        if (lane == 0 && q < nq) sc1_store(part + r * ps + (size_t)code * PC + kq + q, v);
+                        if (q >= nq) break;
+                        const double v = wave_sum(okr ? t[q] * zi[r] : 0.0);
+                        if (lane == 0) sc1_store(part + r * ps + (size_t)code * PC + kq + q, v);
                     }
             }
             sf_arrive(sf.cnt + s);
@@ -1404,8 +1407,9 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             for (int r = 0; r < R; r++)
 #pragma unroll
                 for (int q = 0; q < 16; q++) {
+                    if (q >= nq) break;
                     const double t = wave_sum(acc[r][q]);
-                    if (lane == 0 && q < nq) xs[r][0][kq + q] = t;
+                    if (lane == 0) xs[r][0][kq + q] = t;
                 }
         }
         __syncthreads();
