@@ -1036,6 +1036,7 @@ k_tail_bwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double
 // drains as long as it is resident (ntb <= kChainMaxBlocks).
 constexpr int kChainMaxBlocks = 200;
 constexpr size_t kChainLds = 96 * 1024;
+static_assert(2 * PC * (PC + 1) * sizeof(double) <= kChainLds, "k_tail_bwd_chain scratch");
 
 __device__ __forceinline__ void chain_wait(const int* flags, int j, int epoch) {
     if (threadIdx.x == 0)
@@ -1165,14 +1166,33 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
         }
         __syncthreads();
     }
+    // The 16 column sums of each wave: wave_sum's shfl_down tree (v[l] +=
+    // v[l + o], o = 32 .. 1, result in lane 0), redone from LDS by one thread
+    // per (right-hand side, column) -- the same adds in the same order, so
+    // bitwise the same, without 16 R serial chains of 6 cross-lane permutes.
+    // Scratch = the dynamic LDS pad, rows padded to 65 doubles (conflict-free
+    // column writes and row reads).
+    double* part = lds_pad;   // [R][PC][PC + 1]
     if (nq > 0) {
 #pragma unroll
         for (int r = 0; r < R; r++)
 #pragma unroll
-            for (int q = 0; q < 16; q++) {   // all 16 in one block: the reductions overlap
-                const double v = wave_sum(acc[r][q]);
-                if (lane == 0 && q < nq) xs[r][kq + q] = v;
-            }
+            for (int q = 0; q < 16; q++) part[(size_t)(r * PC + kq + q) * (PC + 1) + lane] = acc[r][q];
+    }
+    __syncthreads();
+    if (tid < R * PC) {
+        const int r = tid / PC, c = tid % PC;
+        if (c < nc) {
+            const double* __restrict__ x = part + (size_t)(r * PC + c) * (PC + 1);
+            double s[32];
+#pragma unroll
+            for (int l = 0; l < 32; l++) s[l] = x[l] + x[l + 32];
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+                for (int l = 0; l < o; l++) s[l] += s[l + o];
+            xs[r][c] = s[0];
+        }
     }
     __syncthreads();
     if (wv == 0) {
