@@ -531,6 +531,33 @@ __device__ __forceinline__ void tri_upper(double (&zr)[R], const double (*Ls)[PC
     }
 }
 
+// Column sums of a wave's 16 (x R) per-lane partials without 16 R serial
+// chains of cross-lane permutes: each wave writes its partials to LDS
+// scratch (rows padded to PC + 1 doubles: conflict-free column writes and
+// row reads), then one thread per (right-hand side, column) redoes
+// wave_sum's shfl_down tree (v[l] += v[l + o], o = 32 .. 1, result in lane
+// 0) on its row -- the same adds in the same order, so bitwise the same.
+// Scratch: R * PC * (PC + 1) doubles; a __syncthreads between the two.
+template <int R>
+__device__ __forceinline__ void colsum_put(double* red, const double (&v)[R][16], int kq, int nq, int lane) {
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+            if (q < nq) red[(size_t)(r * PC + kq + q) * (PC + 1) + lane] = v[r][q];
+}
+__device__ __forceinline__ double colsum_tree(const double* red, int r, int c) {
+    const double* __restrict__ x = red + (size_t)(r * PC + c) * (PC + 1);
+    double s[32];
+#pragma unroll
+    for (int l = 0; l < 32; l++) s[l] = x[l] + x[l + 32];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+        for (int l = 0; l < o; l++) s[l] += s[l + o];
+    return s[0];
+}
+
 template <int R>
 __device__ __forceinline__ void flag_bad(const PlanView& p, const int (&bad)[R]) {
 #pragma unroll
@@ -1166,34 +1193,10 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
         }
         __syncthreads();
     }
-    // The 16 column sums of each wave: wave_sum's shfl_down tree (v[l] +=
-    // v[l + o], o = 32 .. 1, result in lane 0), redone from LDS by one thread
-    // per (right-hand side, column) -- the same adds in the same order, so
-    // bitwise the same, without 16 R serial chains of 6 cross-lane permutes.
-    // Scratch = the dynamic LDS pad, rows padded to 65 doubles (conflict-free
-    // column writes and row reads).
-    double* part = lds_pad;   // [R][PC][PC + 1]
-    if (nq > 0) {
-#pragma unroll
-        for (int r = 0; r < R; r++)
-#pragma unroll
-            for (int q = 0; q < 16; q++) part[(size_t)(r * PC + kq + q) * (PC + 1) + lane] = acc[r][q];
-    }
+    double* red = lds_pad;   // colsum scratch
+    if (nq > 0) colsum_put<R>(red, acc, kq, nq, lane);
     __syncthreads();
-    if (tid < R * PC) {
-        const int r = tid / PC, c = tid % PC;
-        if (c < nc) {
-            const double* __restrict__ x = part + (size_t)(r * PC + c) * (PC + 1);
-            double s[32];
-#pragma unroll
-            for (int l = 0; l < 32; l++) s[l] = x[l] + x[l + 32];
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1)
-#pragma unroll
-                for (int l = 0; l < o; l++) s[l] += s[l + o];
-            xs[r][c] = s[0];
-        }
-    }
+    if (tid < R * PC && tid % PC < nc) xs[tid / PC][tid % PC] = colsum_tree(red, tid / PC, tid % PC);
     __syncthreads();
     if (wv == 0) {
         double zr[R];
@@ -1352,6 +1355,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
     double eps[R];
     load_eps<R>(epsp, eps);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double* red = lds_pad;   // colsum scratch
     if (tid == 0) lds_pad[0] = 0.0;
     for (int it = blockIdx.x; it < sf.nitems; it += gridDim.x) {
         const int2 w = sf.items[it];
@@ -1373,17 +1377,17 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, max(nq, 1) - 1) * h];
             if (par >= 0) chain_wait(sf.flag, par, sf.epoch);
             if (nq > 0) {
-                double zi[R];
+                double zi[R], v[R][16];
                 sf_zrow<R>(sf, V, ri, zi);
 #pragma unroll
                 for (int r = 0; r < R; r++)
 #pragma unroll
-                    for (int q = 0; q < 16; q++) {
-                        if (q >= nq) break;
-                        const double v = wave_sum(okr ? t[q] * zi[r] : 0.0);
-                        if (lane == 0) sc1_store(part + r * ps + (size_t)code * PC + kq + q, v);
-                    }
+                    for (int q = 0; q < 16; q++) v[r][q] = okr ? t[q] * zi[r] : 0.0;
+                colsum_put<R>(red, v, kq, nq, lane);
             }
+            __syncthreads();
+            if (tid < R * PC && tid % PC < nc)
+                sc1_store(part + (tid / PC) * ps + (size_t)code * PC + tid % PC, colsum_tree(red, tid / PC, tid % PC));
             sf_arrive(sf.cnt + s);
             continue;
         }
@@ -1423,16 +1427,13 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
                         for (int r = 0; r < R; r++) acc[r][q] += t[q] * zi[r];
                     }
             }
-#pragma unroll
-            for (int r = 0; r < R; r++)
-#pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    if (q >= nq) break;
-                    const double t = wave_sum(acc[r][q]);
-                    if (lane == 0) xs[r][0][kq + q] = t;
-                }
+            colsum_put<R>(red, acc, kq, nq, lane);
         }
         __syncthreads();
+        if (code != -2) {
+            if (tid < R * PC && tid % PC < nc) xs[tid / PC][0][tid % PC] = colsum_tree(red, tid / PC, tid % PC);
+            __syncthreads();
+        }
         if (wv == 0) {
             int bad[R] = {};
             double zr[R];
