@@ -12,12 +12,37 @@ constexpr int kRedThreads = 256;
 __device__ __forceinline__ double ref_max(double x, double y) { return x > y ? x : y; }
 __device__ __forceinline__ double ref_abs(double x) { return x > 0 ? x : -x; }
 
+// Lane l reads lane l + N of its 16-lane row (DPP row_shl:N, a VALU
+// modifier instead of an LDS-crossbar ds_bpermute); lanes whose source
+// leaves the row keep their own value.
+template <int N>
+__device__ __forceinline__ double dpp_row_down(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = (int)b, hi = (int)(b >> 32);
+    const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, 0x100 + N, 0xf, 0xf, false);
+    const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, 0x100 + N, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi2 << 32) | (unsigned int)lo2);
+}
+
+// Tree v[l] (+)= v[l + o], o = 32, 16, 8, 4, 2, 1; result valid in lane 0.
+// The two cross-row steps go through ds_bpermute, the four in-row steps
+// through DPP; lane 0 sees exactly the adds of the all-shuffle tree.
 __device__ __forceinline__ double wave_sum(double v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    v += __shfl_down(v, 32, 64);
+    v += __shfl_down(v, 16, 64);
+    v += dpp_row_down<8>(v);
+    v += dpp_row_down<4>(v);
+    v += dpp_row_down<2>(v);
+    v += dpp_row_down<1>(v);
     return v;
 }
 __device__ __forceinline__ double wave_max(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_down(v, o, 64));
+    v = fmax(v, __shfl_down(v, 32, 64));
+    v = fmax(v, __shfl_down(v, 16, 64));
+    v = fmax(v, dpp_row_down<8>(v));
+    v = fmax(v, dpp_row_down<4>(v));
+    v = fmax(v, dpp_row_down<2>(v));
+    v = fmax(v, dpp_row_down<1>(v));
     return v;
 }
 
