@@ -2,13 +2,17 @@
 """bench.py -- ipo-hip headline benchmark.
 
 Metric (BASELINE.json): IPM iterations/sec on netlib dfl001, HSD method
-(hsd.c, configs[2]), fp64, one MI355X per rank.  A "step" is one
-interior-point iteration (KKT assembly + supernodal LDL' + two refined
-solves + the O(m+n) step/centering/ratio/update kernels).  The timed region
-is one HSD solve from the reference's start point with the problem already
-resident in HBM (setup = upload + host symbolic analysis, reported apart),
-capped at --steps iterations; the solve converges (mu < 1e-12) after 117
-iterations, which is the default.
+(hsd.c, configs[2]), fp64, one MI355X per rank, at the reference's stopping
+rule.  A "step" is one complete HSD solve of dfl001 from the reference's
+start point to convergence (mu < 1e-12, the metric's "duality gap" proxy,
+SURVEY.md 0.6: 117 interior-point iterations, each one KKT assembly +
+supernodal LDL' + two refined solves + the O(m+n) step/centering/ratio/
+update kernels), with the problem already resident in HBM (setup = upload +
+host symbolic analysis, reported apart).  --warmup W untimed solves, then
+exactly --steps K timed solves; value = iterations of the K solves / their
+wall time.  Every timed solve must end optimal with the golden iteration
+count +-1, otherwise value is null and "metric_condition_met" is false: an
+unconverged run is not reported under the converged label.
 
 N > 1: dfl001 does not shard, so ranks run independent
 replicas; value = all ranks' iterations / max wall time over ranks.
@@ -49,6 +53,7 @@ PHASE_KERNELS = {"gather": "k_update+k_update_reduce", "diag": "k_panel|k_diag",
                  "forward": "k_forward|k_fwd_diag|k_fwd_gemv|k_fwd_sf|k_tail_gather|k_tail_fwd|k_tail_fwd_chain",
                  "backward": "k_backward|k_bwd_partial|k_bwd_finish|k_bwd_sf|k_tail_dscale|k_tail_bwd|k_tail_bwd_chain"}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak, MI355X_MICROARCH.md
+GOLDEN_ITERS = {"dfl001": 117, "25fv47": 91, "afiro": 33}   # evaluate/v1-cf4d5ba/netlib/ipo/*.mps.sol
 
 
 def dist_env():
@@ -84,6 +89,13 @@ class Dist:
             return v
         t = self._t(v)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def min(self, v):
+        if not self.dist:
+            return v
+        t = self._t(v)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
         return float(t.item())
 
     def sum(self, v):
@@ -144,8 +156,8 @@ def block_angular_leg(d, args, sync):
         uid = d.bcast_bytes(ipo_amd.rccl_unique_id() if d.rank == 0 else None, 128)
     ctx = ipo_amd.ShardContext(loc, d.world, d.rank, rccl_id=uid)
     try:
-        if args.warmup > 0:
-            ctx.run("hsd", max_iter=args.warmup)
+        if args.ba_warmup > 0:
+            ctx.run("hsd", max_iter=args.ba_warmup)
         (status, st, _), el = timed_replicas(d, lambda: ctx.run("hsd", max_iter=args.ba_steps), sync)
         setup = d.max(ctx.setup_seconds)
     finally:
@@ -161,14 +173,18 @@ def block_angular_leg(d, args, sync):
             "setup_s": setup, "generate_s": t_gen}
 
 
+WATCHDOG_EXIT = 3
+
+
 def with_watchdog(seconds, fn, on_timeout):
-    """fn() under a watchdog thread: after `seconds` it calls on_timeout() and ends the process."""
+    """fn() under a watchdog thread: after `seconds` it calls on_timeout() and
+    ends the process with a non-zero code (a hang is never a success)."""
     done = threading.Event()
 
     def dog():
         if not done.wait(seconds):
             on_timeout()
-            os._exit(0)
+            os._exit(WATCHDOG_EXIT)
     threading.Thread(target=dog, daemon=True).start()
     try:
         return fn()
@@ -217,14 +233,15 @@ def cpu_baseline(mps, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200, help="IPM iterations timed (MAX_ITER; the solve stops at convergence, 117 for dfl001)")
-    ap.add_argument("--warmup", type=int, default=2, help="untimed IPM iterations before the timed solve")
+    ap.add_argument("--steps", type=int, default=5, help="timed steps: complete HSD solves to convergence (117 iterations each on dfl001)")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed complete solves before the timed ones")
     ap.add_argument("--problem", default="dfl001")
     ap.add_argument("--cpu-iters", type=int, default=3, help="HSD iterations of the CPU oracle sample (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip the instrumented second solve (no roofline)")
     ap.add_argument("--block-angular", choices=["on", "off"], default="on",
                     help="also run BASELINE configs[4] sharded over the ranks (reported under block_angular)")
     ap.add_argument("--ba-steps", type=int, default=200, help="MAX_ITER of the block-angular solve")
+    ap.add_argument("--ba-warmup", type=int, default=2, help="untimed IPM iterations before the block-angular solve")
     ap.add_argument("--ba-timeout", type=float, default=300.0, help="watchdog for the block-angular leg (s)")
     args = ap.parse_args()
 
@@ -245,18 +262,25 @@ def main():
     path = mps_path(args.problem)
     p = ipo_amd.load_mps(path)
     ctx = ipo_amd.Context(p)                       # upload + symbolic (not timed)
-    if args.warmup > 0:
-        ctx.run("hsd", max_iter=args.warmup)
-    # the timed region: one solve with no instrumentation
-    (status, st, _), elapsed = timed_replicas(d, lambda: ctx.run("hsd", max_iter=args.steps), sync)
-    iters = st["iters"]
+    golden = GOLDEN_ITERS.get(args.problem)
+    for _ in range(args.warmup):
+        ctx.run("hsd")
+    # the timed region: K complete solves with no instrumentation
+
+    def solves():
+        return [ctx.run("hsd") for _ in range(args.steps)]
+    runs, elapsed = timed_replicas(d, solves, sync)
+    status, st, _ = runs[-1]
+    iters = sum(r[1]["iters"] for r in runs)
+    converged = all(r[0] == 0 and (golden is None or abs(r[1]["iters"] - golden) <= 1) for r in runs)
+    converged = d.min(1.0 if converged else 0.0) > 0.5
     total_iters = d.sum(iters)
-    value = total_iters / elapsed
-    # the same solve again with per-phase HIP events on the solver's stream
+    value = total_iters / elapsed if converged else None
+    # one more solve with per-phase HIP events on the solver's stream
     # (the events cost ~10 % of wall time, so they stay out of `value`)
-    st_t, elapsed_t = st, elapsed
+    st_t, elapsed_t = st, elapsed / max(args.steps, 1)
     if not args.no_timing:
-        (_, st_t, _), elapsed_t = timed_replicas(d, lambda: ctx.run("hsd", max_iter=args.steps, timing=True), sync)
+        (_, st_t, _), elapsed_t = timed_replicas(d, lambda: ctx.run("hsd", timing=True), sync)
 
     # dominant kernel: the phase with the most device time in the timed
     # region (HIP events on the solver's stream); algorithmic work per
@@ -296,13 +320,17 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_l, "share_of_timed_region": ph["share_of_timed_region"]})
 
     out = {
-        "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": d.world, "steps": iters,
-        "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / max(iters, 1), "higher_is_better": True,
+        "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": d.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / max(args.steps, 1), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": f"netlib {args.problem}.mps (reference problems/netlib, tests/golden copy)",
-        "config": {"workload": f"{args.problem} hsd (BASELINE configs[2])", "method": "hsd", "m": p.m, "n": p.n,
+        "metric_condition_met": converged,
+        "config": {"workload": f"{args.problem} hsd (BASELINE configs[2]), one step = one complete solve to mu < 1e-12",
+                   "method": "hsd", "m": p.m, "n": p.n,
                    "nz": p.nz, "parallelism": f"replicas{d.world}", "status": ipo_amd.STATUS_TEXT.get(status, status),
-                   "iterations": iters, "golden_iterations": 117 if args.problem == "dfl001" else None,
+                   "iterations_per_solve": [r[1]["iters"] for r in runs], "iterations_timed": iters,
+                   "ms_per_iteration": 1e3 * elapsed / max(iters, 1),
+                   "golden_iterations": golden,
                    "final_mu": st["final_mu"], "final_pobj": st["final_pobj"], "final_dobj": st["final_dobj"],
                    "setup_s": ctx.setup_seconds, "lnz": st["lnz"], "nsup": st["nsup"], "levels": st["nlevels"],
                    "factor_ms_total": st_t["factor_ms"], "solve_ms_total": st_t["solve_ms"],
@@ -315,7 +343,8 @@ def main():
     if d.rank == 0 and d.world == 1 and args.cpu_iters > 0:
         try:
             out["cpu_baseline"] = cpu_baseline(path, args.cpu_iters)
-            out["config"]["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+            if value is not None:
+                out["config"]["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
         except Exception as e:  # the GPU number stands on its own
             out["cpu_baseline"] = {"error": str(e)}
     ctx.close()

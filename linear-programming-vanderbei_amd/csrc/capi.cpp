@@ -105,7 +105,8 @@ void fill_stats(ipo_hip_stats* st, const ipo::IpmResult& r, const ipo::KktDevice
 
 int solve_impl(ipo::Method method, int m, int n, int nz, const int* iA, const int* kA, const double* A,
                const double* b, const double* c, double f, double* x, double* y, double* w, double* z, FILE* trace,
-               int max_iter, int timing, ipo_hip_stats* stats) {
+               int max_iter, int timing, ipo_hip_stats* stats, bool* dev_err = nullptr) {
+    if (dev_err) *dev_err = false;
     try {
         if (method != ipo::Method::Hsdls) print_small(trace, m, n, kA, iA, A, b, c);   // hsdls.c has no echo
         ipo::IpmSolver S(m, n, kA, iA, A, b, c, f);
@@ -123,6 +124,7 @@ int solve_impl(ipo::Method method, int m, int n, int nz, const int* iA, const in
     } catch (const std::exception& e) {
         set_err(e.what());
         if (trace) std::fprintf(trace, "ipo_hip: %s\n", e.what());
+        if (dev_err) *dev_err = true;
         return 7;
     }
 }
@@ -276,6 +278,7 @@ int ipo_hip_run_mps(const char* path, int method, FILE* out, int timing, ipo_hip
     if (out) std::fprintf(out, "m = %d,n = %d,nz = %d \n", p.m, p.n, p.kA.empty() ? 0 : p.kA[p.n]);
     ipo::SolverForm s;
     int status = ipo::to_solver_form(p, s);
+    bool dev_err = false;
     if (stats) std::memset(stats, 0, sizeof(*stats));
     if (status == 0) {
         if (out && s.m < 7 && s.n < 7) {   // solve.c:210-222
@@ -295,9 +298,14 @@ int ipo_hip_run_mps(const char* path, int method, FILE* out, int timing, ipo_hip
         std::vector<double> x(s.n + s.m, 0.0), y(s.n + s.m, 0.0), w(s.m > 0 ? s.m : 1, 0.0), z(s.n > 0 ? s.n : 1, 0.0);
         status = solve_impl(method_from_int(method), s.m, s.n, s.nz, s.iA.data(),
                             s.kA.data(), s.A.data(), s.b.data(), s.c.data(), s.f, x.data(), y.data(), w.data(),
-                            z.data(), out, 200, timing, stats);
+                            z.data(), out, 200, timing, stats, &dev_err);
     }
-    if (out) { std::fprintf(out, "%s \n", kStatusText[status]); std::fflush(out); }
+    // a device / host exception is not a numerical outcome: no status text for it
+    if (out) {
+        if (dev_err) std::fprintf(out, "device error: %s\n", g_err.c_str());
+        else std::fprintf(out, "%s \n", kStatusText[status]);
+        std::fflush(out);
+    }
     return status;
 }
 

@@ -163,10 +163,12 @@ class KktDevice {
     int sf_level_ = 0;                    // first level of the range (nlevels: none)
     int nsf_f_ = 0, nsf_b_ = 0, sf_grid_ = 1;
     int sf_fwd_epoch_ = 0, sf_bwd_epoch_ = 0;
+    long long sf_ticket_next_[2] = {0, 0};   // work-item ticket counters (forward, backward): next launch's base
+    int sf_tbase(int d, int nitems);
     size_t zpad_stride_ = 1;
     std::vector<int> h_chunk0_;           // per supernode: first solve chunk (-1: not chunked)
     DevBuf<int2> dsf_items_f_, dsf_items_b_;
-    DevBuf<int> dsf_need_, dsf_par_, dsf_zbase_, dsf_zpi_, dsf_fcnt_, dsf_fflag_, dsf_bcnt_, dsf_bflag_;
+    DevBuf<int> dsf_need_, dsf_par_, dsf_zbase_, dsf_zpi_, dsf_fcnt_, dsf_fflag_, dsf_bcnt_, dsf_bflag_, dsf_ticket_;
     DevBuf<int> dybase_;                  // per supernode: first ybuf slot of its update values
     DevBuf<double> dZpad_;                // padded z slices of the range, 2 right-hand sides
     std::vector<int> fu_ptr_;             // per level: fused panel units [fu_ptr_[l], fu_ptr_[l+1])

@@ -1215,10 +1215,16 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
 // ------------------------------------------- sync-free sweeps, top levels
 // The narrow top of the elimination tree (levels >= sf_level_, a few
 // supernodes each) in one persistent launch per direction instead of one or
-// two launches per level.  One workgroup per CU (dynamic LDS); workgroup w
-// takes the work items w, w + G, ... in list order, and an item only waits
-// on items earlier in the list (descendants forward, ancestors backward), so
-// the grid always drains.  Items: (s, -1) a whole supernode, (s, -2) the
+// two launches per level.  One workgroup per CU (dynamic LDS).  Workgroups
+// draw the work items in list order from a global ticket counter (one
+// agent-scope atomic per item, drawn one item ahead), and an item only waits
+// on items earlier in the list (descendants forward, ancestors backward).
+// An item is therefore only ever held by a running workgroup, and every item
+// it waits on was drawn earlier by a running workgroup: the grid drains
+// whatever share of the CUs the launch gets (co-tenant kernels, several
+// shards on one device).  The counter is never reset within a run: each
+// launch draws exactly nitems + gridDim.x tickets (every workgroup stops at
+// its first ticket past the list), so the host passes the launch's base.  Items: (s, -1) a whole supernode, (s, -2) the
 // diagonal part (forward) / the finish (backward) of a chunked supernode,
 // (s, c >= 0) its 64-row chunk c.  Hand-offs follow MI355X_MICROARCH.md
 // (inter-workgroup visibility, table row 1): the producer writes the values
@@ -1241,7 +1247,18 @@ struct SfView {
     double* zpad;       // padded z slices of R right-hand sides
     size_t zps;
     int epoch;
+    int* ticket;        // work-item counter (see above)
+    int tbase;          // its value when this launch starts
 };
+
+// next work item of this workgroup: thread 0's ticket, through LDS
+__device__ __forceinline__ int sf_draw(const SfView& sf) {
+    return __hip_atomic_fetch_add(sf.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - sf.tbase;
+}
+__device__ __forceinline__ void sf_next(int* tk, int nxt) {
+    if (threadIdx.x == 0) *tk = nxt;
+    __syncthreads();
+}
 
 __device__ __forceinline__ void sf_arrive(int* c) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1261,8 +1278,13 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
     double eps[R];
     load_eps<R>(epsp, eps);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid == 0) lds_pad[0] = 0.0;
-    for (int it = blockIdx.x; it < sf.nitems; it += gridDim.x) {
+    __shared__ int tk[2];
+    if (tid == 0) { lds_pad[0] = 0.0; tk[0] = sf_draw(sf); }
+    __syncthreads();
+    for (int par_ = 0;; par_ ^= 1) {
+        const int it = tk[par_];
+        if (it >= sf.nitems) break;
+        const int nxt = tid == 0 ? sf_draw(sf) : 0;    // drawn one item ahead, stored when the item is done
         const int2 w = sf.items[it];
         const int s = w.x, code = w.y;
         const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
@@ -1333,6 +1355,7 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
             if (par >= 0) sf_arrive(sf.cnt + par);
             else __syncthreads();
         }
+        sf_next(&tk[par_ ^ 1], nxt);
     }
 }
 
@@ -1356,8 +1379,13 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
     load_eps<R>(epsp, eps);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     double* red = lds_pad;   // colsum scratch
-    if (tid == 0) lds_pad[0] = 0.0;
-    for (int it = blockIdx.x; it < sf.nitems; it += gridDim.x) {
+    __shared__ int tk[2];
+    if (tid == 0) { lds_pad[0] = 0.0; tk[0] = sf_draw(sf); }
+    __syncthreads();
+    for (int par_ = 0;; par_ ^= 1) {
+        const int it = tk[par_];
+        if (it >= sf.nitems) break;
+        const int nxt = tid == 0 ? sf_draw(sf) : 0;    // drawn one item ahead, stored when the item is done
         const int2 w = sf.items[it];
         const int s = w.x, code = w.y;
         const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
@@ -1389,6 +1417,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             if (tid < R * PC && tid % PC < nc)
                 sc1_store(part + (tid / PC) * ps + (size_t)code * PC + tid % PC, colsum_tree(red, tid / PC, tid % PC));
             sf_arrive(sf.cnt + s);
+            sf_next(&tk[par_ ^ 1], nxt);
             continue;
         }
         stage_l11(panel, h, nc, Ls);          // the factor does not depend on the hand-off
@@ -1454,6 +1483,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             flag_bad<R>(p, bad);
         }
         chain_publish(sf.flag, s, sf.epoch);
+        sf_next(&tk[par_ ^ 1], nxt);
     }
 }
 
@@ -1859,6 +1889,9 @@ void KktDevice::build_sync_free_plan() {
             b->alloc(ns);
             IPO_HIP_CHECK(hipMemsetAsync(b->get(), 0, ns * sizeof(int), s));
         }
+        dsf_ticket_.alloc(2);
+        IPO_HIP_CHECK(hipMemsetAsync(dsf_ticket_.get(), 0, 2 * sizeof(int), s));
+        sf_ticket_next_[0] = sf_ticket_next_[1] = 0;
         int dev = 0;
         IPO_HIP_CHECK(hipGetDevice(&dev));
         IPO_HIP_CHECK(hipDeviceGetAttribute(&sf_grid_, hipDeviceAttributeMultiprocessorCount, dev));
@@ -2098,7 +2131,8 @@ void KktDevice::sweep(double* dz, const double* epsp) {
     }
     if (sf_level_ < plan_.nlevels) {      // the narrow top levels in one launch
         const SfView sf{dsf_items_f_.get(), nsf_f_, dsf_fcnt_.get(), dsf_fflag_.get(), dsf_need_.get(), dsf_par_.get(),
-                        dsf_zbase_.get(), dsf_zpi_.get(), dZpad_.get(), zpad_stride_, ++sf_fwd_epoch_};
+                        dsf_zbase_.get(), dsf_zpi_.get(), dZpad_.get(), zpad_stride_, ++sf_fwd_epoch_,
+                        dsf_ticket_.get(), sf_tbase(0, nsf_f_)};
         hipLaunchKernelGGL(k_fwd_sf<R>, dim3(std::min(sf_grid_, nsf_f_)), dim3(NT), kChainLds, s, pv, sf,
                            dyrow_ptr_.get(), dyrow_idx_.get(), dchunk_r0_.get(), V, epsp);
     }
@@ -2120,7 +2154,8 @@ void KktDevice::sweep(double* dz, const double* epsp) {
     }
     if (sf_level_ < plan_.nlevels) {
         const SfView sf{dsf_items_b_.get(), nsf_b_, dsf_bcnt_.get(), dsf_bflag_.get(), dsf_need_.get(), dsf_par_.get(),
-                        dsf_zbase_.get(), dsf_zpi_.get(), dZpad_.get(), zpad_stride_, ++sf_bwd_epoch_};
+                        dsf_zbase_.get(), dsf_zpi_.get(), dZpad_.get(), zpad_stride_, ++sf_bwd_epoch_,
+                        dsf_ticket_.get() + 1, sf_tbase(1, nsf_b_)};
         hipLaunchKernelGGL(k_bwd_sf<R>, dim3(std::min(sf_grid_, nsf_b_)), dim3(NT), kChainLds, s, pv, sf,
                            dchunk_r0_.get(), dsup_chunk0_.get(), dPartial_.get(), ps, V, epsp);
     }
@@ -2148,6 +2183,20 @@ void KktDevice::sweep(double* dz, const double* epsp) {
         tm_.phase_count[kPhForward]++;
         tm_.phase_count[kPhBackward]++;
     }
+}
+
+// Ticket base of the next sync-free launch of direction d over nitems items:
+// each launch draws nitems + grid tickets; the counter is cleared (in stream
+// order) before it could overflow.
+int KktDevice::sf_tbase(int d, int nitems) {
+    const long long draw = static_cast<long long>(nitems) + std::min(sf_grid_, nitems);
+    if (sf_ticket_next_[d] + draw > (1LL << 30)) {
+        IPO_HIP_CHECK(hipMemsetAsync(dsf_ticket_.get() + d, 0, sizeof(int), stream_));
+        sf_ticket_next_[d] = 0;
+    }
+    const int base = static_cast<int>(sf_ticket_next_[d]);
+    sf_ticket_next_[d] += draw;
+    return base;
 }
 
 // Very large dense tails (more blocks than the chain kernels keep resident):
@@ -2248,7 +2297,6 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
     hipStream_t s = stream_;
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev0_, s));
     const int m = m_, n = n_, T = T_;
-    IPO_HIP_CHECK(hipMemsetAsync(dIncons_.get(), 0, 2 * sizeof(int), s));
     {   // maxbc_r = MAX(maxv(fx_r), maxv(fy_r)) + 1   (ldlt.c:367)
         RedJobs j{};
         j.nj = 2 * R;
@@ -2270,7 +2318,12 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
     auto dxv = [&](int r) { return dDx_.get() + (size_t)r * n; };
     auto ryv = [&](int r) { return dRy_.get() + (size_t)r * m; };
     auto rxv = [&](int r) { return dRx_.get() + (size_t)r * n; };
+    // the reference's consistency flag is that of each system's last rawsolve
+    // (ldlt.c:379, 424): flags are cleared before every sweep, and the sweep's
+    // right-hand-side slot q of an active system is read back after it
+    int incons[2] = {0, 0};
     while (active[0] || active[1]) {
+        IPO_HIP_CHECK(hipMemsetAsync(dIncons_.get(), 0, 2 * sizeof(int), s));
         for (int r = 0; r < R; r++)
             if (active[r])
                 hipLaunchKernelGGL(k_perm_in, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, dperm_.get(),
@@ -2297,10 +2350,12 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
                            dScal_.get());
         xsum(dScal_.get(), nq, RedOp::Max);
         IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), nq * sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 2, dIncons_.get(), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         int q = 0;
         for (int r = 0; r < R; r++) {
             if (!active[r]) continue;
+            incons[r] = hFlags_[2 + q];
             rs_old[r] = rs[r];
             rs[r] = hScal_[q++];
             pass[r]++;
@@ -2314,13 +2369,12 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
         IPO_HIP_CHECK(hipMemcpyAsync(dfy[r], dyv(r), sizeof(double) * m, hipMemcpyDeviceToDevice, s));
         IPO_HIP_CHECK(hipMemcpyAsync(dfx[r], dxv(r), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
     }
-    IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 2, dIncons_.get(), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
     IPO_HIP_CHECK(hipStreamSynchronize(s));
     if (timing_) { float ms = 0; IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_)); tm_.solve_ms += ms; }
     tm_.solves += R;
     last_passes_ = pass[0] + pass[1];
-    for (int r = 0; r < R; r++) ok[r] = hFlags_[2 + r] ? 0 : 1;
+    for (int r = 0; r < R; r++) ok[r] = incons[r] ? 0 : 1;
 }
 
 int KktDevice::solve(const double* dE, const double* dD, double* dfy, double* dfx) {

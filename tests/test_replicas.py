@@ -38,7 +38,9 @@ def _rank_main(rank, world, port, q):
 
     res, elapsed = bench.timed_replicas(d, block, lambda: None)
     total = d.sum(res)
-    q.put((rank, res, elapsed, total))
+    # the convergence gate: every rank must report its solves converged
+    gate = d.min(1.0 if rank == 0 else 0.0)
+    q.put((rank, res, elapsed, total, gate))
     d.close()
 
 
@@ -55,7 +57,8 @@ def test_replicas_max_time_and_sum_over_two_gloo_ranks():
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    (r0, it0, t0, tot0), (r1, it1, t1, tot1) = out
+    (r0, it0, t0, tot0, g0), (r1, it1, t1, tot1, g1) = out
+    assert g0 == g1 == 0.0                        # one unconverged rank voids the value everywhere
     assert (it0, it1) == (3, 6)
     assert tot0 == tot1 == 9                      # value numerator: all ranks' iterations
     assert t0 == t1                               # max over ranks, identical on every rank

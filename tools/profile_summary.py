@@ -77,7 +77,7 @@ for ph, names in PHASE_KERNELS.items():
     if nl:
         phases[ph] = {"kernels": ks, "launches": nl, "hbm_bytes_per_launch": tot / nl}
 with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:
-    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, bench.py --steps 10 --no-timing "
+    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, bench.py --steps 1 --warmup 0 --no-timing "
                          "(dfl001 hsd, first 10 iterations); FETCH_SIZE doubled (gfx950)",
                "phases": phases, "kernels": kern}, fh, indent=1)
 line = [ln for ln in open(os.path.join(src, f"{tag}_bench.log")) if ln.startswith("{")][-1]
