@@ -496,16 +496,350 @@ k_panel(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j
     if (tid < nc) { p.dg[c0 + tid] = dv[tid]; p.live[c0 + tid] = 1; }
 }
 
+// ------------------------------------------------------- windowed panel
+// The same fused diagonal block + panel rows as k_panel, with the column
+// chain cut into four 16-column windows instead of 64 barrier steps.  Wave
+// w of half 0 (waves 0-3) keeps window w (columns 16w..16w+15) of the
+// block's 64 rows, wave w of half 1 (waves 4-7) window w of tile j + 1.
+// Phase t (one workgroup barrier each):
+//   half 0: every wave w >= t applies the 16 rank-1 updates of window t-1
+//           to its columns (in k order), then wave t factors window t
+//           right-looking on its own, every cross-lane value (pivot, its
+//           |terms|, the window's c_j) by v_readlane -- no LDS round trip
+//           and no workgroup barrier inside a window;
+//   half 1: one phase behind: waves w >= t-1 apply the updates of tile
+//           window t-2, then wave t-1 solves window t-1 of the tile rows
+//           (l = b(k) / d_k, b(j) -= l Ct[k][j]).
+// What crosses waves lives in LDS: Ct[k][r] = l(r, k) d_k (a row of
+// L11 D: the update operand of both halves), Lr[k][r] / Lb[k][r] = l(r, k)
+// of the block rows / tile rows.  Every entry sees the updates k = 0, 1,
+// ... in order with the operations of factor_diag_fast / solve_rows (l =
+// a / d, a -= l (l_j d_k), |terms| of each pivot in dscale order), so the
+// factor is bitwise that of k_panel and of k_diag + k_trsm.  A pivot that
+// fails the zero test raises a flag the whole workgroup reads after the
+// phase's barrier; the panel then stops unwritten (flags[1]), as k_panel.
+constexpr int WIN = 16;
+constexpr int CTS = PC + 2;           // Ct row stride: 16-B aligned rows for ds_read_b128
+
+// in-kernel clock stamps for tools/ubench_panel.hip (compiled out otherwise)
+#ifdef IPO_PANEL_STAMPS
+__device__ long long g_stamps[8][16];
+#define PANEL_STAMP(slot)                                                                         \
+    do {                                                                                          \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) g_stamps[threadIdx.x >> 6][slot] = clock64(); \
+    } while (0)
+#else
+#define PANEL_STAMP(slot) do {} while (0)
+#endif
+
+__device__ __forceinline__ void win_row(const double* __restrict__ row, double (&c)[WIN]) {
+#pragma unroll
+    for (int q = 0; q < WIN; q += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(row + q);
+        c[q] = v.x;
+        c[q + 1] = v.y;
+    }
+}
+
+// The window routines come in a FULL form (all 16 columns inside the
+// block: no per-column guard, so a window is one basic block the compiler
+// can schedule across -- the next step's pivot chain in the shadow of the
+// previous step's updates) and a guarded form for the last, partial window.
+// Window factorisation (half 0, wave t): every cross-lane value by v_readlane.
+template <bool FULL>
+__device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& tz_any, int cw0, int nc, int lane,
+                                           int h0, double tau, double (*Ct)[CTS], double (*Lr)[PC], double* dv) {
+#pragma unroll
+    for (int i = 0; i < WIN; i++) {
+        const int k = cw0 + i;
+        if (FULL || k < nc) {
+            const double dk = lane_bcast(a[i], k);
+            const double dsk = lane_bcast(dsc, k);
+            tz_any = tz_any || fabs(dk) <= tau * dsk;
+            const bool below = lane > k && lane < h0;
+            const double l = below ? a[i] / dk : 0.0;
+            a[i] = below ? l : a[i];
+            const double c = l * dk;
+            Ct[k][lane] = c;
+            Lr[k][lane] = l;
+            dv[k] = dk;                   // every lane stores the same value: no EXEC branch
+            dsc = dsc + fabs(l * c);
+            // column k + 1 (the next pivot's) by v_readlane, the rest of the
+            // window from the LDS row just written: a wavefront fence orders
+            // the reads after the write for the compiler (the LDS runs one
+            // wave's operations in issue order) without pinning the ALU work,
+            // so the next pivot chain can start under the read latency
+            if (i + 1 < WIN) a[i + 1] = a[i + 1] - l * lane_bcast(c, cw0 + i + 1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            if (i + 2 < WIN) {
+                double cc[WIN];
+                win_row(&Ct[k][cw0], cc);
+#pragma unroll
+                for (int q = i + 2; q < WIN; q++) a[q] = a[q] - l * cc[q];
+            }
+        }
+    }
+}
+
+// Rank-1 updates k = kw .. min(kw + 16, k1) - 1 of another window, in k
+// order, on this wave's 16 columns (L = Lr for block rows, Lb for tile rows;
+// DSC: also the |terms| of the diagonal entries this wave owns).
+template <bool FULL, bool DSC>
+__device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw, int k1, int lane, int cw0,
+                                          double (*Ct)[CTS], double (*L)[PC]) {
+    // software-pipelined: step i + 1's LDS operands are read before step i's
+    // arithmetic, so the read latency hides under the updates
+    double l = 0.0, ck = 0.0, cc[WIN];
+    if (FULL || kw < k1) {
+        l = L[kw][lane];
+        if (DSC) ck = Ct[kw][lane];
+        win_row(&Ct[kw][cw0], cc);
+    }
+#pragma unroll
+    for (int i = 0; i < WIN; i++) {
+        const int k = kw + i;
+        if (FULL || k < k1) {
+            double ln = 0.0, ckn = 0.0, cn[WIN];
+            if (i + 1 < WIN && (FULL || k + 1 < k1)) {
+                ln = L[k + 1][lane];
+                if (DSC) ckn = Ct[k + 1][lane];
+                win_row(&Ct[k + 1][cw0], cn);
+            }
+#pragma unroll
+            for (int q = 0; q < WIN; q++) a[q] = a[q] - l * cc[q];
+            if (DSC) dsc = dsc + fabs(l * ck);
+            l = ln;
+            ck = ckn;
+#pragma unroll
+            for (int q = 0; q < WIN; q++) cc[q] = cn[q];
+        }
+    }
+}
+
+// Window solve of the tile rows (half 1, wave t - 1): solve_rows' form.
+template <bool FULL>
+__device__ __forceinline__ void win_solve(double (&a)[WIN], int cw0, int nc, bool rok, int lane, double (*Ct)[CTS],
+                                          double (*Lb)[PC], const double* dv) {
+#pragma unroll
+    for (int i = 0; i < WIN; i++) {
+        const int k = cw0 + i;
+        if (FULL || k < nc) {
+            const double l = rok ? a[i] / dv[k] : 0.0;
+            a[i] = l;
+            Lb[k][lane] = l;
+            double cc[WIN];
+            win_row(&Ct[k][cw0], cc);
+#pragma unroll
+            for (int q = i + 1; q < WIN; q++) a[q] = a[q] - l * cc[q];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(PNT)
+k_panel_w(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j, int f0, TailView tv, int kb) {
+    __shared__ __attribute__((aligned(16))) double Ct[PC][CTS];
+    __shared__ double Lr[PC][PC];
+    __shared__ double Lb[PC][PC];
+    __shared__ double dv[PC];
+    __shared__ int tiny_sh;
+    double* panel;
+    double* wbuf = nullptr;
+    int ld, nc, h, c0, j;
+    if (fu_sup) {
+        const int s = fu_sup[f0 + blockIdx.x];
+        j = fu_j[f0 + blockIdx.x];
+        c0 = p.col0[s];
+        nc = p.col0[s + 1] - c0;
+        h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
+        ld = h;
+        panel = p.Lx + p.off[s];
+    } else {
+        const int k0 = kb * PC;
+        j = blockIdx.x;
+        nc = min(PC, tv.nt - k0);
+        h = tv.nt - k0;
+        ld = tv.nt;
+        c0 = tv.tc + k0;
+        panel = tv.S + k0 + (size_t)k0 * tv.nt;
+        wbuf = tv.W;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    PANEL_STAMP(15);
+    const bool h1 = wv >= 4;
+    const int w = wv & 3, cw0 = WIN * w;
+    const int h0 = min(PC, h);
+    const int row = h1 ? TR * (j + 1) + lane : lane;
+    const bool rok = h1 ? row < h : row < h0;
+    const bool tile = TR * (j + 1) < h;             // workgroup has tile rows
+    const int nwin = (nc + WIN - 1) / WIN;
+    double a[WIN];
+#pragma unroll
+    for (int q = 0; q < WIN; q++) {
+        const int c = cw0 + q;
+        const bool ok = rok && c < nc && (h1 || c <= row);
+        const double t = panel[ok ? row + (size_t)c * ld : 0];
+        a[q] = ok ? t : 0.0;
+    }
+    // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
+    double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
+    if (tid == 0) tiny_sh = 0;
+    PANEL_STAMP(0);
+    const int nph = tile ? nwin + 1 : nwin;
+    for (int t = 0; t < nph; t++) {
+        __syncthreads();
+        PANEL_STAMP(1 + 2 * t);
+        if (tiny_sh) break;
+        if (!h1) {
+            if (w >= t && w < nwin) {
+                if (t > 0) {      // updates of window t - 1, k in order
+                    const int kw = WIN * (t - 1), k1 = min(WIN * t, nc);
+                    if (k1 - kw == WIN) win_apply<true, true>(a, dsc, kw, k1, lane, cw0, Ct, Lr);
+                    else win_apply<false, true>(a, dsc, kw, k1, lane, cw0, Ct, Lr);
+                }
+                PANEL_STAMP(2 + 2 * t);
+                if (w == t) {     // factor window t
+                    bool tz_any = false;
+                    if (cw0 + WIN <= nc) win_factor<true>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv);
+                    else win_factor<false>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv);
+                    if (tz_any && lane == 0) tiny_sh = 1;
+                }
+            }
+        } else if (t >= 1 && w >= t - 1 && w < nwin) {
+            if (t > 1) {          // tile updates of window t - 2, k in order
+                const int kw = WIN * (t - 2), k1 = min(WIN * (t - 1), nc);
+                double unused = 0.0;
+                if (k1 - kw == WIN) win_apply<true, false>(a, unused, kw, k1, lane, cw0, Ct, Lb);
+                else win_apply<false, false>(a, unused, kw, k1, lane, cw0, Ct, Lb);
+            }
+            PANEL_STAMP(2 + 2 * t);
+            if (w == t - 1) {     // solve window t - 1 of the tile rows
+                if (cw0 + WIN <= nc) win_solve<true>(a, cw0, nc, rok, lane, Ct, Lb, dv);
+                else win_solve<false>(a, cw0, nc, rok, lane, Ct, Lb, dv);
+            }
+        }
+    }
+    __syncthreads();
+    PANEL_STAMP(12);
+    if (tiny_sh) {
+        if (tid == 0) atomicOr(&p.flags[1], 1);
+        return;
+    }
+    // half 1: its rows of L21 (and W = L21 D on the dense tail)
+    if (h1 && rok) {
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            if (c < nc) {
+                panel[row + (size_t)c * ld] = a[q];
+                if (wbuf) wbuf[row + (size_t)c * ld] = a[q] * dv[c];
+            }
+        }
+    }
+    if (j != 0) return;
+    // workgroup 0, half 0: rows of R_s inside the first 64 rows, then L11'
+    // into the upper slot through an LDS transpose (Ct is free again), D, mark
+    if (!h1 && lane >= nc && lane < h0) {
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            if (c < nc) {
+                panel[lane + (size_t)c * ld] = a[q];
+                if (wbuf) wbuf[lane + (size_t)c * ld] = a[q] * dv[c];
+            }
+        }
+    }
+    if (!h1) {
+#pragma unroll
+        for (int q = 0; q < WIN; q++) Ct[lane][cw0 + q] = a[q];
+    }
+    __syncthreads();
+    for (int rr = 1 + wv; rr < nc; rr += PNT / 64)
+        if (lane < rr) panel[lane + (size_t)rr * ld] = Ct[rr][lane];
+    if (tid < nc) { p.dg[c0 + tid] = dv[tid]; p.live[c0 + tid] = 1; }
+    PANEL_STAMP(13);
+}
+
+// ------------------------------------------------------- small panels
+// Supernodes with at most 16 columns and 64 rows (the bulk of the bottom
+// levels): one wave each, four per workgroup, no barrier and no LDS.  Lane
+// r keeps row r, columns 0..15 in registers; column step k: pivot and its
+// |terms| by v_readlane, l = a / d_k below the diagonal, c_r = l d_k, and
+// a_r(q) -= l c_q with c_q by v_readlane -- the operations and order of
+// factor_diag_fast per entry (bitwise the same factor).  A pivot that fails
+// the zero test stops the wave before it writes anything and raises
+// flags[1], as the other fused kernels.
+constexpr int SNC = 16;
+
+__global__ void __launch_bounds__(256)
+k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count) {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + wv;
+    if (q >= count) return;
+    const int s = sups[q0 + q];
+    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
+    const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]), ld = h;
+    double* panel = p.Lx + p.off[s];
+    const bool rok = lane < h;
+    double a[SNC];
+#pragma unroll
+    for (int c = 0; c < SNC; c++) {
+        const bool ok = rok && c < nc && c <= lane;
+        const double t = panel[ok ? lane + (size_t)c * ld : 0];
+        a[c] = ok ? t : 0.0;
+    }
+    double dsc = lane < nc ? p.dscale[c0 + lane] : 0.0;
+    double mydv = 0.0;
+#pragma unroll
+    for (int k = 0; k < SNC; k++) {
+        if (k < nc) {
+            const double dk = lane_bcast(a[k], k);
+            const double dsk = lane_bcast(dsc, k);
+            if (fabs(dk) <= p.tau * dsk) {          // wave-uniform
+                if (lane == 0) atomicOr(&p.flags[1], 1);
+                return;
+            }
+            const bool below = lane > k && rok;
+            const double l = below ? a[k] / dk : 0.0;
+            a[k] = below ? l : a[k];
+            mydv = lane == k ? dk : mydv;
+            const double c = l * dk;
+            dsc = dsc + fabs(l * c);
+#pragma unroll
+            for (int qq = k + 1; qq < SNC; qq++)
+                if (qq < nc) a[qq] = a[qq] - l * lane_bcast(c, qq);
+        }
+    }
+    // rows of R_s: L21; rows of the block: L11' into the upper slot
+    if (rok) {
+#pragma unroll
+        for (int c = 0; c < SNC; c++) {
+            if (c < nc && lane >= nc) panel[lane + (size_t)c * ld] = a[c];
+            else if (c < lane && lane < nc) panel[c + (size_t)lane * ld] = a[c];
+        }
+    }
+    if (lane < nc) { p.dg[c0 + lane] = mydv; p.live[c0 + lane] = 1; }
+}
+
 }  // namespace
+
+int g_panel_kind = 2;
+
+void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s) {
+    if (count > 0) hipLaunchKernelGGL(k_panel_s, dim3((count + 3) / 4), dim3(256), 0, s, pv, sups, q0, count);
+}
 
 void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,
                   int kb, hipStream_t s) {
+    const bool w = g_panel_kind == 2;
     if (fu_sup) {
-        if (count > 0) hipLaunchKernelGGL(k_panel, dim3(count), dim3(PNT), 0, s, pv, fu_sup, fu_j, f0, tv, -1);
+        if (count <= 0) return;
+        if (w) hipLaunchKernelGGL(k_panel_w, dim3(count), dim3(PNT), 0, s, pv, fu_sup, fu_j, f0, tv, -1);
+        else hipLaunchKernelGGL(k_panel, dim3(count), dim3(PNT), 0, s, pv, fu_sup, fu_j, f0, tv, -1);
     } else {
         const int h = tv.nt - kb * PC;
-        hipLaunchKernelGGL(k_panel, dim3(std::max(1, (h + TR - 1) / TR - 1)), dim3(PNT), 0, s, pv, nullptr, nullptr, 0,
-                           tv, kb);
+        const int g = std::max(1, (h + TR - 1) / TR - 1);
+        if (w) hipLaunchKernelGGL(k_panel_w, dim3(g), dim3(PNT), 0, s, pv, nullptr, nullptr, 0, tv, kb);
+        else hipLaunchKernelGGL(k_panel, dim3(g), dim3(PNT), 0, s, pv, nullptr, nullptr, 0, tv, kb);
     }
 }
 

@@ -173,6 +173,8 @@ class KktDevice {
     DevBuf<double> dZpad_;                // padded z slices of the range, 2 right-hand sides
     std::vector<int> fu_ptr_;             // per level: fused panel units [fu_ptr_[l], fu_ptr_[l+1])
     DevBuf<int> dfu_sup_, dfu_j_;         // fused panel unit -> supernode, tile pair index
+    std::vector<int> small_ptr_;          // per level: small panels [small_ptr_[l], small_ptr_[l+1]) (k_panel_s)
+    DevBuf<int> dsmall_sups_;
     bool use_panel_ = true;               // fused diagonal-block + panel kernels (IPO_HIP_PANEL=0: off)
     bool factor_pass(const double* dE, const double* dD, bool fused);
     std::vector<int> chunk_ptr_;          // per level: solve chunks [chunk_ptr_[l], chunk_ptr_[l+1])

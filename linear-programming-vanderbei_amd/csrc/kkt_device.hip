@@ -1255,16 +1255,25 @@ struct SfView {
 __device__ __forceinline__ int sf_draw(const SfView& sf) {
     return __hip_atomic_fetch_add(sf.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - sf.tbase;
 }
+// End of an item: the next ticket goes to LDS before the item's last
+// barrier (no extra barrier), then the hand-off of MI355X_MICROARCH.md.
 __device__ __forceinline__ void sf_next(int* tk, int nxt) {
     if (threadIdx.x == 0) *tk = nxt;
     __syncthreads();
 }
-
-__device__ __forceinline__ void sf_arrive(int* c) {
+__device__ __forceinline__ void sf_arrive_next(int* c, int* tk, int nxt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) *tk = nxt;
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void sf_publish_next(int* flags, int i, int epoch, int* tk, int nxt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) *tk = nxt;
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flags + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 
 template <int R>
 __global__ void __launch_bounds__(NT)
@@ -1284,7 +1293,11 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
     for (int par_ = 0;; par_ ^= 1) {
         const int it = tk[par_];
         if (it >= sf.nitems) break;
-        const int nxt = tid == 0 ? sf_draw(sf) : 0;    // drawn one item ahead, stored when the item is done
+        // the next item's ticket is drawn once this item's wait is over (its
+        // atomic then overlaps the item's work, not the wait) and stored at
+        // the item's last barrier
+        int nxt = 0;
+        int* const slot = &tk[par_ ^ 1];
         const int2 w = sf.items[it];
         const int s = w.x, code = w.y;
         const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
@@ -1295,6 +1308,7 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
             stage_l11(panel, h, nc, Ls);      // the factor does not depend on the hand-off
             if (tid < nc) lv[tid] = p.live[c0 + tid];
             chain_wait(sf.cnt, s, sf.epoch * sf.need[s]);
+            if (tid == 0) nxt = sf_draw(sf);
             fwd_diag<R, true, true>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv);
             if (code == -1) {       // y_s = L21 z_s, one row per thread (k_forward)
                 for (int i = tid; i < hb; i += NT) {
@@ -1311,17 +1325,18 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
 #pragma unroll
                     for (int r = 0; r < R; r++) sc1_store(V.y + r * V.ys + p.ybase[s] + i, acc[r]);
                 }
-                if (par >= 0) sf_arrive(sf.cnt + par);
-                else __syncthreads();
+                if (par >= 0) sf_arrive_next(sf.cnt + par, slot, nxt);
+                else sf_next(slot, nxt);
             } else {                // z_s for the chunk items
                 if (tid < nc) {
 #pragma unroll
                     for (int r = 0; r < R; r++) sc1_store(sf.zpad + r * sf.zps + sf.zbase[s] + tid, zl[r][tid]);
                 }
-                chain_publish(sf.flag, s, sf.epoch);
+                sf_publish_next(sf.flag, s, sf.epoch, slot, nxt);
             }
         } else {                    // y over one 64-row chunk (k_fwd_gemv)
             chain_wait(sf.flag, s, sf.epoch);
+            if (tid == 0) nxt = sf_draw(sf);
             if (tid < nc) {
 #pragma unroll
                 for (int r = 0; r < R; r++) zl[r][tid] = sc1_load(sf.zpad + r * sf.zps + sf.zbase[s] + tid);
@@ -1352,10 +1367,9 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
                     sc1_store(V.y + r * V.ys + p.ybase[s] + i,
                               ((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane]);
             }
-            if (par >= 0) sf_arrive(sf.cnt + par);
-            else __syncthreads();
+            if (par >= 0) sf_arrive_next(sf.cnt + par, slot, nxt);
+            else sf_next(slot, nxt);
         }
-        sf_next(&tk[par_ ^ 1], nxt);
     }
 }
 
@@ -1385,7 +1399,8 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
     for (int par_ = 0;; par_ ^= 1) {
         const int it = tk[par_];
         if (it >= sf.nitems) break;
-        const int nxt = tid == 0 ? sf_draw(sf) : 0;    // drawn one item ahead, stored when the item is done
+        int nxt = 0;                // next ticket: drawn after this item's wait, stored at its last barrier
+        int* const slot = &tk[par_ ^ 1];
         const int2 w = sf.items[it];
         const int s = w.x, code = w.y;
         const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
@@ -1404,6 +1419,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
 #pragma unroll
             for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, max(nq, 1) - 1) * h];
             if (par >= 0) chain_wait(sf.flag, par, sf.epoch);
+            if (tid == 0) nxt = sf_draw(sf);
             if (nq > 0) {
                 double zi[R], v[R][16];
                 sf_zrow<R>(sf, V, ri, zi);
@@ -1416,14 +1432,14 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             __syncthreads();
             if (tid < R * PC && tid % PC < nc)
                 sc1_store(part + (tid / PC) * ps + (size_t)code * PC + tid % PC, colsum_tree(red, tid / PC, tid % PC));
-            sf_arrive(sf.cnt + s);
-            sf_next(&tk[par_ ^ 1], nxt);
+            sf_arrive_next(sf.cnt + s, slot, nxt);
             continue;
         }
         stage_l11(panel, h, nc, Ls);          // the factor does not depend on the hand-off
         if (tid < nc) lv[tid] = p.live[c0 + tid];
         if (code == -2) chain_wait(sf.cnt, s, sf.epoch * ((hb + 63) / 64));
         else if (par >= 0) chain_wait(sf.flag, par, sf.epoch);
+        if (tid == 0) nxt = sf_draw(sf);
         if (code == -2) {           // chunk partials in the order of k_bwd_finish
             const int cf = sup_chunk0[s], nch = (hb + 63) / 64;
             double x[R];
@@ -1482,8 +1498,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             }
             flag_bad<R>(p, bad);
         }
-        chain_publish(sf.flag, s, sf.epoch);
-        sf_next(&tk[par_ ^ 1], nxt);
+        sf_publish_next(sf.flag, s, sf.epoch, slot, nxt);
     }
 }
 
@@ -1600,21 +1615,31 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dlevel_sups_.upload(plan_.level_sups, s);
     {   // fused panel units (k_panel): per supernode max(1, tiles - 1) workgroups,
         // workgroup j holding the diagonal block and 64-row tile j + 1
-        std::vector<int> fs, fj;
+        // (supernodes of at most 16 columns and 64 rows go to the one-wave
+        // small-panel kernel instead: list small_sups_, per level small_ptr_)
+        std::vector<int> fs, fj, ss;
         fu_ptr_.assign(plan_.nlevels + 1, 0);
+        small_ptr_.assign(plan_.nlevels + 1, 0);
         for (int l = 0; l < plan_.nlevels; l++) {
             for (int q = plan_.level_ptr[l]; q < plan_.level_ptr[l + 1]; q++) {
                 const int sp = plan_.level_sups[q];
-                const int h = plan_.col0[sp + 1] - plan_.col0[sp] + plan_.rowptr[sp + 1] - plan_.rowptr[sp];
+                const int nc = plan_.col0[sp + 1] - plan_.col0[sp];
+                const int h = nc + plan_.rowptr[sp + 1] - plan_.rowptr[sp];
+                if (nc <= 16 && h <= kTileRows) { ss.push_back(sp); continue; }
                 const int nw = std::max(1, ceil_div(h, kTileRows) - 1);
                 for (int j = 0; j < nw; j++) { fs.push_back(sp); fj.push_back(j); }
             }
             fu_ptr_[l + 1] = static_cast<int>(fs.size());
+            small_ptr_[l + 1] = static_cast<int>(ss.size());
         }
         dfu_sup_.upload(fs, s);
         dfu_j_.upload(fj, s);
+        dsmall_sups_.upload(ss, s);
         IPO_HIP_CHECK(hipStreamSynchronize(s));
-        if (const char* e = std::getenv("IPO_HIP_PANEL")) use_panel_ = std::atoi(e) != 0;
+        if (const char* e = std::getenv("IPO_HIP_PANEL")) {
+            use_panel_ = std::atoi(e) != 0;
+            if (use_panel_) g_panel_kind = std::atoi(e) == 1 ? 1 : 2;
+        }
     }
     {   // solve chunks: levels holding a panel with more than kChunkRows rows below
         // its diagonal block are solved in 64-row chunks (two launches each way)
@@ -1990,8 +2015,10 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         ph_begin(s);
         if (fused) {
-            launch_panel(pv, dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], fu_ptr_[l + 1] - fu_ptr_[l], tv, -1, s);
-            ph_end(kPhDiag, 1, s);
+            const int nsm = small_ptr_[l + 1] - small_ptr_[l], nfu = fu_ptr_[l + 1] - fu_ptr_[l];
+            launch_panel_small(pv, dsmall_sups_.get(), small_ptr_[l], nsm, s);
+            launch_panel(pv, dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], nfu, tv, -1, s);
+            ph_end(kPhDiag, (nsm > 0) + (nfu > 0), s);
         } else {
             launch_diag(pv, dlevel_sups_.get(), q0, q1 - q0, tv, 0, s);
             ph_end(kPhDiag, 1, s);

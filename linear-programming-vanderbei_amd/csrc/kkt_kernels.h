@@ -60,5 +60,12 @@ void launch_trsm(const PlanView& pv, int u0, int count, const TailView& tv, int 
 // the zero test sets flags[1] and leaves the panel unwritten.
 void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,
                   int kb, hipStream_t s);
+// Fused panel of supernodes sups[q0 .. q0+count) that have at most 16
+// columns and 64 rows (one wave each, k_panel_s); same bail-out contract.
+void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s);
+// which fused panel kernel launch_panel runs: 1 = k_panel (8 waves, one
+// barrier per column), 2 = k_panel_w (one wave, no barrier; default);
+// IPO_HIP_PANEL=0 turns the fused path off, =1 / =2 choose the kernel
+extern int g_panel_kind;
 
 }  // namespace ipo
