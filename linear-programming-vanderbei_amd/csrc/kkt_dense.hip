@@ -3,6 +3,7 @@
 // path of ldlt.c:600-614) and the panel triangular solve L21 = A21 L11^-T D^-1.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "dev_common.h"
@@ -635,19 +636,33 @@ __device__ __forceinline__ void win_solve(double (&a)[WIN], int cw0, int nc, boo
     }
 }
 
-__global__ void __launch_bounds__(PNT)
-k_panel_w(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j, int f0, TailView tv, int kb) {
-    __shared__ __attribute__((aligned(16))) double Ct[PC][CTS];
-    __shared__ double Lr[PC][PC];
-    __shared__ double Lb[PC][PC];
-    __shared__ double dv[PC];
-    __shared__ int tiny_sh;
+// LDS image of the windowed panel (one raw buffer, so a kernel can share it
+// with the trailing-update tiles below)
+struct PanelLds {
+    double Ct[PC][CTS];
+    double Lr[PC][PC];
+    double Lb[PC][PC];
+    double dv[PC];
+    int tiny;
+};
+
+// Workgroup `bid` of a windowed panel: fused unit f0 + bid of a sparse level
+// (fu_sup != nullptr) or block column kb of the dense tail, whose W = L21 D
+// goes to wtail.
+__device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __restrict__ fu_sup,
+                                             const int* __restrict__ fu_j, int f0, const TailView& tv, int kb, int bid,
+                                             PanelLds& S, double* wtail) {
+    double (*Ct)[CTS] = S.Ct;
+    double (*Lr)[PC] = S.Lr;
+    double (*Lb)[PC] = S.Lb;
+    double* dv = S.dv;
+    int& tiny_sh = S.tiny;
     double* panel;
     double* wbuf = nullptr;
     int ld, nc, h, c0, j;
     if (fu_sup) {
-        const int s = fu_sup[f0 + blockIdx.x];
-        j = fu_j[f0 + blockIdx.x];
+        const int s = fu_sup[f0 + bid];
+        j = fu_j[f0 + bid];
         c0 = p.col0[s];
         nc = p.col0[s + 1] - c0;
         h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
@@ -655,13 +670,13 @@ k_panel_w(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu
         panel = p.Lx + p.off[s];
     } else {
         const int k0 = kb * PC;
-        j = blockIdx.x;
+        j = bid;
         nc = min(PC, tv.nt - k0);
         h = tv.nt - k0;
         ld = tv.nt;
         c0 = tv.tc + k0;
         panel = tv.S + k0 + (size_t)k0 * tv.nt;
-        wbuf = tv.W;
+        wbuf = wtail;
     }
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     PANEL_STAMP(15);
@@ -759,6 +774,127 @@ k_panel_w(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu
     PANEL_STAMP(13);
 }
 
+__global__ void __launch_bounds__(PNT)
+k_panel_w(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j, int f0, TailView tv, int kb) {
+    __shared__ __attribute__((aligned(16))) char lds[sizeof(PanelLds)];
+    panel_w_body(p, fu_sup, fu_j, f0, tv, kb, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), tv.W);
+}
+
+// ------------------------------------------- dense tail: look-ahead steps
+// Trailing update of the dense tail, one 64 x 64 tile (bi, bj) by 512
+// threads: S(bi, bj) -= L(bi, kb) W(bj, kb)' with v_mfma_f64_16x16x4_f64,
+// every 16 x 16 fragment accumulated over k = 0..63 in the order of
+// k_tail_syrk (bitwise the same update); wave w owns rows 32 (w & 1) ..
+// + 31, columns 16 (w >> 1) .. + 15.  On a diagonal tile the |terms| go to
+// dscale as k_tail_syrk adds them.
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+struct SyrkLds {
+    double As[TR][PC + 1];
+    double Bs[TR][PC + 1];
+};
+
+__device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& tv, int kb, int bi, int bj,
+                                             const double* __restrict__ W, SyrkLds& L) {
+    const int nt = tv.nt, k0 = kb * PC, nc = min(PC, nt - k0), tid = threadIdx.x;
+    const double* Lcol = tv.S + (size_t)k0 * nt;
+    {
+        double va[TR * PC / PNT], vb[TR * PC / PNT];
+#pragma unroll
+        for (int u = 0; u < TR * PC / PNT; u++) {
+            const int idx = tid + u * PNT, rr = idx % TR, k = idx / TR;
+            const int ra = bi * TR + rr, rb = bj * TR + rr;
+            const bool oka = k < nc && ra < nt, okb = k < nc && rb < nt;
+            const double x = Lcol[oka ? ra + (size_t)k * nt : 0];
+            const double y = W[okb ? (rb - k0) + (size_t)k * nt : 0];
+            va[u] = oka ? x : 0.0;
+            vb[u] = okb ? y : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < TR * PC / PNT; u++) {
+            const int idx = tid + u * PNT;
+            L.As[idx % TR][idx / TR] = va[u];
+            L.Bs[idx % TR][idx / TR] = vb[u];
+        }
+    }
+    __syncthreads();
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int wr = (wv & 1) * 32, wc = (wv >> 1) * 16;
+    double4_t acc[2];
+#pragma unroll
+    for (int a = 0; a < 2; a++) acc[a] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < PC; kk += 4) {
+        double av[2];
+#pragma unroll
+        for (int a = 0; a < 2; a++) av[a] = L.As[wr + a * 16 + li][kk + lk];
+        const double bv = L.Bs[wc + li][kk + lk];
+#pragma unroll
+        for (int a = 0; a < 2; a++) acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv, acc[a], 0, 0, 0);
+    }
+    const bool diag_tile = bi == bj;
+    double old[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int rr = wr + a * 16 + (lane >> 4) + 4 * i, cc = wc + (lane & 15);
+            const int rg = bi * TR + rr, cg = bj * TR + cc;
+            const bool ok = rg < nt && cg < nt && !(diag_tile && cc > rr);
+            old[a][i] = ok ? tv.S[rg + (size_t)cg * nt] : 0.0;
+        }
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int rr = wr + a * 16 + (lane >> 4) + 4 * i, cc = wc + (lane & 15);
+            const int rg = bi * TR + rr, cg = bj * TR + cc;
+            if (rg < nt && cg < nt && !(diag_tile && cc > rr)) tv.S[rg + (size_t)cg * nt] = old[a][i] - acc[a][i];
+        }
+    if (diag_tile && tid < TR) {
+        const int rg = bi * TR + tid;
+        if (rg < nt) {
+            double as = 0.0;
+            for (int k = 0; k < nc; k++) as += fabs(L.As[tid][k] * L.Bs[tid][k]);
+            p.dscale[tv.tc + rg] += as;
+        }
+    }
+}
+
+constexpr size_t kTailStepLds = sizeof(PanelLds) > sizeof(SyrkLds) ? sizeof(PanelLds) : sizeof(SyrkLds);
+
+// Step t of the look-ahead dense-tail factorisation, one launch:
+//   workgroups [0, gp):  panel of block column t (k_panel_w's body), its
+//                        W = L21 D into Wcur;
+//   the rest:            R(t - 1), the update of block column t - 1 on the
+//                        columns right of t: tiles (bi, bj), bj >= t + 1.
+// Block column t already holds every update from blocks < t: those of
+// blocks <= t - 2 from earlier R launches, that of block t - 1 from
+// k_tail_urgent(t - 1) right before this launch -- so the big trailing
+// update runs beside the panel instead of between two panels, and every
+// entry still receives the updates of blocks 0, 1, ... in order (bitwise
+// the factor of panel + k_tail_syrk).  W is double-buffered by parity: R
+// reads block t - 1's while the panel writes block t's.
+__global__ void __launch_bounds__(PNT)
+k_tail_pr(PlanView p, TailView tv, int t, int gp, const double* __restrict__ Wprev, double* __restrict__ Wcur) {
+    __shared__ __attribute__((aligned(16))) char lds[kTailStepLds];
+    if ((int)blockIdx.x < gp) {
+        panel_w_body(p, nullptr, nullptr, 0, tv, t, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), Wcur);
+        return;
+    }
+    int tile = blockIdx.x - gp, bj = t + 1;
+    while (tile >= tv.ntb - bj) { tile -= tv.ntb - bj; bj++; }
+    syrk_tile512(p, tv, t - 1, bj + tile, bj, Wprev, *reinterpret_cast<SyrkLds*>(lds));
+}
+
+// U(t): block t's update of block column t + 1 only (tiles (bi, t + 1))
+__global__ void __launch_bounds__(PNT)
+k_tail_urgent(PlanView p, TailView tv, int t, const double* __restrict__ W) {
+    __shared__ __attribute__((aligned(16))) char lds[sizeof(SyrkLds)];
+    syrk_tile512(p, tv, t, t + 1 + blockIdx.x, t + 1, W, *reinterpret_cast<SyrkLds*>(lds));
+}
+
 // ------------------------------------------------------- small panels
 // Supernodes with at most 16 columns and 64 rows (the bulk of the bottom
 // levels): one wave each, four per workgroup, no barrier and no LDS.  Lane
@@ -823,6 +959,18 @@ k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count) {
 }  // namespace
 
 int g_panel_kind = 2;
+
+void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const double* Wprev, double* Wcur,
+                      hipStream_t s) {
+    const int h = tv.nt - t * PC;
+    const int gp = std::max(1, (h + TR - 1) / TR - 1);
+    const int nr = t > 0 ? (tv.ntb - t - 1) * (tv.ntb - t) / 2 : 0;
+    hipLaunchKernelGGL(k_tail_pr, dim3(gp + nr), dim3(PNT), 0, s, pv, tv, t, gp, Wprev, Wcur);
+}
+
+void launch_tail_urgent(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s) {
+    if (tv.ntb - t - 1 > 0) hipLaunchKernelGGL(k_tail_urgent, dim3(tv.ntb - t - 1), dim3(PNT), 0, s, pv, tv, t, W);
+}
 
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s) {
     if (count > 0) hipLaunchKernelGGL(k_panel_s, dim3((count + 3) / 4), dim3(256), 0, s, pv, sups, q0, count);

@@ -1800,7 +1800,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dtail_kslot_ptr_.upload(plan_.tail_kslot_ptr, s);
         static_assert(sizeof(TailTask) == 32, "TailTask layout");
         dtail_tasks_.upload(reinterpret_cast<const uint64_t*>(plan_.tail_tasks.data()), plan_.tail_tasks.size() * 4, s);
-        dW_.alloc(static_cast<size_t>(plan_.nt) * kPanelCols);
+        dW_.alloc(2 * static_cast<size_t>(plan_.nt) * kPanelCols);   // two block columns (look-ahead tail)
         dChainFlags_.alloc(plan_.ntb);
         IPO_HIP_CHECK(hipMemsetAsync(dChainFlags_.get(), 0, plan_.ntb * sizeof(int), s));
         if (plan_.ntb <= kChainMaxBlocks) {
@@ -2034,6 +2034,20 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
         // shards: S = sum of every shard's assembled + gathered tail (exchange.h)
         xsum(tv.S, static_cast<size_t>(plan_.nt) * plan_.nt, RedOp::Sum);
         xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
+        if (fused && g_panel_kind == 2) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
+            const size_t wst = static_cast<size_t>(plan_.nt) * kPanelCols;
+            for (int t = 0; t < plan_.ntb; t++) {
+                double* wc = dW_.get() + (t & 1) * wst;
+                ph_begin(s);
+                launch_tail_step(pv, tv, t, dW_.get() + ((t + 1) & 1) * wst, wc, s);
+                ph_end(kPhDiag, 1, s);
+                if (t + 1 < plan_.ntb) {
+                    ph_begin(s);
+                    launch_tail_urgent(pv, tv, t, wc, s);
+                    ph_end(kPhSyrk, 1, s);
+                }
+            }
+        } else
         for (int kb = 0; kb < plan_.ntb; kb++) {
             const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
             const int below = plan_.nt - k0 - nc;

@@ -60,6 +60,13 @@ void launch_trsm(const PlanView& pv, int u0, int count, const TailView& tv, int 
 // the zero test sets flags[1] and leaves the panel unwritten.
 void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,
                   int kb, hipStream_t s);
+// Look-ahead dense tail (fused path with k_panel_w): step t = panel of block
+// column t beside the trailing update of block t - 1 on columns > t (one
+// launch, W of block t into Wcur, block t - 1's read from Wprev), then
+// launch_tail_urgent(t): block t's update of block column t + 1.
+void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const double* Wprev, double* Wcur,
+                      hipStream_t s);
+void launch_tail_urgent(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s);
 // Fused panel of supernodes sups[q0 .. q0+count) that have at most 16
 // columns and 64 rows (one wave each, k_panel_s); same bail-out contract.
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s);

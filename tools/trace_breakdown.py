@@ -46,11 +46,13 @@ def main():
     acc = defaultdict(lambda: [0, 0.0])
     gaps, span = 0.0, 0.0
     for it in its:
-        first_syrk = next((i for i, r in enumerate(it) if r[2] == "k_tail_syrk"), None)
+        first_syrk = next((i for i, r in enumerate(it) if r[2] in ("k_tail_syrk", "k_tail_urgent")), None)
         t1 = next((i for i, r in enumerate(it) if r[2] == "k_min_abs_partial"), len(it))
         t0 = t1
         if first_syrk is not None:
             t0 = max(i for i in range(first_syrk) if it[i][2].startswith("k_update")) + 1
+            if it[first_syrk][2] == "k_tail_urgent":     # look-ahead tail: starts at its first step
+                t0 = next(i for i in range(first_syrk) if it[i][2] == "k_tail_pr")
         for i, (s, e, k, g) in enumerate(it):
             region = "factor-sparse" if i < t0 else ("factor-tail" if i < t1 else "solve+vec")
             a = acc[(region, k)]
