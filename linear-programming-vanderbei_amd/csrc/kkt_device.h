@@ -42,6 +42,7 @@ struct KktTimers {
     double sweep_ms = 0.0;    // forward + backward substitution sweeps (timing mode)
     long factors = 0, solves = 0, rawsolves = 0;
     long panel_redos = 0;     // factorisations redone without the fused panel kernels
+    long redo_where[4] = {0, 0, 0, 0};   // ... by the kernel that bailed (k_panel, k_panel_w sparse / tail, k_panel_s)
 };
 
 class KktDevice {
@@ -190,6 +191,9 @@ class KktDevice {
     DevBuf<int> dtail_task_ptr_, dkslot_, dkslot_ptr_, dtail_kslot_, dtail_kslot_ptr_;
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;
+    bool coop_tail_ = false;       // redo path: k_tail_diag_coop instead of k_diag + k_trsm on the tail
+    DevBuf<double> dCoopMax_;      // its per-tile maxima
+    DevBuf<int> dCoopCtr_;         // its grid-barrier counter
     // numeric
     DevBuf<double> dLx_, dDg_;
     DevBuf<int> dLive_;

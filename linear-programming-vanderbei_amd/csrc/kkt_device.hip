@@ -23,6 +23,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -1801,6 +1802,16 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         static_assert(sizeof(TailTask) == 32, "TailTask layout");
         dtail_tasks_.upload(reinterpret_cast<const uint64_t*>(plan_.tail_tasks.data()), plan_.tail_tasks.size() * 4, s);
         dW_.alloc(2 * static_cast<size_t>(plan_.nt) * kPanelCols);   // two block columns (look-ahead tail)
+        {   // cooperative redo kernel for the tail: all tiles of a block column resident at once
+            int dev = 0, ncu = 0, coop = 0;
+            IPO_HIP_CHECK(hipGetDevice(&dev));
+            IPO_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+            IPO_HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
+            coop_tail_ = coop != 0 && plan_.ntb <= ncu;
+            if (const char* e = std::getenv("IPO_HIP_COOP_TAIL")) coop_tail_ = coop_tail_ && std::atoi(e) != 0;
+            dCoopMax_.alloc(std::max(1, plan_.ntb));
+            dCoopCtr_.alloc(1);
+        }
         dChainFlags_.alloc(plan_.ntb);
         IPO_HIP_CHECK(hipMemsetAsync(dChainFlags_.get(), 0, plan_.ntb * sizeof(int), s));
         if (plan_.ntb <= kChainMaxBlocks) {
@@ -1928,6 +1939,10 @@ void KktDevice::build_sync_free_plan() {
 }
 
 KktDevice::~KktDevice() {
+    if (std::getenv("IPO_HIP_DEBUG_REDO"))
+        std::fprintf(stderr, "kkt: %ld factorisations, %ld redone; bails k_panel %ld, k_panel_w sparse %ld, tail %ld, "
+                             "k_panel_s %ld\n", tm_.factors, tm_.panel_redos, tm_.redo_where[0], tm_.redo_where[1],
+                     tm_.redo_where[2], tm_.redo_where[3]);
     if (hScal_) (void)hipHostFree(hScal_);
     if (hFlags_) (void)hipHostFree(hFlags_);
     if (ev0_) (void)hipEventDestroy(ev0_);
@@ -1984,6 +1999,7 @@ void KktDevice::factor(const double* dE, const double* dD) {
     // redone with the per-phase kernels, which own the dependent-pivot rule
     if (!factor_pass(dE, dD, use_panel_)) {
         tm_.panel_redos++;
+        for (int b = 0; b < 4; b++) tm_.redo_where[b] += (hFlags_[1] >> b) & 1;
         factor_pass(dE, dD, false);
     }
     tm_.factors++;
@@ -2054,6 +2070,9 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
             ph_begin(s);
             if (fused) {
                 launch_panel(pv, nullptr, nullptr, 0, 0, tv, kb, s);
+                ph_end(kPhDiag, 1, s);
+            } else if (coop_tail_) {   // dependent-pivot rule over all rows of the block column, one launch
+                launch_tail_diag_coop(pv, tv, kb, dCoopMax_.get(), dCoopCtr_.get(), s);
                 ph_end(kPhDiag, 1, s);
             } else {
                 launch_diag(pv, nullptr, 0, 1, tv, kb, s);

@@ -56,3 +56,24 @@ def test_panel_kinds_hsd_trace_bitwise(name):
     columns, dependent-pivot redos): identical printed traces."""
     texts = [_with_panel(kind, lambda: ipo_amd.run_mps(mps_path(name), "hsd"))[1] for kind in ("1", "2")]
     assert texts[0] == texts[1]
+
+
+def _with_env(var, val, fn):
+    old = os.environ.get(var)
+    os.environ[var] = val
+    try:
+        return fn()
+    finally:
+        if old is None:
+            del os.environ[var]
+        else:
+            os.environ[var] = old
+
+
+def test_coop_tail_redo_bitwise():
+    """The redo path's dense tail with dependent pivots: the cooperative
+    k_tail_diag_coop against k_diag + k_trsm (partial substitution per row)
+    on the dfl001 HSD solve, whose redone factorisations hit dependent pivots
+    in the tail -- identical traces."""
+    texts = [_with_env("IPO_HIP_COOP_TAIL", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1] for v in ("0", "1")]
+    assert texts[0] == texts[1]
