@@ -165,6 +165,7 @@ class KktDevice {
     int nsf_f_ = 0, nsf_b_ = 0, sf_grid_ = 1;
     int sf_fwd_epoch_ = 0, sf_bwd_epoch_ = 0;
     long long sf_ticket_next_[2] = {0, 0};   // work-item ticket counters (forward, backward): next launch's base
+    std::vector<int2> h_sf_items_f_;         // forward sync-free items (host copy, developer stamps)
     int sf_tbase(int d, int nitems);
     size_t zpad_stride_ = 1;
     std::vector<int> h_chunk0_;           // per supernode: first solve chunk (-1: not chunked)

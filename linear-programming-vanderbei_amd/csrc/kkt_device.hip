@@ -22,6 +22,10 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <algorithm>
+#include <climits>
+#include <array>
+#include <map>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -614,9 +618,24 @@ struct SweepVecs {
 // Forward, diagonal part of supernode s: subtract the y values of solved
 // descendants from its rows, solve L11.  Leaves z_s in zl[r] and in z.
 // 4 threads per row; partial sums combined as (p0 + p1) + (p2 + p3).
+// per-item wall-clock stamps of the last forward sync-free sweep (developer
+// build with -DIPO_SF_STAMPS; dumped by ~KktDevice)
+#ifdef IPO_SF_STAMPS
+__device__ long long g_sfst[1 << 15][10];
+#define SF_STAMP(it, slot) do { if (threadIdx.x == 0 && (it) >= 0 && (it) < (1 << 15)) g_sfst[it][slot] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define SF_NOTE(it, slot, v) do { if (threadIdx.x == 0 && (it) >= 0 && (it) < (1 << 15)) g_sfst[it][slot] = (v); } while (0)
+#else
+#define SF_STAMP(it, slot) do {} while (0)
+#define SF_NOTE(it, slot, v) do {} while (0)
+#endif
+
+// sidx != nullptr: the supernode's update-list indices, yrow_idx[yrow_ptr[c0]
+// ..], already staged in LDS by the caller (before its hand-off wait), so
+// only the value loads remain on the chain -- sixteen in flight per thread.
 template <int R, bool SC = false, bool STAGED = false>
 __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
-                         const SweepVecs& V, const double (&eps)[R], double (*zl)[PC], double (*Ls)[PC + 1], int* lv) {
+                         const SweepVecs& V, const double (&eps)[R], double (*zl)[PC], double (*Ls)[PC + 1], int* lv,
+                         const int* sidx = nullptr, int stamp_it = -1) {
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -624,33 +643,47 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
         stage_l11(p.Lx + p.off[s], h, nc, Ls);
         if (tid < nc) lv[tid] = p.live[c0 + tid];
     }
-    for (int base = 0; base < nc; base += blockDim.x >> 2) {
-        const int k = base + (tid >> 2), part = tid & 3;
+    // P threads per row (P = 256 / nc rounded down to a power of two, 4..64):
+    // part q sums the entries q, q + P, ... of the row's list in list order
+    // (sixteen loads in flight), then a fixed xor-butterfly combines the P
+    // partial sums -- the same order in every kernel that calls this.
+#ifdef IPO_FWD_P4
+    const int P = 4;
+#else
+    const int P = nc > 32 ? 4 : nc > 16 ? 8 : nc > 8 ? 16 : nc > 4 ? 32 : 64;
+#endif
+    const int ebase = sidx ? yrow_ptr[c0] : 0;
+    // list index e: the staged LDS copy or the global list (no pointer
+    // arithmetic across address spaces)
+    auto lidx = [&](int e) { return sidx ? sidx[e - ebase] : yrow_idx[e]; };
+    for (int base = 0; base < nc; base += blockDim.x / P) {
+        const int k = base + tid / P, part = tid & (P - 1);
         double acc[R];
 #pragma unroll
         for (int r = 0; r < R; r++) acc[r] = 0.0;
         if (k < nc) {
-            // eight, then four entries in flight per thread: index loads
-            // first, then values; one running sum per part in list order
             const int v = c0 + k;
             const int e1 = yrow_ptr[v + 1];
             int e = yrow_ptr[v] + part;
-            for (; e + 28 < e1; e += 32) {
-                int ix[8];
+#ifdef IPO_SF_STAMPS
+            if (tid == 0 && stamp_it >= 0) { g_sfst[stamp_it][9] = e1 + e; SF_STAMP(stamp_it, 7); }
+#endif
+            for (; e + 15 * P < e1; e += 16 * P) {
+                int ix[16];
 #pragma unroll
-                for (int u = 0; u < 8; u++) ix[u] = yrow_idx[e + 4 * u];
+                for (int u = 0; u < 16; u++) ix[u] = lidx(e + u * P);
 #pragma unroll
                 for (int r = 0; r < R; r++) {
                     const double* yb = V.y + r * V.ys;
-                    double yv[8];
+                    double yv[16];
 #pragma unroll
-                    for (int u = 0; u < 8; u++) yv[u] = ld_h<SC>(yb + ix[u]);
+                    for (int u = 0; u < 16; u++) yv[u] = ld_h<SC>(yb + ix[u]);
 #pragma unroll
-                    for (int u = 0; u < 8; u++) acc[r] += yv[u];
+                    for (int u = 0; u < 16; u++) acc[r] += yv[u];
                 }
             }
-            for (; e + 12 < e1; e += 16) {
-                const int i0 = yrow_idx[e], i1 = yrow_idx[e + 4], i2 = yrow_idx[e + 8], i3 = yrow_idx[e + 12];
+            for (; e + 3 * P < e1; e += 4 * P) {
+                const int i0 = lidx(e), i1 = lidx(e + P), i2 = lidx(e + 2 * P), i3 = lidx(e + 3 * P);
 #pragma unroll
                 for (int r = 0; r < R; r++) {
                     const double* yb = V.y + r * V.ys;
@@ -662,22 +695,27 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
                     acc[r] += y3;
                 }
             }
-            for (; e < e1; e += 4) {
-                const int i0 = yrow_idx[e];
+            for (; e < e1; e += P) {
+                const int i0 = lidx(e);
 #pragma unroll
                 for (int r = 0; r < R; r++) acc[r] += ld_h<SC>(V.y + r * V.ys + i0);
             }
         }
+#ifdef IPO_SF_STAMPS
+        if (tid == 0 && stamp_it >= 0) { g_sfst[stamp_it][9] += (long long)acc[0]; SF_STAMP(stamp_it, 8); }
+#endif
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const double o1 = __shfl_xor(acc[r], 1, 64);
-            const double pr = (part & 1) ? o1 + acc[r] : acc[r] + o1;
-            const double o2 = __shfl_xor(pr, 2, 64);
-            const double tot = (part & 2) ? o2 + pr : pr + o2;
-            if (part == 0 && k < nc) zl[r][k] = V.z[r * V.zs + c0 + k] - tot;
+            double pr = acc[r];
+            for (int o = 1; o < P; o <<= 1) {
+                const double ot = __shfl_xor(pr, o, 64);
+                pr = (part & o) ? ot + pr : pr + ot;
+            }
+            if (part == 0 && k < nc) zl[r][k] = V.z[r * V.zs + c0 + k] - pr;
         }
     }
     __syncthreads();
+    SF_STAMP(stamp_it, 5);
     if (wv == 0) {
         int bad[R] = {};
         double zr[R];
@@ -1066,10 +1104,13 @@ constexpr int kChainMaxBlocks = 200;
 constexpr size_t kChainLds = 96 * 1024;
 static_assert(2 * PC * (PC + 1) * sizeof(double) <= kChainLds, "k_tail_bwd_chain scratch");
 
+#ifndef IPO_POLL_SLEEP
+#define IPO_POLL_SLEEP 1
+#endif
 __device__ __forceinline__ void chain_wait(const int* flags, int j, int epoch) {
     if (threadIdx.x == 0)
         while (__hip_atomic_load(const_cast<int*>(flags + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch)
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(IPO_POLL_SLEEP);
     __syncthreads();
 }
 __device__ __forceinline__ void chain_publish(int* flags, int i, int epoch) {
@@ -1236,6 +1277,8 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
 // slices, the zpad mirror, per-chunk partials), written once per sweep, so
 // no consumer can have cached a line before its producer wrote it.  The
 // arithmetic per supernode is that of the per-level kernels (bitwise).
+constexpr int kSfIdx = static_cast<int>(kChainLds / sizeof(int));   // update-list indices staged per item
+
 struct SfView {
     const int2* items;
     int nitems;
@@ -1262,6 +1305,7 @@ __device__ __forceinline__ void sf_next(int* tk, int nxt) {
     if (threadIdx.x == 0) *tk = nxt;
     __syncthreads();
 }
+
 __device__ __forceinline__ void sf_arrive_next(int* c, int* tk, int nxt) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (threadIdx.x == 0) *tk = nxt;
@@ -1299,6 +1343,7 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
         // the item's last barrier
         int nxt = 0;
         int* const slot = &tk[par_ ^ 1];
+        SF_STAMP(it, 0);
         const int2 w = sf.items[it];
         const int s = w.x, code = w.y;
         const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
@@ -1306,13 +1351,45 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
         const int par = sf.parent[s];
         const double* panel = p.Lx + p.off[s];
         if (code < 0) {
-            stage_l11(panel, h, nc, Ls);      // the factor does not depend on the hand-off
+            // the factor does not depend on the hand-off: L11, the marks and
+            // (whole supernodes, hb <= 128 rows: one per thread) this
+            // thread's row of L21 are loaded before the wait
+            double lr[PC];
+            const bool pre = code == -1 && hb <= NT && tid < hb;
+            if (code == -1 && hb > 0) {
+                const double* __restrict__ row = panel + nc + min(tid, hb - 1);
+#pragma unroll
+                for (int k = 0; k < PC; k++) lr[k] = row[(size_t)min(k, nc - 1) * h];
+            }
+            stage_l11(panel, h, nc, Ls);
             if (tid < nc) lv[tid] = p.live[c0 + tid];
+            // the update-list indices do not depend on the hand-off either
+            const int eb = yrow_ptr[c0], ne = yrow_ptr[c0 + nc] - eb;
+            int* sidx = reinterpret_cast<int*>(lds_pad);
+            const bool stg = ne <= kSfIdx;
+            if (stg)
+                for (int e = tid; e < ne; e += NT) sidx[e] = yrow_idx[eb + e];
             chain_wait(sf.cnt, s, sf.epoch * sf.need[s]);
+            SF_STAMP(it, 1);
             if (tid == 0) nxt = sf_draw(sf);
-            fwd_diag<R, true, true>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv);
+            SF_NOTE(it, 6, ne);
+            fwd_diag<R, true, true>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv, stg ? sidx : nullptr, it);
+            SF_STAMP(it, 2);
             if (code == -1) {       // y_s = L21 z_s, one row per thread (k_forward)
-                for (int i = tid; i < hb; i += NT) {
+                if (pre) {
+                    double acc[R];
+#pragma unroll
+                    for (int r = 0; r < R; r++) acc[r] = 0.0;
+#pragma unroll
+                    for (int k = 0; k < PC; k++)
+                        if (k < nc) {
+#pragma unroll
+                            for (int r = 0; r < R; r++) acc[r] += lr[k] * zl[r][k];
+                        }
+#pragma unroll
+                    for (int r = 0; r < R; r++) sc1_store(V.y + r * V.ys + p.ybase[s] + tid, acc[r]);
+                }
+                for (int i = hb <= NT ? hb : tid; i < hb; i += NT) {
                     const double* __restrict__ row = panel + nc + i;
                     double acc[R];
 #pragma unroll
@@ -1326,32 +1403,36 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
 #pragma unroll
                     for (int r = 0; r < R; r++) sc1_store(V.y + r * V.ys + p.ybase[s] + i, acc[r]);
                 }
-                if (par >= 0) sf_arrive_next(sf.cnt + par, slot, nxt);
-                else sf_next(slot, nxt);
+                if (par >= 0) { SF_STAMP(it, 3); sf_arrive_next(sf.cnt + par, slot, nxt); SF_STAMP(it, 4); }
+                else { SF_STAMP(it, 3); sf_next(slot, nxt); SF_STAMP(it, 4); }
             } else {                // z_s for the chunk items
                 if (tid < nc) {
 #pragma unroll
                     for (int r = 0; r < R; r++) sc1_store(sf.zpad + r * sf.zps + sf.zbase[s] + tid, zl[r][tid]);
                 }
-                sf_publish_next(sf.flag, s, sf.epoch, slot, nxt);
+                { SF_STAMP(it, 3); sf_publish_next(sf.flag, s, sf.epoch, slot, nxt); SF_STAMP(it, 4); }
             }
         } else {                    // y over one 64-row chunk (k_fwd_gemv)
+            const int i = chunk_r0[code] + lane, kq = wv * 16, nq = min(16, nc - kq);
+            double t[16];             // the factor tile is loaded before the wait
+            {
+                const double* __restrict__ row = panel + nc + min(i, hb - 1) + (size_t)(nq > 0 ? kq : 0) * h;
+#pragma unroll
+                for (int q = 0; q < 16; q++) t[q] = row[(size_t)min(q, max(nq, 1) - 1) * h];
+            }
             chain_wait(sf.flag, s, sf.epoch);
+            SF_STAMP(it, 1);
+            SF_STAMP(it, 2);
             if (tid == 0) nxt = sf_draw(sf);
             if (tid < nc) {
 #pragma unroll
                 for (int r = 0; r < R; r++) zl[r][tid] = sc1_load(sf.zpad + r * sf.zps + sf.zbase[s] + tid);
             }
             __syncthreads();
-            const int i = chunk_r0[code] + lane, kq = wv * 16, nq = min(16, nc - kq);
             double acc[R];
 #pragma unroll
             for (int r = 0; r < R; r++) acc[r] = 0.0;
             if (i < hb && nq > 0) {
-                const double* __restrict__ row = panel + nc + i + (size_t)kq * h;
-                double t[16];
-#pragma unroll
-                for (int q = 0; q < 16; q++) t[q] = row[(size_t)min(q, nq - 1) * h];
 #pragma unroll
                 for (int q = 0; q < 16; q++)
                     if (q < nq) {
@@ -1368,8 +1449,8 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
                     sc1_store(V.y + r * V.ys + p.ybase[s] + i,
                               ((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane]);
             }
-            if (par >= 0) sf_arrive_next(sf.cnt + par, slot, nxt);
-            else sf_next(slot, nxt);
+            if (par >= 0) { SF_STAMP(it, 3); sf_arrive_next(sf.cnt + par, slot, nxt); SF_STAMP(it, 4); }
+            else { SF_STAMP(it, 3); sf_next(slot, nxt); SF_STAMP(it, 4); }
         }
     }
 }
@@ -1914,6 +1995,7 @@ void KktDevice::build_sync_free_plan() {
     nsf_b_ = static_cast<int>(bi.size());
     if (sf_level_ < P.nlevels) {
         dsf_items_f_.upload(fi, s);
+        h_sf_items_f_ = fi;
         dsf_items_b_.upload(bi, s);
         dsf_need_.upload(need, s);
         dsf_par_.upload(par, s);
@@ -1938,7 +2020,45 @@ void KktDevice::build_sync_free_plan() {
     IPO_HIP_CHECK(hipStreamSynchronize(s));   // the host vectors above are locals
 }
 
+#ifdef IPO_SF_STAMPS
+// Per-level summary of the last forward sync-free sweep's stamps (10 ns
+// ticks): items, mean wait / diag (gather + L11 solve) / rest / hand-off,
+// and when the level's last item finished.
+static void dump_sf_stamps(const std::vector<int2>& items, const KktPlan& P) {
+    std::vector<long long> st((size_t)(1 << 15) * 10);
+    if (hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_sfst), st.size() * sizeof(long long)) != hipSuccess) return;
+    const int n = std::min<int>(items.size(), 1 << 15);
+    long long t0 = LLONG_MAX;
+    for (int i = 0; i < n; i++) t0 = std::min(t0, st[i * 10]);
+    std::map<int, std::array<double, 7>> lv;   // level -> items, wait, diag, rest, end, handoff, ...
+    for (int i = 0; i < n; i++) {
+        const long long* x = &st[i * 10];
+        auto& a = lv[P.level[items[i].x]];
+        a[0] += 1; a[1] += x[1] - x[0]; a[2] += x[2] - x[1]; a[3] += x[3] - x[2]; a[4] = std::max<double>(a[4], x[4] - t0);
+        a[5] += x[4] - x[3];
+    }
+    if (const char* f = std::getenv("IPO_SF_STAMPS_FILE")) {
+        if (FILE* fo = std::fopen(f, "w")) {
+            for (int i = 0; i < n; i++) {
+                const long long* x = &st[i * 10];
+                std::fprintf(fo, "%d %d %d %d %lld %lld %lld %lld %lld %lld %lld %lld %lld\n", items[i].x, items[i].y,
+                             P.level[items[i].x], P.parent[items[i].x], x[0] - t0, x[1] - t0, x[2] - t0, x[3] - t0,
+                             x[4] - t0, x[5] - t0, x[6], x[7] - t0, x[8] - t0);
+            }
+            std::fclose(fo);
+        }
+    }
+    std::fprintf(stderr, "sf forward: level items wait diag rest handoff end(us)\n");
+    for (auto& [l, a] : lv)
+        std::fprintf(stderr, "  %3d %4.0f %7.2f %7.2f %7.2f %6.2f %8.1f\n", l, a[0], a[1] / a[0] / 100, a[2] / a[0] / 100,
+                     a[3] / a[0] / 100, a[5] / a[0] / 100, a[4] / 100);
+}
+#endif
+
 KktDevice::~KktDevice() {
+#ifdef IPO_SF_STAMPS
+    if (!h_sf_items_f_.empty()) dump_sf_stamps(h_sf_items_f_, plan_);
+#endif
     if (std::getenv("IPO_HIP_DEBUG_REDO"))
         std::fprintf(stderr, "kkt: %ld factorisations, %ld redone; bails k_panel %ld, k_panel_w sparse %ld, tail %ld, "
                              "k_panel_s %ld\n", tm_.factors, tm_.panel_redos, tm_.redo_where[0], tm_.redo_where[1],

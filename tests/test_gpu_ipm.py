@@ -47,9 +47,14 @@ UNSTABLE = sorted(set(available_problems()) - set(STABLE))
 # Rounding-stable problems on which the GPU's summation order still lands
 # outside +-1 iteration (the GPU matches the host emulator of its own
 # arithmetic, tools/kkt_emul.cpp, on every one of them).  share1b is
-# unstable but converges under the FMA oracle, not on the GPU.
+# unstable but converges under the FMA oracle, not on the GPU; agg3 (unstable)
+# reaches the reference's mu plateau but sits at 1.7e-12 from iteration 61
+# on, where the reference sat at 1.2e-12 for four iterations before crossing
+# the 1e-12 stop at 69 -- which side of the threshold the plateau lands on
+# is rounding luck (the forward update sums of kkt_device.hip's fwd_diag
+# decide it; the pre-round-2 order converged in 73).
 KNOWN_DIVERGENT = {"agg2": "61 vs 57", "bandm": "57 vs 55", "blend": "35 vs 33", "stocfor2": "99 vs 89",
-                   "share1b": "iteration limit vs 179"}
+                   "share1b": "iteration limit vs 179", "agg3": "mu plateau 1.7e-12: iteration limit vs 69"}
 
 
 def _check_header_and_start(text, gold, rows, grows):

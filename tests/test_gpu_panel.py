@@ -77,3 +77,11 @@ def test_coop_tail_redo_bitwise():
     in the tail -- identical traces."""
     texts = [_with_env("IPO_HIP_COOP_TAIL", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1] for v in ("0", "1")]
     assert texts[0] == texts[1]
+
+
+def test_sync_free_sweeps_bitwise():
+    """The sync-free top-level sweeps (k_fwd_sf / k_bwd_sf) against the
+    per-level launches (IPO_HIP_SF=0): the same arithmetic per supernode, so
+    the dfl001 HSD traces are identical."""
+    texts = [_with_env("IPO_HIP_SF", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1] for v in ("0", "1")]
+    assert texts[0] == texts[1]
