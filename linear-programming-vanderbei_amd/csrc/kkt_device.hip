@@ -485,11 +485,55 @@ k_tail_syrk(PlanView p, TailView tv, int kb) {
 // row of L in registers; z_j is broadcast by v_readlane.  A dropped column j
 // (mark false) keeps z_j when |z_j| > eps (and the system is flagged
 // inconsistent), else z_j = 0 -- ldlt.c:446-470.
+// Fast form when every column of the block is live (the common case):
+// NS = 16, 32 or 64 >= nc steps with no per-step branch (a step j >= nc
+// subtracts L(r, j) z_j = 0 * 0 and changes nothing), so the chain is one
+// basic block the compiler can schedule; the same mul-then-subtract per
+// entry as the general form (bitwise the same result).
+template <int R, int NS>
+__device__ __forceinline__ void tri_lower_live(double (&zr)[R], const double (*Ls)[PC + 1]) {
+    const int lane = threadIdx.x & 63;
+    double lr[NS];
+#pragma unroll
+    for (int j = 0; j < NS; j++) lr[j] = Ls[lane][j];
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const double zj = lane_bcast(zr[r], j);
+            const double nz = zr[r] - lr[j] * zj;
+            zr[r] = lane > j ? nz : zr[r];
+        }
+    }
+}
+template <int R, int NS>
+__device__ __forceinline__ void tri_upper_live(double (&zr)[R], const double (*Ls)[PC + 1]) {
+    const int lane = threadIdx.x & 63;
+    double lc[NS];
+#pragma unroll
+    for (int j = 0; j < NS; j++) lc[j] = Ls[j][lane];
+#pragma unroll
+    for (int j = NS - 1; j >= 0; j--) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const double zj = lane_bcast(zr[r], j);
+            const double nz = zr[r] - lc[j] * zj;
+            zr[r] = lane < j ? nz : zr[r];
+        }
+    }
+}
+
 template <int R>
 __device__ __forceinline__ void tri_lower(double (&zr)[R], const double (*Ls)[PC + 1], const int* lv, int nc,
                                           const double (&eps)[R], int (&bad)[R]) {
     const int lane = threadIdx.x & 63;
     const uint64_t lm = __ballot(lane < nc && lv[lane]);
+    if (lm == (nc >= 64 ? ~0ull : (1ull << nc) - 1ull)) {     // every column live (wave-uniform)
+        if (nc <= 16) tri_lower_live<R, 16>(zr, Ls);
+        else if (nc <= 32) tri_lower_live<R, 32>(zr, Ls);
+        else tri_lower_live<R, 64>(zr, Ls);
+        return;
+    }
     double lr[PC];
 #pragma unroll
     for (int j = 0; j < PC; j++) lr[j] = lane < nc ? Ls[lane][j] : 0.0;
@@ -516,6 +560,12 @@ __device__ __forceinline__ void tri_upper(double (&zr)[R], const double (*Ls)[PC
                                           const double (&eps)[R], int (&bad)[R]) {
     const int lane = threadIdx.x & 63;
     const uint64_t lm = __ballot(lane < nc && lv[lane]);
+    if (lm == (nc >= 64 ? ~0ull : (1ull << nc) - 1ull)) {     // every column live (wave-uniform)
+        if (nc <= 16) tri_upper_live<R, 16>(zr, Ls);
+        else if (nc <= 32) tri_upper_live<R, 32>(zr, Ls);
+        else tri_upper_live<R, 64>(zr, Ls);
+        return;
+    }
     double lc[PC];
 #pragma unroll
     for (int j = 0; j < PC; j++) lc[j] = j < nc ? Ls[j][lane] : 0.0;
