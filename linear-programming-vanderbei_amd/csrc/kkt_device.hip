@@ -685,7 +685,7 @@ __device__ long long g_sfst[1 << 15][10];
 template <int R, bool SC = false, bool STAGED = false>
 __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
                          const SweepVecs& V, const double (&eps)[R], double (*zl)[PC], double (*Ls)[PC + 1], int* lv,
-                         const int* sidx = nullptr, int stamp_it = -1) {
+                         const int* sidx = nullptr, int stamp_it = -1, const int* sptr = nullptr) {
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -702,7 +702,8 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
 #else
     const int P = nc > 32 ? 4 : nc > 16 ? 8 : nc > 8 ? 16 : nc > 4 ? 32 : 64;
 #endif
-    const int ebase = sidx ? yrow_ptr[c0] : 0;
+    // sptr: the rows' list bounds yrow_ptr[c0 .. c0 + nc], staged in LDS by the caller
+    const int ebase = sidx ? (sptr ? sptr[0] : yrow_ptr[c0]) : 0;
     // list index e: the staged LDS copy or the global list (no pointer
     // arithmetic across address spaces)
     auto lidx = [&](int e) { return sidx ? sidx[e - ebase] : yrow_idx[e]; };
@@ -713,11 +714,25 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
         for (int r = 0; r < R; r++) acc[r] = 0.0;
         if (k < nc) {
             const int v = c0 + k;
-            const int e1 = yrow_ptr[v + 1];
-            int e = yrow_ptr[v] + part;
+            const int e1 = sptr ? sptr[k + 1] : yrow_ptr[v + 1];
+            int e = (sptr ? sptr[k] : yrow_ptr[v]) + part;
 #ifdef IPO_SF_STAMPS
             if (tid == 0 && stamp_it >= 0) { g_sfst[stamp_it][9] = e1 + e; SF_STAMP(stamp_it, 7); }
 #endif
+            for (; e + 31 * P < e1; e += 32 * P) {     // 32 loads in flight per right-hand side
+                int ix[32];
+#pragma unroll
+                for (int u = 0; u < 32; u++) ix[u] = lidx(e + u * P);
+                double yv[R][32];
+#pragma unroll
+                for (int r = 0; r < R; r++)
+#pragma unroll
+                    for (int u = 0; u < 32; u++) yv[r][u] = ld_h<SC>(V.y + r * V.ys + ix[u]);
+#pragma unroll
+                for (int r = 0; r < R; r++)
+#pragma unroll
+                    for (int u = 0; u < 32; u++) acc[r] += yv[r][u];
+            }
             for (; e + 15 * P < e1; e += 16 * P) {
                 int ix[16];
 #pragma unroll
@@ -1379,6 +1394,7 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
     __shared__ double Ls[PC][PC + 1];
     __shared__ int lv[PC];
     __shared__ double red[R][4][64];
+    __shared__ int sptr[PC + 1];
     double eps[R];
     load_eps<R>(epsp, eps);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1419,11 +1435,13 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
             const bool stg = ne <= kSfIdx;
             if (stg)
                 for (int e = tid; e < ne; e += NT) sidx[e] = yrow_idx[eb + e];
+            if (tid <= nc) sptr[tid] = yrow_ptr[c0 + tid];
             chain_wait(sf.cnt, s, sf.epoch * sf.need[s]);
             SF_STAMP(it, 1);
             if (tid == 0) nxt = sf_draw(sf);
             SF_NOTE(it, 6, ne);
-            fwd_diag<R, true, true>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv, stg ? sidx : nullptr, it);
+            fwd_diag<R, true, true>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv, stg ? sidx : nullptr, it,
+                                    stg ? sptr : nullptr);
             SF_STAMP(it, 2);
             if (code == -1) {       // y_s = L21 z_s, one row per thread (k_forward)
                 if (pre) {
@@ -1506,9 +1524,9 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
 }
 
 // z of row ri for the backward sweep: the padded mirror inside the range
+// (pi = sf.zpi[ri], looked up before the hand-off wait)
 template <int R>
-__device__ __forceinline__ void sf_zrow(const SfView& sf, const SweepVecs& V, int ri, double (&zi)[R]) {
-    const int pi = sf.zpi[ri];
+__device__ __forceinline__ void sf_zrow(const SfView& sf, const SweepVecs& V, int ri, int pi, double (&zi)[R]) {
 #pragma unroll
     for (int r = 0; r < R; r++) zi[r] = pi >= 0 ? sc1_load(sf.zpad + r * sf.zps + pi) : V.z[r * V.zs + ri];
 }
@@ -1546,6 +1564,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             const bool okr = i < hb;
             const int ic = okr ? i : 0;
             const int ri = rows[ic];
+            const int pi = sf.zpi[ri];
             double t[16];             // the factor tile is loaded before the wait
             const double* __restrict__ col = panel + nc + ic + (size_t)(nq > 0 ? kq : 0) * h;
 #pragma unroll
@@ -1554,7 +1573,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             if (tid == 0) nxt = sf_draw(sf);
             if (nq > 0) {
                 double zi[R], v[R][16];
-                sf_zrow<R>(sf, V, ri, zi);
+                sf_zrow<R>(sf, V, ri, pi, zi);
 #pragma unroll
                 for (int r = 0; r < R; r++)
 #pragma unroll
@@ -1567,8 +1586,37 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             sf_arrive_next(sf.cnt + s, slot, nxt);
             continue;
         }
-        stage_l11(panel, h, nc, Ls);          // the factor does not depend on the hand-off
+        // nothing below depends on the hand-off but the z values of the
+        // ancestors' rows and the chunk partials: L11, the marks, this
+        // block's own z / d / mark (D^-1 z) and, for a whole supernode
+        // (hb <= 128: two rows per lane at most), its L21 tiles and row
+        // lookups are loaded before the wait
+        stage_l11(panel, h, nc, Ls);
         if (tid < nc) lv[tid] = p.live[c0 + tid];
+        double zown[R], dgo = 1.0;
+        int lvo = 1;
+        if (wv == 0 && lane < nc) {
+#pragma unroll
+            for (int r = 0; r < R; r++) zown[r] = V.z[r * V.zs + c0 + lane];
+            lvo = p.live[c0 + lane];
+            dgo = p.dg[c0 + lane];
+        }
+        constexpr int kPre = 2;       // rows per lane prefetched (hb <= 128)
+        double tp[kPre][16];
+        int rip[kPre], pip[kPre];
+        const bool pre = code == -1 && hb <= 64 * kPre && nq > 0;
+        if (pre) {
+#pragma unroll
+            for (int u = 0; u < kPre; u++) {
+                const int i = min(lane + 64 * u, max(hb - 1, 0));
+                rip[u] = hb > 0 ? rows[i] : 0;
+                const double* __restrict__ col = panel + nc + i + (size_t)kq * h;
+#pragma unroll
+                for (int q = 0; q < 16; q++) tp[u][q] = col[(size_t)min(q, nq - 1) * h];
+            }
+#pragma unroll
+            for (int u = 0; u < kPre; u++) pip[u] = hb > 0 ? sf.zpi[rip[u]] : -1;
+        }
         if (code == -2) chain_wait(sf.cnt, s, sf.epoch * ((hb + 63) / 64));
         else if (par >= 0) chain_wait(sf.flag, par, sf.epoch);
         if (tid == 0) nxt = sf_draw(sf);
@@ -1584,6 +1632,27 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
                 }
 #pragma unroll
             for (int r = 0; r < R; r++) xs[r][wv][lane] = x[r];
+        } else if (pre) {           // L21' z_R from the prefetched tiles (same sums as below)
+            double acc[R][16];
+#pragma unroll
+            for (int r = 0; r < R; r++)
+#pragma unroll
+                for (int q = 0; q < 16; q++) acc[r][q] = 0.0;
+            double zi[kPre][R];
+#pragma unroll
+            for (int u = 0; u < kPre; u++)
+                if (lane + 64 * u < hb) sf_zrow<R>(sf, V, rip[u], pip[u], zi[u]);
+#pragma unroll
+            for (int u = 0; u < kPre; u++)
+                if (lane + 64 * u < hb) {
+#pragma unroll
+                    for (int q = 0; q < 16; q++)
+                        if (q < nq) {
+#pragma unroll
+                            for (int r = 0; r < R; r++) acc[r][q] += tp[u][q] * zi[u][r];
+                        }
+                }
+            colsum_put<R>(red, acc, kq, nq, lane);
         } else if (nq > 0) {        // L21' z_R over all rows (k_backward)
             double acc[R][16];
 #pragma unroll
@@ -1592,7 +1661,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
                 for (int q = 0; q < 16; q++) acc[r][q] = 0.0;
             for (int i = lane; i < hb; i += 64) {
                 double zi[R];
-                sf_zrow<R>(sf, V, rows[i], zi);
+                sf_zrow<R>(sf, V, rows[i], sf.zpi[rows[i]], zi);
                 const double* __restrict__ col = panel + nc + i + (size_t)kq * h;
                 double t[16];
 #pragma unroll
@@ -1618,7 +1687,14 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             for (int r = 0; r < R; r++) {
                 const double sub = code == -2 ? ((xs[r][0][lane] + xs[r][1][lane]) + xs[r][2][lane]) + xs[r][3][lane]
                                               : xs[r][0][lane];
-                zr[r] = lane < nc ? dscale_rule(p, c0 + lane, V.z[r * V.zs + c0 + lane], eps[r], bad[r]) - sub : 0.0;
+                double zd = 0.0;        // dscale_rule on the prefetched z, d, mark (ldlt.c:473-480)
+                if (lane < nc) {
+                    zd = zown[r];
+                    if (lvo) zd = zd / dgo;
+                    else if (fabs(zd) > eps[r]) bad[r] = 1;
+                    else zd = 0.0;
+                }
+                zr[r] = lane < nc ? zd - sub : 0.0;
             }
             tri_upper<R>(zr, Ls, lv, nc, eps, bad);
             if (lane < nc) {
