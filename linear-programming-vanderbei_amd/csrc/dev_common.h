@@ -46,6 +46,28 @@ __device__ __forceinline__ double wave_max(double v) {
     return v;
 }
 
+// Sparse row (or column) product sum_k v[k] x[idx[k]] for k in [kb, ke),
+// accumulated in k order (the reference's smx order, linalg.c:62-70) with
+// sixteen index and value loads in flight: a long row costs a few memory
+// round trips instead of one per entry.
+__device__ __forceinline__ double sparse_dot(int kb, int ke, const double* __restrict__ v, const int* __restrict__ idx,
+                                             const double* __restrict__ x) {
+    double s = 0.0;
+    int k = kb;
+    for (; k + 16 <= ke; k += 16) {
+        int ix[16];
+        double a[16], b[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) { ix[u] = idx[k + u]; a[u] = v[k + u]; }
+#pragma unroll
+        for (int u = 0; u < 16; u++) b[u] = x[ix[u]];
+#pragma unroll
+        for (int u = 0; u < 16; u++) s += a[u] * b[u];
+    }
+    for (; k < ke; k++) s += v[k] * x[idx[k]];
+    return s;
+}
+
 // Sum over a 256-thread block; result valid in thread 0.
 __device__ __forceinline__ double block_sum(double v, double* sh /* >= 4 */) {
     v = wave_sum(v);

@@ -52,7 +52,7 @@ k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict
             double ax = 0.0;
             if (i >= mrow) ax = lax[i - mrow];      // linking row of a shard: summed over the shards
             else
-                for (int k = kAt[i]; k < kAt[i + 1]; k++) ax += At[k] * x[iAt[k]];
+                ax = sparse_dot(kAt[i], kAt[i + 1], At, iAt, x);
             const double r1 = ax - b[i] * phi + w[i];
             if (i < mcnt) sr += r1 * r1;
             const double rho = -(1 - delta) * r1 + w[i] - delta * mu / y[i];
@@ -62,7 +62,7 @@ k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict
         } else {
             const int j = i - m;
             double aty = 0.0;
-            for (int k = kA[j]; k < kA[j + 1]; k++) aty += A[k] * y[iA[k]];
+            aty = sparse_dot(kA[j], kA[j + 1], A, iA, y);
             const double s1 = -aty + c[j] * phi + z[j];
             ss += s1 * s1;
             const double sg = -(1 - delta) * s1 + z[j] - delta * mu / x[j];
@@ -188,14 +188,14 @@ k_pf_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict_
             double ax = 0.0;
             if (i >= mrow) ax = lax[i - mrow];      // linking row of a shard: summed over the shards
             else
-                for (int k = kAt[i]; k < kAt[i + 1]; k++) ax += At[k] * x[iAt[k]];
+                ax = sparse_dot(kAt[i], kAt[i + 1], At, iAt, x);
             const double r = b[i] - ax - w[i];
             rho[i] = r;
             if (i < mcnt) sr += r * r;
         } else {
             const int j = i - m;
             double aty = 0.0;
-            for (int k = kA[j]; k < kA[j + 1]; k++) aty += A[k] * y[iA[k]];
+            aty = sparse_dot(kA[j], kA[j + 1], A, iA, y);
             const double s = c[j] - aty + z[j];
             sig[j] = s;
             ss += s * s;

@@ -1121,15 +1121,23 @@ void launch_tail_urgent(const PlanView& pv, const TailView& tv, int t, const dou
     if (tv.ntb - t - 1 > 0) hipLaunchKernelGGL(k_tail_urgent, dim3(tv.ntb - t - 1), dim3(PNT), 0, s, pv, tv, t, W);
 }
 
-void launch_tail_diag_coop(const PlanView& pv, const TailView& tv, int kb, double* gmax, int* gctr, hipStream_t s) {
+bool launch_tail_diag_coop(const PlanView& pv, const TailView& tv, int kb, double* gmax, int* gctr, hipStream_t s) {
     const int below = tv.nt - kb * PC - std::min(PC, tv.nt - kb * PC);
     const int g = std::max(1, (below + TR - 1) / TR);
     IPO_HIP_CHECK(hipMemsetAsync(gctr, 0, sizeof(int), s));
     PlanView p = pv;
     TailView t = tv;
     void* args[] = {&p, &t, &kb, &gmax, &gctr};
-    IPO_HIP_CHECK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_tail_diag_coop), dim3(g), dim3(NT), args,
-                                             0, s));
+    // a cooperative launch is refused (not queued) when its workgroups cannot
+    // all be resident, e.g. beside another tenant: the caller then takes the
+    // two-kernel path, so the grid barrier can never wait on an absent peer
+    const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_tail_diag_coop), dim3(g), dim3(NT),
+                                                    args, 0, s);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return true;
 }
 
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s) {

@@ -1752,14 +1752,14 @@ k_kkt_residual(int m, int n, const int* __restrict__ kAt, const int* __restrict_
             double s = 0.0;
             if (i >= mrow) s = axl[i - mrow];      // linking row: product summed over the shards
             else
-                for (int k = kAt[i]; k < kAt[i + 1]; k++) s += At[k] * dx[iAt[k]];
+                s = sparse_dot(kAt[i], kAt[i + 1], At, iAt, dx);
             const double r = fy[i] - (s - E[i] * dy[i]);
             ry[i] = r;
             mx = fmax(mx, ref_abs(r));
         } else {
             const int j = i - m;
             double s = 0.0;
-            for (int k = kA[j]; k < kA[j + 1]; k++) s += A[k] * dy[iA[k]];
+            s = sparse_dot(kA[j], kA[j + 1], A, iA, dy);
             const double r = fx[j] - (s + D[j] * dx[j]);
             rx[j] = r;
             mx = fmax(mx, ref_abs(r));
@@ -2317,9 +2317,8 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
             if (fused) {
                 launch_panel(pv, nullptr, nullptr, 0, 0, tv, kb, s);
                 ph_end(kPhDiag, 1, s);
-            } else if (coop_tail_) {   // dependent-pivot rule over all rows of the block column, one launch
-                launch_tail_diag_coop(pv, tv, kb, dCoopMax_.get(), dCoopCtr_.get(), s);
-                ph_end(kPhDiag, 1, s);
+            } else if (coop_tail_ && launch_tail_diag_coop(pv, tv, kb, dCoopMax_.get(), dCoopCtr_.get(), s)) {
+                ph_end(kPhDiag, 1, s);     // dependent-pivot rule over all rows of the block column, one launch
             } else {
                 launch_diag(pv, nullptr, 0, 1, tv, kb, s);
                 ph_end(kPhDiag, 1, s);
