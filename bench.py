@@ -24,6 +24,9 @@ Also reported:
   cpu_baseline  -- the CPU oracle (oracle/, a single-threaded restatement of
                    the reference's ipo) timed on this host over a bounded
                    sample of the same workload (rank 0, N = 1);
+  hbm_roofline  -- BASELINE configs[3]: the HBM-bound HSD
+                   vector kernels timed alone on the uniform random LP
+                   (m 200k, n 1M, 4M nonzeros), GB/s against HBM peak;
   block_angular -- BASELINE configs[4]: the synthetic
                    block-angular LP (8 diagonal blocks of 25,000 x 100,000,
                    banded, + 512 linking rows of 2,000 nonzeros) solved by
@@ -176,6 +179,31 @@ def block_angular_leg(d, args, sync):
 WATCHDOG_EXIT = 3
 
 
+HBM_WORKLOAD = ("synthetic random sparse LP, BASELINE configs[3] uniform variant: m=200,000, n=1,000,000, "
+                "4 nnz/column (4.0e6, density 0.002%), seed 20251121")
+
+
+def hbm_roofline_leg(reps):
+    """BASELINE configs[3]: the HBM-bound HSD vector kernels
+    (A x / A'y residuals, directions + ratio test, step) timed alone on the
+    uniform random LP, device-resident; algorithmic bytes per launch over the
+    average launch time against the HBM peak.  The factorisation of this LP
+    is not attempted (uniform rows make L near-dense)."""
+    import ipo_amd
+    p = ipo_amd.synth_random(200000, 1000000, 4, 0)
+    res = ipo_amd.vector_bench(p, reps)
+    kernels = {}
+    for k, (ms, byts) in res.items():
+        gbs = byts / (ms * 1e-3) / 1e9
+        kernels[k] = {"ms_per_launch": ms, "algorithmic_bytes_per_launch": byts, "achieved_gbs": gbs,
+                      "frac": gbs / HBM_PEAK_GBS}
+    top = max(kernels, key=lambda k: kernels[k]["ms_per_launch"])
+    t = kernels[top]
+    return {"workload": HBM_WORKLOAD, "m": p.m, "n": p.n, "nz": p.nz, "launches_timed": reps, "kernels": kernels,
+            "roofline": {"bound": "hbm", "kernel": top, "achieved": t["achieved_gbs"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": t["frac"], "traffic": None}}
+
+
 def with_watchdog(seconds, fn, on_timeout):
     """fn() under a watchdog thread: after `seconds` it calls on_timeout() and
     ends the process with a non-zero code (a hang is never a success)."""
@@ -243,6 +271,8 @@ def main():
     ap.add_argument("--ba-steps", type=int, default=200, help="MAX_ITER of the block-angular solve")
     ap.add_argument("--ba-warmup", type=int, default=2, help="untimed IPM iterations before the block-angular solve")
     ap.add_argument("--ba-timeout", type=float, default=300.0, help="watchdog for the block-angular leg (s)")
+    ap.add_argument("--hbm", choices=["on", "off"], default="on",
+                    help="also time the HBM-bound vector kernels on BASELINE configs[3] (reported under hbm_roofline)")
     args = ap.parse_args()
 
     d = Dist()
@@ -348,6 +378,11 @@ def main():
         except Exception as e:  # the GPU number stands on its own
             out["cpu_baseline"] = {"error": str(e)}
     ctx.close()
+    if args.hbm == "on" and d.rank == 0:
+        try:
+            out["hbm_roofline"] = hbm_roofline_leg(20)
+        except Exception as e:  # noqa: BLE001 -- the headline number stands on its own
+            out["hbm_roofline"] = {"workload": HBM_WORKLOAD, "error": repr(e)}
     if args.block_angular == "on":
         def on_timeout():
             if d.rank == 0:

@@ -161,6 +161,15 @@ int ipo_hip_symbolic_forced(int m, int n, const int *kA, const int *iA, int nfor
  * ys/ws (m) when non-NULL.  band = 0: uniform rows; band > 0: rows from a
  * window of that width around floor(j m / n).  Returns 0, or -1 on bad
  * sizes (ipo_hip_last_error). */
+/* The HBM-bound per-iteration kernels of the HSD loop (A x / A'y with the
+ * residual and right-hand-side vectors, directions + ratio test, step;
+ * hsd.c:182-274) timed alone on device-resident inputs for the LP (m, n, A
+ * CSC): ms3[k] = average ms per launch over `reps`, bytes3[k] = algorithmic
+ * HBM bytes per launch.  Measurement entry of bench.py (no reference
+ * counterpart).  Returns 0, or -1 (ipo_hip_last_error). */
+int ipo_hip_vector_bench(int m, int n, const int *kA, const int *iA, const double *A, int reps, double *ms3,
+                         double *bytes3);
+
 int ipo_hip_synth_random(int m, int n, int per_col, int band, unsigned long long seed, int *nz, int *kA, int *iA,
                          double *A, double *b, double *c, double *xs, double *ys, double *ws, double *zs);
 /* nblocks diagonal blocks (mb x nb, banded random per block) + nlink linking

@@ -554,6 +554,17 @@ void synth_out(const ipo::SynthLP& o, int* kA, int* iA, double* A, double* b, do
 
 extern "C" {
 
+int ipo_hip_vector_bench(int m, int n, const int* kA, const int* iA, const double* A, int reps, double* ms3,
+                         double* bytes3) {
+    try {
+        ipo::vector_bench(m, n, kA, iA, A, reps, ms3, bytes3);
+        return 0;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
+
 int ipo_hip_synth_random(int m, int n, int per_col, int band, unsigned long long seed, int* nz, int* kA, int* iA,
                          double* A, double* b, double* c, double* xs, double* ys, double* ws, double* zs) {
     try {

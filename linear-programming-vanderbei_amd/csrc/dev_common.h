@@ -68,6 +68,43 @@ __device__ __forceinline__ double sparse_dot(int kb, int ke, const double* __res
     return s;
 }
 
+// Sum / max over a block of NW waves in a fixed order; result in thread 0.
+template <int NW>
+__device__ __forceinline__ double block_sum_w(double v, double* sh /* >= NW */) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) {
+        r = sh[0];
+#pragma unroll
+        for (int q = 1; q < NW; q++) r += sh[q];
+    }
+    __syncthreads();
+    return r;
+}
+template <int NW>
+__device__ __forceinline__ double block_max_w(double v, double* sh) {
+    v = wave_max(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double r = 0.0;
+    if (threadIdx.x == 0) {
+        r = sh[0];
+#pragma unroll
+        for (int q = 1; q < NW; q++) r = fmax(r, sh[q]);
+    }
+    __syncthreads();
+    return r;
+}
+// Threads per block of the SpMV residual kernels (k_hsd_residuals,
+// k_pf_residuals, k_kkt_residual): kRedBlocks blocks of kResThreads, so a
+// large LP keeps 16 waves per CU of independent rows in flight; their
+// partials (printed norms, order-free maxima) stay kRedBlocks per quantity.
+constexpr int kResThreads = 1024;
+
 // Sum over a 256-thread block; result valid in thread 0.
 __device__ __forceinline__ double block_sum(double v, double* sh /* >= 4 */) {
     v = wave_sum(v);

@@ -55,6 +55,10 @@ struct ShardSpec {
 
 // Problem uploaded to HBM once; run() iterates from the reference's start
 // point and can be called repeatedly (the bench times run()).
+// bench.py's HBM-roofline leg: the HBM-bound HSD vector kernels timed alone
+// (ipm_device.hip); out[3] ms per launch, bytes[3] algorithmic bytes per launch
+void vector_bench(int m, int n, const int* kA, const int* iA, const double* A, int reps, double* out, double* bytes);
+
 class IpmSolver {
   public:
     IpmSolver(int m, int n, const int* kA, const int* iA, const double* A, const double* b, const double* c,

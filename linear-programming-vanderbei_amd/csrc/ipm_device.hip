@@ -15,8 +15,10 @@
 #include <cmath>
 #include <cstdlib>
 #include <stdexcept>
+#include <vector>
 
 #include "dev_common.h"
+#include "hip_util.h"
 #include "ipm.h"
 
 namespace ipo {
@@ -37,7 +39,7 @@ __global__ void __launch_bounds__(NT) k_fill(int n, double v, double* __restrict
 // cols j < n (hsd.c:191-198, 215, 220, 225):
 //   s1 = -(A'y)_j + c_j phi + z_j ;  ||s1||^2 partial
 //   sigma = -(1-delta) s1 + z - delta mu / x ;  D = z / x ;  fx = -sigma ;  gx = -c
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(kResThreads)
 k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
                 const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
                 const double* __restrict__ b, const double* __restrict__ c, const double* __restrict__ x,
@@ -45,9 +47,9 @@ k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict
                 double delta, double mu, double* __restrict__ E, double* __restrict__ D, double* __restrict__ fy,
                 double* __restrict__ fx, double* __restrict__ gy, double* __restrict__ gx, double* __restrict__ part,
                 int mrow, int mcnt, const double* __restrict__ lax) {
-    __shared__ double sh[4];
+    __shared__ double sh[kResThreads / 64];
     double sr = 0.0, ss = 0.0;
-    for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
+    for (int i = blockIdx.x * kResThreads + threadIdx.x; i < m + n; i += kRedBlocks * kResThreads) {
         if (i < m) {
             double ax = 0.0;
             if (i >= mrow) ax = lax[i - mrow];      // linking row of a shard: summed over the shards
@@ -71,8 +73,8 @@ k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict
             gx[j] = -c[j];
         }
     }
-    sr = block_sum(sr, sh);
-    ss = block_sum(ss, sh);
+    sr = block_sum_w<kResThreads / 64>(sr, sh);
+    ss = block_sum_w<kResThreads / 64>(ss, sh);
     if (threadIdx.x == 0) { part[blockIdx.x] = sr; part[kRedBlocks + blockIdx.x] = ss; }
 }
 
@@ -174,16 +176,16 @@ k_hsdls_directions(int m, int n, double dphi, double beta, double delta, double 
 
 // ---------------------------------------------------------------- intpt
 // rho = b - A x - w, sigma = c - A'y + z and their squared norms (intpt.c:139-149)
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(kResThreads)
 k_pf_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
                const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
                const double* __restrict__ b, const double* __restrict__ c, const double* __restrict__ x,
                const double* __restrict__ y, const double* __restrict__ w, const double* __restrict__ z,
                double* __restrict__ rho, double* __restrict__ sig, double* __restrict__ part, int mrow, int mcnt,
                const double* __restrict__ lax) {
-    __shared__ double sh[4];
+    __shared__ double sh[kResThreads / 64];
     double sr = 0.0, ss = 0.0;
-    for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
+    for (int i = blockIdx.x * kResThreads + threadIdx.x; i < m + n; i += kRedBlocks * kResThreads) {
         if (i < m) {
             double ax = 0.0;
             if (i >= mrow) ax = lax[i - mrow];      // linking row of a shard: summed over the shards
@@ -201,8 +203,8 @@ k_pf_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict_
             ss += s * s;
         }
     }
-    sr = block_sum(sr, sh);
-    ss = block_sum(ss, sh);
+    sr = block_sum_w<kResThreads / 64>(sr, sh);
+    ss = block_sum_w<kResThreads / 64>(ss, sh);
     if (threadIdx.x == 0) { part[blockIdx.x] = sr; part[kRedBlocks + blockIdx.x] = ss; }
 }
 
@@ -394,7 +396,7 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
             break;
         }
         link_ax(x_.get());
-        hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(NT), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
+        hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
                            K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), phi, delta, mu,
                            E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get(), mrow(), mcnt_,
                            lax());
@@ -495,7 +497,7 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
             break;
         }
         link_ax(x_.get());
-        hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(NT), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
+        hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
                            K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), phi, delta, mu,
                            E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get(), mrow(), mcnt_,
                            lax());
@@ -576,7 +578,7 @@ int IpmSolver::run_intpt(const IpmOptions& opt, IpmResult* res) {
     int status = 5, iter;
     for (iter = 0; iter < opt.max_iter; iter++) {
         link_ax(x_.get());
-        hipLaunchKernelGGL(k_pf_residuals, dim3(kRedBlocks), dim3(NT), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
+        hipLaunchKernelGGL(k_pf_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
                            K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), rho_.get(),
                            sig_.get(), part_.get(), mrow(), mcnt_, lax());
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get() + 8);
@@ -629,6 +631,87 @@ int IpmSolver::run_intpt(const IpmOptions& opt, IpmResult* res) {
     IPO_HIP_CHECK(hipStreamSynchronize(s));
     res->iters = iter;
     return status;
+}
+
+// The HBM-bound per-iteration kernels of the HSD loop timed on their own
+// (bench.py's hbm_roofline leg, BASELINE configs[3] uniform): A x / A' y
+// with the residual and right-hand-side vectors (k_hsd_residuals), the
+// directions + ratio test (k_hsd_directions) and the step (k_step), each
+// with the launch geometry of run_hsd, on device-resident inputs, `reps`
+// launches timed with HIP events on one stream.  out[3] = average ms per
+// launch; bytes[3] = algorithmic HBM bytes per launch (every array element
+// read or written once).
+void vector_bench(int m, int n, const int* kA, const int* iA, const double* A, int reps, double* out, double* bytes) {
+    const long nz = kA[n];
+    // CSR of A (the reference's atnum, hsd.c:111)
+    std::vector<int> kAt(m + 1, 0), iAt(nz);
+    std::vector<double> At(nz);
+    for (long k = 0; k < nz; k++) kAt[iA[k] + 1]++;
+    for (int i = 0; i < m; i++) kAt[i + 1] += kAt[i];
+    {
+        std::vector<int> pos(kAt.begin(), kAt.end() - 1);
+        for (int j = 0; j < n; j++)
+            for (int k = kA[j]; k < kA[j + 1]; k++) { iAt[pos[iA[k]]] = j; At[pos[iA[k]]++] = A[k]; }
+    }
+    hipStream_t s;
+    IPO_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    DevBuf<int> dkA, diA, dkAt, diAt;
+    DevBuf<double> dA, dAt, vec;
+    dkA.upload(kA, n + 1, s);
+    diA.upload(iA, nz, s);
+    dA.upload(A, nz, s);
+    dkAt.upload(kAt, s);
+    diAt.upload(iAt, s);
+    dAt.upload(At, s);
+    const size_t N = static_cast<size_t>(m) + n;
+    vec.alloc(24 * N + 2 * kRedBlocks);
+    {
+        std::vector<double> v(24 * N, 1.0);
+        for (size_t i = 0; i < v.size(); i++) v[i] = 0.5 + (i % 997) * 1e-3;
+        vec.upload(v, s);
+    }
+    double* V = vec.get();
+    auto col = [&](int q) { return V + q * N; };      // n-vectors at col(q), m-vectors at col(q) + n
+    double* part = V + 24 * N;
+    hipEvent_t e0, e1;
+    IPO_HIP_CHECK(hipEventCreate(&e0));
+    IPO_HIP_CHECK(hipEventCreate(&e1));
+    const int gv = static_cast<int>((N + NT - 1) / NT);
+    for (int kq = 0; kq < 3; kq++) {
+        for (int r = -2; r < reps; r++) {                 // two untimed launches first
+            if (r == 0) IPO_HIP_CHECK(hipEventRecord(e0, s));
+            if (kq == 0)
+                hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, dkAt.get(), diAt.get(),
+                                   dAt.get(), dkA.get(), diA.get(), dA.get(), col(0) + n, col(1), col(2), col(3) + n,
+                                   col(4) + n, col(5), 1.0, 0.5, 0.1, col(6) + n, col(7), col(8) + n, col(9),
+                                   col(10) + n, col(11), part, m, m, static_cast<const double*>(nullptr));
+            else if (kq == 1)
+                hipLaunchKernelGGL(k_hsd_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, 0.3, 0.5, 0.1, col(9),
+                                   col(11), col(8) + n, col(10) + n, col(2), col(5), col(3) + n, col(4) + n, col(7),
+                                   col(6) + n, col(12), col(13), col(14) + n, col(15) + n, part);
+            else
+                hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, 1e-9, col(16), col(12), col(17), col(13),
+                                   col(18) + n, col(14) + n, col(19) + n, col(15) + n);
+        }
+        IPO_HIP_CHECK(hipEventRecord(e1, s));
+        IPO_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        IPO_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        out[kq] = ms / reps;
+    }
+    IPO_HIP_CHECK(hipGetLastError());
+    // algorithmic bytes (N = m + n): residuals -- CSR + CSC of A (12 B per
+    // entry each, 4 B per pointer), b w y / c z x read once (x, y also the
+    // gathered operands), E fy gy / D fx gx written: 24 nz + 4 N + 48 N;
+    // directions -- 5 vectors read per row / column, 2 written: 56 N;
+    // step -- 4 read, 2 written: 48 N
+    bytes[0] = 24.0 * nz + 52.0 * N;
+    bytes[1] = 56.0 * N;
+    bytes[2] = 48.0 * N;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    IPO_HIP_CHECK(hipStreamSynchronize(s));
+    (void)hipStreamDestroy(s);
 }
 
 int ipm_solve_host(int m, int n, int nz, const int* iA, const int* kA, const double* A, const double* b,

@@ -1738,16 +1738,16 @@ k_perm_out(int T, int m, const int* __restrict__ iperm, const double* __restrict
 //   ry_j = fy_j - ((A dx)_j - E_j dy_j)        row gather over CSR
 //   rx_i = fx_i - ((A' dy)_i + D_i dx_i)       column gather over CSC
 // plus max-abs partials of both (ldlt.c:401).
-__global__ void __launch_bounds__(NT)
+__global__ void __launch_bounds__(kResThreads)
 k_kkt_residual(int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
                const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
                const double* __restrict__ E, const double* __restrict__ D, const double* __restrict__ fy,
                const double* __restrict__ fx, const double* __restrict__ dy, const double* __restrict__ dx,
                double* __restrict__ ry, double* __restrict__ rx, double* __restrict__ part, int mrow,
                const double* __restrict__ axl) {
-    __shared__ double sh[4];
+    __shared__ double sh[kResThreads / 64];
     double mx = 0.0;
-    for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
+    for (int i = blockIdx.x * kResThreads + threadIdx.x; i < m + n; i += kRedBlocks * kResThreads) {
         if (i < m) {
             double s = 0.0;
             if (i >= mrow) s = axl[i - mrow];      // linking row: product summed over the shards
@@ -1765,7 +1765,7 @@ k_kkt_residual(int m, int n, const int* __restrict__ kAt, const int* __restrict_
             mx = fmax(mx, ref_abs(r));
         }
     }
-    mx = block_max(mx, sh);
+    mx = block_max_w<kResThreads / 64>(mx, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = mx;
 }
 
@@ -2646,7 +2646,7 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
                 launch_link_ax(mrow, m, dkAt_.get(), diAt_.get(), dAt_.get(), dxv(r), axl, s);
                 xsum(axl, nforced_, RedOp::Sum);
             }
-            hipLaunchKernelGGL(k_kkt_residual, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dkAt_.get(), diAt_.get(),
+            hipLaunchKernelGGL(k_kkt_residual, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, dkAt_.get(), diAt_.get(),
                                dAt_.get(), dkA_.get(), diA_.get(), dA_.get(), dE, dD, dfy[r], dfx[r], dyv(r), dxv(r),
                                ryv(r), rxv(r), dPart_.get() + (size_t)nq * kRedBlocks, mrow, axl);
             nq++;

@@ -75,7 +75,7 @@ EXPORTED = [
     "ipo_hip_ctx_create", "ipo_hip_ctx_run", "ipo_hip_ctx_download", "ipo_hip_ctx_destroy",
     "ipo_hip_ctx_setup_seconds", "ipo_hip_kkt_set_epsdiag",
     "ipo_hip_synth_random", "ipo_hip_synth_block_angular", "ipo_hip_symbolic_forced",
-    "ipo_hip_set_device", "ipo_hip_rccl_unique_id", "ipo_hip_ctx_create_shard",
+    "ipo_hip_set_device", "ipo_hip_rccl_unique_id", "ipo_hip_ctx_create_shard", "ipo_hip_vector_bench",
 ]
 
 # int (*)(void *user, double *buf, long n, int op)  -- ipo_hip_allreduce_fn
@@ -140,6 +140,8 @@ def lib() -> C.CDLL:
     L.ipo_hip_ctx_destroy.restype = None
     L.ipo_hip_ctx_setup_seconds.argtypes = [_P]
     L.ipo_hip_ctx_setup_seconds.restype = _D
+    L.ipo_hip_vector_bench.argtypes = [_I, _I, _P, _P, _P, _I, _P, _P]
+    L.ipo_hip_vector_bench.restype = _I
     L.ipo_hip_synth_random.argtypes = [_I, _I, _I, _I, C.c_ulonglong, C.POINTER(_I)] + [_P] * 9
     L.ipo_hip_synth_random.restype = _I
     L.ipo_hip_synth_block_angular.argtypes = [_I] * 7 + [C.c_ulonglong] + [C.POINTER(_I)] * 3 + [_P] * 9
@@ -500,6 +502,22 @@ def synth_random(m, n, per_col=4, band=0, seed=SYNTH_SEED) -> SynthProblem:
     if L.ipo_hip_synth_random(m, n, per_col, band, seed, C.byref(nz), *[_ptr(a) for a in arrs]):
         raise IpoHipError("synth_random: " + last_error())
     return SynthProblem(m, n, kA, iA, A, b, c, 0.0, xs, ys, ws, zs)
+
+
+VECTOR_KERNELS = ("k_hsd_residuals", "k_hsd_directions", "k_step")
+
+
+def vector_bench(p, reps=20) -> dict:
+    """Time the HBM-bound HSD vector kernels alone on LP p (device-resident
+    inputs): {kernel: (ms per launch, algorithmic bytes per launch)}."""
+    require_gpu()
+    ms, by = np.zeros(3), np.zeros(3)
+    kA = np.ascontiguousarray(p.kA, np.int32)
+    iA = np.ascontiguousarray(p.iA, np.int32)
+    A = np.ascontiguousarray(p.A, np.float64)
+    if lib().ipo_hip_vector_bench(p.m, p.n, _ptr(kA), _ptr(iA), _ptr(A), reps, _ptr(ms), _ptr(by)):
+        raise IpoHipError("vector_bench: " + last_error())
+    return {k: (float(ms[i]), float(by[i])) for i, k in enumerate(VECTOR_KERNELS)}
 
 
 def synth_block_angular(nblocks=8, mb=25000, nb=100000, per_col=4, band=256, nlink=512, link_nz=2000,
