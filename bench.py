@@ -54,7 +54,7 @@ METRIC = "IPM iterations/sec (ADA^T factor+solve) on netlib dfl001; duality gap 
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, AMD spec (the guide has no fp64 row)
 PHASE_KERNELS = {"gather": "k_update+k_update_reduce",
                  "diag": "k_panel_w|k_panel_s|k_tail_pr|k_panel|k_diag|k_tail_diag_coop", "trsm": "k_trsm",
-                 "tail_syrk": "k_tail_urgent|k_tail_syrk",
+                 "tail_syrk": "k_tail_syrk",
                  "forward": "k_forward|k_fwd_diag|k_fwd_gemv|k_fwd_sf|k_tail_gather|k_tail_fwd|k_tail_fwd_chain",
                  "backward": "k_backward|k_bwd_partial|k_bwd_finish|k_bwd_sf|k_tail_dscale|k_tail_bwd|k_tail_bwd_chain"}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak, MI355X_MICROARCH.md

@@ -695,88 +695,125 @@ __device__ __forceinline__ void win_row(const double* __restrict__ row, double (
 // block: no per-column guard, so a window is one basic block the compiler
 // can schedule across -- the next step's pivot chain in the shadow of the
 // previous step's updates) and a guarded form for the last, partial window.
-// Window factorisation (half 0, wave t): every cross-lane value by v_readlane.
+// Progress counters of the windows (LDS): a wave publishes how many columns
+// of its window it has written (Ct / Lr / Lb / dv), the waves that apply or
+// solve against that window wait for the column they need -- a dataflow
+// between the waves instead of one workgroup barrier per window.  One wave's
+// LDS operations execute in issue order, so data stored before a count is
+// visible to a wave that has read the count; the wavefront fences only keep
+// the compiler from moving LDS accesses across the count.
+__device__ __forceinline__ void df_publish(int* prog, int v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __hip_atomic_store(prog, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void df_wait(const int* prog, int v, int& seen) {
+    if (seen < v) {
+        int x;
+        while ((x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(prog, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_WORKGROUP))) < v)
+            __builtin_amdgcn_s_sleep(1);
+        seen = x;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Window factorisation (half 0, wave w): every cross-lane value by
+// v_readlane; column i of the window is published after its pivot step.
+// Software-pipelined: step i forms pivot i + 1 (its column updated first,
+// by v_readlane) before the rest of its updates, so the division of the next
+// pivot issues interleaved with them instead of after them.
 template <bool FULL>
 __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& tz_any, int cw0, int nc, int lane,
-                                           int h0, double tau, double (*Ct)[CTS], double (*Lr)[PC], double* dv) {
+                                           int h0, double tau, double (*Ct)[CTS], double (*Lr)[PC], double* dv,
+                                           int* prog) {
+    double dk = lane_bcast(a[0], cw0);
+    tz_any |= fabs(dk) <= tau * lane_bcast(dsc, cw0);   // no short-circuit: no branch
+    double l = lane > cw0 && lane < h0 ? a[0] / dk : 0.0;
 #pragma unroll
     for (int i = 0; i < WIN; i++) {
         const int k = cw0 + i;
         if (FULL || k < nc) {
-            const double dk = lane_bcast(a[i], k);
-            const double dsk = lane_bcast(dsc, k);
-            tz_any = tz_any || fabs(dk) <= tau * dsk;
             const bool below = lane > k && lane < h0;
-            const double l = below ? a[i] / dk : 0.0;
             a[i] = below ? l : a[i];
             const double c = l * dk;
             Ct[k][lane] = c;
             Lr[k][lane] = l;
             dv[k] = dk;                   // every lane stores the same value: no EXEC branch
-            dsc = dsc + fabs(l * c);
-            // column k + 1 (the next pivot's) by v_readlane, the rest of the
-            // window from the LDS row just written: a wavefront fence orders
-            // the reads after the write for the compiler (the LDS runs one
-            // wave's operations in issue order) without pinning the ALU work,
-            // so the next pivot chain can start under the read latency
-            if (i + 1 < WIN) a[i + 1] = a[i + 1] - l * lane_bcast(c, cw0 + i + 1);
+            // the wavefront fence orders the reads of the row just written
+            // (and the published count) after the writes for the compiler;
+            // the LDS runs one wave's operations in issue order
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            if (i + 2 < WIN) {
-                double cc[WIN];
-                win_row(&Ct[k][cw0], cc);
-#pragma unroll
-                for (int q = i + 2; q < WIN; q++) a[q] = a[q] - l * cc[q];
+            __hip_atomic_store(prog, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            dsc = dsc + fabs(l * c);
+            double cc[WIN];
+            if (i + 2 < WIN) win_row(&Ct[k][cw0], cc);
+            const double lk = l;
+            if (i + 1 < WIN && (FULL || k + 1 < nc)) {
+                // pivot k + 1: its column by v_readlane, then l of the next step
+                a[i + 1] = a[i + 1] - lk * lane_bcast(c, k + 1);
+                dk = lane_bcast(a[i + 1], k + 1);
+                tz_any |= fabs(dk) <= tau * lane_bcast(dsc, k + 1);
+                l = lane > k + 1 && lane < h0 ? a[i + 1] / dk : 0.0;
             }
+#pragma unroll
+            for (int q = i + 2; q < WIN; q++) a[q] = a[q] - lk * cc[q];
         }
     }
 }
 
-// Rank-1 updates k = kw .. min(kw + 16, k1) - 1 of another window, in k
+// Rank-1 updates k = kw .. kw + 15 of an earlier (always full) window, in k
 // order, on this wave's 16 columns (L = Lr for block rows, Lb for tile rows;
-// DSC: also the |terms| of the diagonal entries this wave owns).
-template <bool FULL, bool DSC>
-__device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw, int k1, int lane, int cw0,
-                                          double (*Ct)[CTS], double (*L)[PC]) {
+// DSC: also the |terms| of the diagonal entries this wave owns), each as soon
+// as the window's owner has published column k.  (The 16 column multipliers
+// come as one broadcast LDS row: by v_readlane from the lanes holding them
+// the updates ran at half the speed.)
+template <bool DSC>
+__device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw, int lane, int cw0,
+                                          double (*Ct)[CTS], double (*L)[PC], const int* prog) {
     // software-pipelined: step i + 1's LDS operands are read before step i's
     // arithmetic, so the read latency hides under the updates
-    double l = 0.0, ck = 0.0, cc[WIN];
-    if (FULL || kw < k1) {
-        l = L[kw][lane];
-        if (DSC) ck = Ct[kw][lane];
-        win_row(&Ct[kw][cw0], cc);
-    }
-#pragma unroll
+    int seen = 0;
+    double l, ck = 0.0, cc[WIN];
+    df_wait(prog, 1, seen);
+    l = L[kw][lane];
+    if (DSC) ck = Ct[kw][lane];
+    win_row(&Ct[kw][cw0], cc);
+#pragma unroll 2
     for (int i = 0; i < WIN; i++) {
         const int k = kw + i;
-        if (FULL || k < k1) {
-            double ln = 0.0, ckn = 0.0, cn[WIN];
-            if (i + 1 < WIN && (FULL || k + 1 < k1)) {
-                ln = L[k + 1][lane];
-                if (DSC) ckn = Ct[k + 1][lane];
-                win_row(&Ct[k + 1][cw0], cn);
-            }
-#pragma unroll
-            for (int q = 0; q < WIN; q++) a[q] = a[q] - l * cc[q];
-            if (DSC) dsc = dsc + fabs(l * ck);
-            l = ln;
-            ck = ckn;
-#pragma unroll
-            for (int q = 0; q < WIN; q++) cc[q] = cn[q];
+        double ln = 0.0, ckn = 0.0, cn[WIN];
+        if (i + 1 < WIN) {
+            df_wait(prog, i + 2, seen);
+            ln = L[k + 1][lane];
+            if (DSC) ckn = Ct[k + 1][lane];
+            win_row(&Ct[k + 1][cw0], cn);
         }
+#pragma unroll
+        for (int q = 0; q < WIN; q++) a[q] = a[q] - l * cc[q];
+        if (DSC) dsc = dsc + fabs(l * ck);
+        l = ln;
+        ck = ckn;
+#pragma unroll
+        for (int q = 0; q < WIN; q++) cc[q] = cn[q];
     }
 }
 
-// Window solve of the tile rows (half 1, wave t - 1): solve_rows' form.
+// Window solve of the tile rows (half 1, wave w): solve_rows' form, step i
+// once half 0 has published pivot i of the window (wprog); publishes Lb.
 template <bool FULL>
 __device__ __forceinline__ void win_solve(double (&a)[WIN], int cw0, int nc, bool rok, int lane, double (*Ct)[CTS],
-                                          double (*Lb)[PC], const double* dv) {
+                                          double (*Lb)[PC], const double* dv, const int* wprog, int* prog) {
+    int seen = 0;
 #pragma unroll
     for (int i = 0; i < WIN; i++) {
         const int k = cw0 + i;
         if (FULL || k < nc) {
+            df_wait(wprog, i + 1, seen);
             const double l = rok ? a[i] / dv[k] : 0.0;
             a[i] = l;
             Lb[k][lane] = l;
+            df_publish(prog, i + 1);
             double cc[WIN];
             win_row(&Ct[k][cw0], cc);
 #pragma unroll
@@ -785,6 +822,18 @@ __device__ __forceinline__ void win_solve(double (&a)[WIN], int cw0, int nc, boo
     }
 }
 
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+// Dense-tail panels of the look-ahead factorisation first apply block
+// column t - 1's update to their own rows (the diagonal block and tile j +
+// 1), the way k_tail_syrk would: operands staged here, products (old - acc
+// is formed by the panel on its loaded values) left in Ad / Aj as [row][col].
+struct PreLds {
+    double Ad[TR][PC + 1];
+    double Aj[TR][PC + 1];
+    double Bs[TR][PC + 1];
+};
+
 // LDS image of the windowed panel (one raw buffer, so a kernel can share it
 // with the trailing-update tiles below)
 struct PanelLds {
@@ -792,6 +841,7 @@ struct PanelLds {
     double Lr[PC][PC];
     double Lb[PC][PC];
     double dv[PC];
+    int prog[8];                          // published columns: windows of half 0, then of half 1
     int tiny;
 };
 
@@ -800,7 +850,7 @@ struct PanelLds {
 // goes to wtail.
 __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __restrict__ fu_sup,
                                              const int* __restrict__ fu_j, int f0, const TailView& tv, int kb, int bid,
-                                             PanelLds& S, double* wtail) {
+                                             PanelLds& S, double* wtail, const double* __restrict__ wpre = nullptr) {
     double (*Ct)[CTS] = S.Ct;
     double (*Lr)[PC] = S.Lr;
     double (*Lb)[PC] = S.Lb;
@@ -830,7 +880,9 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     PANEL_STAMP(15);
     const bool h1 = wv >= 4;
-    const int w = wv & 3, cw0 = WIN * w;
+    // half 1 takes the windows in the order 2 3 0 1, so the waves sharing a
+    // SIMD (wv, wv + 4) never both own the last window's long chain
+    const int w = h1 ? (wv + 2) & 3 : wv, cw0 = WIN * w;
     const int h0 = min(PC, h);
     const int row = h1 ? TR * (j + 1) + lane : lane;
     const bool rok = h1 ? row < h : row < h0;
@@ -846,72 +898,149 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     }
     // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
     double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
-    if (tid == 0) tiny_sh = 0;
-    PANEL_STAMP(0);
-    const int nph = tile ? nwin + 1 : nwin;
-    for (int t = 0; t < nph; t++) {
+    if (wpre) {
+        // dense tail, block column kb > 0: block kb - 1's update of this
+        // workgroup's rows, k_tail_syrk's MFMA fragments and order; the
+        // entries get old - acc and the pivots' |terms| old + sum_k |l w|,
+        // the operations of k_tail_syrk's tile, without a launch of its own
+        PreLds& P = *reinterpret_cast<PreLds*>(&S);
+        const int nt = tv.nt, kp = (kb - 1) * PC;
+        const double* Lcol = tv.S + (size_t)kp * nt;
+        constexpr int NU = TR * PC / PNT;
+        {
+            // all 3 NU loads in flight, then into LDS
+            double vd[NU], vj[NU], vw[NU];
+            const int rr = tid % TR, rd = kb * TR + rr, rj = (kb + j + 1) * TR + rr;
+            const bool okd = rd < nt, okj = rj < nt;
+#pragma unroll
+            for (int u = 0; u < NU; u++) {
+                const int k = (tid + u * PNT) / TR;
+                const double x = Lcol[okd ? rd + (size_t)k * nt : 0];
+                const double y = Lcol[okj ? rj + (size_t)k * nt : 0];
+                const double z = wpre[okd ? (rd - kp) + (size_t)k * nt : 0];
+                vd[u] = okd ? x : 0.0;
+                vj[u] = okj ? y : 0.0;
+                vw[u] = okd ? z : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < NU; u++) {
+                const int k = (tid + u * PNT) / TR;
+                P.Ad[rr][k] = vd[u];
+                P.Aj[rr][k] = vj[u];
+                P.Bs[rr][k] = vw[u];
+            }
+        }
         __syncthreads();
-        PANEL_STAMP(1 + 2 * t);
-        if (tiny_sh) break;
+        double asum = 0.0;
+        if (!h1 && lane < nc && (lane >> 4) == w)
+            for (int k = 0; k < PC; k++) asum += fabs(P.Ad[lane][k] * P.Bs[lane][k]);
+        const int wr = (w & 1) * 32, wc = (w >> 1) * 32, li = lane & 15, lk = lane >> 4;
+        double (*Am)[PC + 1] = h1 ? P.Aj : P.Ad;
+        double4_t acc[2][2];
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++) acc[x][y] = (double4_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < PC; kk += 4) {
+            double av[2], bv[2];
+#pragma unroll
+            for (int x = 0; x < 2; x++) av[x] = Am[wr + x * 16 + li][kk + lk];
+#pragma unroll
+            for (int y = 0; y < 2; y++) bv[y] = P.Bs[wc + y * 16 + li][kk + lk];
+#pragma unroll
+            for (int x = 0; x < 2; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+        }
+        __syncthreads();                   // every operand read: Ad / Aj take the products
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++)
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    Am[wr + x * 16 + (lane >> 4) + 4 * i][wc + y * 16 + (lane & 15)] = acc[x][y][i];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            if (rok && c < nc && (h1 || c <= row)) a[q] = a[q] - Am[lane][c];
+        }
+        dsc = dsc + asum;
+        if (!h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc;
+        __syncthreads();                   // the panel's LDS image overwrites P from here
+    }
+    if (tid < 8) S.prog[tid] = 0;
+    if (tid == 0) tiny_sh = 0;
+    __syncthreads();
+    PANEL_STAMP(0);
+    // half 0, wave w: updates of windows 0 .. w - 1, then factor window w;
+    // half 1, wave w: the same updates on the tile rows, then solve window w.
+    // Issue priority: the window chains (factor, solve) and the updates that
+    // gate them over the rest.
+#ifndef IPO_EXP_NOH1
+#define IPO_EXP_NOH1 0
+#endif
+    if (w < nwin && (!h1 || (tile && !IPO_EXP_NOH1))) {
+        int* const prog = S.prog + (h1 ? 4 : 0);
+        double unused = 0.0;
+        for (int t = 0; t < w; t++) {
+            // the updates of window w - 1 gate this wave's own chain
+            if (t + 1 < w) {
+                if (h1) __builtin_amdgcn_s_setprio(0);
+                else __builtin_amdgcn_s_setprio(1);
+            } else {
+                if (h1) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(3);
+            }
+            if (!h1) win_apply<true>(a, dsc, WIN * t, lane, cw0, Ct, Lr, prog + t);
+            else win_apply<false>(a, unused, WIN * t, lane, cw0, Ct, Lb, prog + t);
+        }
+        PANEL_STAMP(1);
         if (!h1) {
-            if (w >= t && w < nwin) {
-                if (t > 0) {      // updates of window t - 1, k in order
-                    const int kw = WIN * (t - 1), k1 = min(WIN * t, nc);
-                    if (k1 - kw == WIN) win_apply<true, true>(a, dsc, kw, k1, lane, cw0, Ct, Lr);
-                    else win_apply<false, true>(a, dsc, kw, k1, lane, cw0, Ct, Lr);
+            bool tz_any = false;
+            __builtin_amdgcn_s_setprio(3);
+            if (cw0 + WIN <= nc) win_factor<true>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv, prog + w);
+            else win_factor<false>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv, prog + w);
+            if (tz_any && lane == 0) tiny_sh = 1;
+        } else {
+            __builtin_amdgcn_s_setprio(3);
+            if (cw0 + WIN <= nc) win_solve<true>(a, cw0, nc, rok, lane, Ct, Lb, dv, S.prog + w, prog + w);
+            else win_solve<false>(a, cw0, nc, rok, lane, Ct, Lb, dv, S.prog + w, prog + w);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        PANEL_STAMP(2);
+        // this wave's rows out as soon as its window is done (a panel that
+        // bails is redone from the assembly on, so what it wrote is moot):
+        // half 1 its rows of L21 (and W = L21 D on the dense tail), half 0 of
+        // workgroup 0 the rows of R_s inside the first 64 rows
+        if (h1 ? rok : (j == 0 && lane >= nc && lane < h0)) {
+            double dw[WIN];
+            win_row(&dv[cw0], dw);        // one LDS round trip, not one per column
+#pragma unroll
+            for (int q = 0; q < WIN; q++) {
+                const int c = cw0 + q;
+                if (c < nc) {
+                    panel[row + (size_t)c * ld] = a[q];
+                    if (wbuf) wbuf[row + (size_t)c * ld] = a[q] * dw[q];
                 }
-                PANEL_STAMP(2 + 2 * t);
-                if (w == t) {     // factor window t
-                    bool tz_any = false;
-                    if (cw0 + WIN <= nc) win_factor<true>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv);
-                    else win_factor<false>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv);
-                    if (tz_any && lane == 0) tiny_sh = 1;
-                }
-            }
-        } else if (t >= 1 && w >= t - 1 && w < nwin) {
-            if (t > 1) {          // tile updates of window t - 2, k in order
-                const int kw = WIN * (t - 2), k1 = min(WIN * (t - 1), nc);
-                double unused = 0.0;
-                if (k1 - kw == WIN) win_apply<true, false>(a, unused, kw, k1, lane, cw0, Ct, Lb);
-                else win_apply<false, false>(a, unused, kw, k1, lane, cw0, Ct, Lb);
-            }
-            PANEL_STAMP(2 + 2 * t);
-            if (w == t - 1) {     // solve window t - 1 of the tile rows
-                if (cw0 + WIN <= nc) win_solve<true>(a, cw0, nc, rok, lane, Ct, Lb, dv);
-                else win_solve<false>(a, cw0, nc, rok, lane, Ct, Lb, dv);
             }
         }
     }
-    __syncthreads();
+    // LDS-only barrier: the global stores above need not drain first
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     PANEL_STAMP(12);
     if (tiny_sh) {
         if (tid == 0) atomicOr(&p.flags[1], fu_sup ? 2 : 4);   // bit: where it bailed (host statistics)
         return;
     }
-    // half 1: its rows of L21 (and W = L21 D on the dense tail)
-    if (h1 && rok) {
-#pragma unroll
-        for (int q = 0; q < WIN; q++) {
-            const int c = cw0 + q;
-            if (c < nc) {
-                panel[row + (size_t)c * ld] = a[q];
-                if (wbuf) wbuf[row + (size_t)c * ld] = a[q] * dv[c];
-            }
-        }
-    }
     if (j != 0) return;
-    // workgroup 0, half 0: rows of R_s inside the first 64 rows, then L11'
-    // into the upper slot through an LDS transpose (Ct is free again), D, mark
-    if (!h1 && lane >= nc && lane < h0) {
-#pragma unroll
-        for (int q = 0; q < WIN; q++) {
-            const int c = cw0 + q;
-            if (c < nc) {
-                panel[lane + (size_t)c * ld] = a[q];
-                if (wbuf) wbuf[lane + (size_t)c * ld] = a[q] * dv[c];
-            }
-        }
-    }
+    // workgroup 0: L11' into the upper slot through an LDS transpose (Ct is
+    // free again), D, mark
     if (!h1) {
 #pragma unroll
         for (int q = 0; q < WIN; q++) Ct[lane][cw0 + q] = a[q];
@@ -936,7 +1065,6 @@ k_panel_w(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu
 // k_tail_syrk (bitwise the same update); wave w owns rows 32 (w & 1) ..
 // + 31, columns 16 (w >> 1) .. + 15.  On a diagonal tile the |terms| go to
 // dscale as k_tail_syrk adds them.
-typedef double double4_t __attribute__((ext_vector_type(4)));
 
 struct SyrkLds {
     double As[TR][PC + 1];
@@ -1011,37 +1139,33 @@ __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& 
     }
 }
 
-constexpr size_t kTailStepLds = sizeof(PanelLds) > sizeof(SyrkLds) ? sizeof(PanelLds) : sizeof(SyrkLds);
+constexpr size_t kTailStepLds0 = sizeof(PanelLds) > sizeof(SyrkLds) ? sizeof(PanelLds) : sizeof(SyrkLds);
+constexpr size_t kTailStepLds = kTailStepLds0 > sizeof(PreLds) ? kTailStepLds0 : sizeof(PreLds);
 
 // Step t of the look-ahead dense-tail factorisation, one launch:
 //   workgroups [0, gp):  panel of block column t (k_panel_w's body), its
 //                        W = L21 D into Wcur;
 //   the rest:            R(t - 1), the update of block column t - 1 on the
 //                        columns right of t: tiles (bi, bj), bj >= t + 1.
-// Block column t already holds every update from blocks < t: those of
-// blocks <= t - 2 from earlier R launches, that of block t - 1 from
-// k_tail_urgent(t - 1) right before this launch -- so the big trailing
-// update runs beside the panel instead of between two panels, and every
-// entry still receives the updates of blocks 0, 1, ... in order (bitwise
-// the factor of panel + k_tail_syrk).  W is double-buffered by parity: R
-// reads block t - 1's while the panel writes block t's.
+// Block column t holds every update from blocks <= t - 2 (earlier R
+// launches); the panel workgroups apply block t - 1's to their own rows
+// first (panel_w_body's pre-update, k_tail_syrk's fragments and order) -- so
+// one launch per block column, the big trailing update beside the panel,
+// and every entry still receives the updates of blocks 0, 1, ... in order
+// (bitwise the factor of panel + k_tail_syrk).  W is double-buffered by
+// parity: the pre-update and R read block t - 1's while the panel writes
+// block t's.
 __global__ void __launch_bounds__(PNT)
 k_tail_pr(PlanView p, TailView tv, int t, int gp, const double* __restrict__ Wprev, double* __restrict__ Wcur) {
     __shared__ __attribute__((aligned(16))) char lds[kTailStepLds];
     if ((int)blockIdx.x < gp) {
-        panel_w_body(p, nullptr, nullptr, 0, tv, t, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), Wcur);
+        panel_w_body(p, nullptr, nullptr, 0, tv, t, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), Wcur,
+                     t > 0 ? Wprev : nullptr);
         return;
     }
     int tile = blockIdx.x - gp, bj = t + 1;
     while (tile >= tv.ntb - bj) { tile -= tv.ntb - bj; bj++; }
     syrk_tile512(p, tv, t - 1, bj + tile, bj, Wprev, *reinterpret_cast<SyrkLds*>(lds));
-}
-
-// U(t): block t's update of block column t + 1 only (tiles (bi, t + 1))
-__global__ void __launch_bounds__(PNT)
-k_tail_urgent(PlanView p, TailView tv, int t, const double* __restrict__ W) {
-    __shared__ __attribute__((aligned(16))) char lds[sizeof(SyrkLds)];
-    syrk_tile512(p, tv, t, t + 1 + blockIdx.x, t + 1, W, *reinterpret_cast<SyrkLds*>(lds));
 }
 
 // ------------------------------------------------------- small panels
@@ -1115,10 +1239,6 @@ void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const doubl
     const int gp = std::max(1, (h + TR - 1) / TR - 1);
     const int nr = t > 0 ? (tv.ntb - t - 1) * (tv.ntb - t) / 2 : 0;
     hipLaunchKernelGGL(k_tail_pr, dim3(gp + nr), dim3(PNT), 0, s, pv, tv, t, gp, Wprev, Wcur);
-}
-
-void launch_tail_urgent(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s) {
-    if (tv.ntb - t - 1 > 0) hipLaunchKernelGGL(k_tail_urgent, dim3(tv.ntb - t - 1), dim3(PNT), 0, s, pv, tv, t, W);
 }
 
 bool launch_tail_diag_coop(const PlanView& pv, const TailView& tv, int kb, double* gmax, int* gctr, hipStream_t s) {

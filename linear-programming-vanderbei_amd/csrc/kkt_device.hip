@@ -2303,11 +2303,6 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
                 ph_begin(s);
                 launch_tail_step(pv, tv, t, dW_.get() + ((t + 1) & 1) * wst, wc, s);
                 ph_end(kPhDiag, 1, s);
-                if (t + 1 < plan_.ntb) {
-                    ph_begin(s);
-                    launch_tail_urgent(pv, tv, t, wc, s);
-                    ph_end(kPhSyrk, 1, s);
-                }
             }
         } else
         for (int kb = 0; kb < plan_.ntb; kb++) {

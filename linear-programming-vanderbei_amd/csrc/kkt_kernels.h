@@ -61,12 +61,11 @@ void launch_trsm(const PlanView& pv, int u0, int count, const TailView& tv, int 
 void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,
                   int kb, hipStream_t s);
 // Look-ahead dense tail (fused path with k_panel_w): step t = panel of block
-// column t beside the trailing update of block t - 1 on columns > t (one
-// launch, W of block t into Wcur, block t - 1's read from Wprev), then
-// launch_tail_urgent(t): block t's update of block column t + 1.
+// column t (which first applies block t - 1's update to its own rows) beside
+// the trailing update of block t - 1 on columns > t -- one launch per block
+// column, W of block t into Wcur, block t - 1's read from Wprev.
 void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const double* Wprev, double* Wcur,
                       hipStream_t s);
-void launch_tail_urgent(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s);
 // Redo path: diagonal block + rows below of dense-tail block column kb with
 // the dependent-pivot rule, one cooperative launch (k_tail_diag_coop);
 // gmax: one double per 64-row tile, gctr: grid-barrier counter (cleared here).

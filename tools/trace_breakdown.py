@@ -2,7 +2,8 @@
 
 Splits every IPM iteration (one k_assemble_A each) into the sparse levels of
 the factorisation, the dense tail of the factorisation (after the last
-k_update* launch before the first k_tail_syrk, up to k_min_abs_partial) and
+k_update* launch before the first k_tail_syrk, or from the first k_tail_pr,
+up to k_min_abs_partial) and
 the rest (solves, vector kernels), and prints per region and kernel the
 launches and device time per iteration, plus the summed gaps between
 consecutive dispatches.
@@ -46,13 +47,14 @@ def main():
     acc = defaultdict(lambda: [0, 0.0])
     gaps, span = 0.0, 0.0
     for it in its:
-        first_syrk = next((i for i, r in enumerate(it) if r[2] in ("k_tail_syrk", "k_tail_urgent")), None)
+        first_syrk = next((i for i, r in enumerate(it) if r[2] == "k_tail_syrk"), None)
+        first_pr = next((i for i, r in enumerate(it) if r[2] == "k_tail_pr"), None)
         t1 = next((i for i, r in enumerate(it) if r[2] == "k_min_abs_partial"), len(it))
         t0 = t1
-        if first_syrk is not None:
+        if first_pr is not None:                         # look-ahead tail: starts at its first step
+            t0 = first_pr
+        elif first_syrk is not None:
             t0 = max(i for i in range(first_syrk) if it[i][2].startswith("k_update")) + 1
-            if it[first_syrk][2] == "k_tail_urgent":     # look-ahead tail: starts at its first step
-                t0 = next(i for i in range(first_syrk) if it[i][2] == "k_tail_pr")
         for i, (s, e, k, g) in enumerate(it):
             region = "factor-sparse" if i < t0 else ("factor-tail" if i < t1 else "solve+vec")
             a = acc[(region, k)]

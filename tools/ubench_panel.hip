@@ -69,11 +69,11 @@ int main(int argc, char** argv) {
 #ifdef IPO_PANEL_STAMPS
     long long st[8][16];
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(ipo::g_stamps), sizeof(st)));
-    std::printf("k_panel_w workgroup 0 stamps (cycles since wave 0 entry); slots: 15 entry, 0 loaded, 2t+1 phase t start, 2t+2 after updates, 12 end, 13 done\n");
+    std::printf("k_panel_w workgroup 0 stamps (cycles since wave 0 entry); slots: 15 entry, 0 loaded, 1 after updates, 2 window done, 12 end, 13 done\n");
     const long long b = st[0][15];
     for (int w = 0; w < 8; w++) {
         std::printf("wave %d:", w);
-        for (int sl : {15, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13}) std::printf(" %d:%lld", sl, st[w][sl] - b);
+        for (int sl : {15, 0, 1, 2, 12, 13}) std::printf(" %d:%lld", sl, st[w][sl] - b);
         std::printf("\n");
     }
 #endif
