@@ -828,10 +828,13 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 // column t - 1's update to their own rows (the diagonal block and tile j +
 // 1), the way k_tail_syrk would: operands staged here, products (old - acc
 // is formed by the panel on its loaded values) left in Ad / Aj as [row][col].
+// Row stride 66: the MFMA operand reads (16 rows x 4 k per wave) hit at
+// most two lanes per bank, a 16-lane column of one k none.
+constexpr int PRS = PC + 2;
 struct PreLds {
-    double Ad[TR][PC + 1];
-    double Aj[TR][PC + 1];
-    double Bs[TR][PC + 1];
+    double Ad[TR][PRS];
+    double Aj[TR][PRS];
+    double Bs[TR][PRS];
 };
 
 // LDS image of the windowed panel (one raw buffer, so a kernel can share it
@@ -931,11 +934,13 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
             }
         }
         __syncthreads();
+        PANEL_STAMP(3);
+        // |terms| of the pivots (half 0, the wave's 16 diagonal rows), k in
+        // order, interleaved with the MFMA steps that read the same k
+        const bool holder = !h1 && lane < nc && (lane >> 4) == w;
         double asum = 0.0;
-        if (!h1 && lane < nc && (lane >> 4) == w)
-            for (int k = 0; k < PC; k++) asum += fabs(P.Ad[lane][k] * P.Bs[lane][k]);
         const int wr = (w & 1) * 32, wc = (w >> 1) * 32, li = lane & 15, lk = lane >> 4;
-        double (*Am)[PC + 1] = h1 ? P.Aj : P.Ad;
+        double (*Am)[PRS] = h1 ? P.Aj : P.Ad;
         double4_t acc[2][2];
 #pragma unroll
         for (int x = 0; x < 2; x++)
@@ -953,24 +958,30 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
 #pragma unroll
                 for (int y = 0; y < 2; y++)
                     acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+            if (holder) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) asum += fabs(P.Ad[lane][kk + u] * P.Bs[lane][kk + u]);
+            }
         }
-        __syncthreads();                   // every operand read: Ad / Aj take the products
+        PANEL_STAMP(4);
+        __syncthreads();                   // every operand read: Ad / Aj take the products, [col][row]
 #pragma unroll
         for (int x = 0; x < 2; x++)
 #pragma unroll
             for (int y = 0; y < 2; y++)
 #pragma unroll
                 for (int i = 0; i < 4; i++)
-                    Am[wr + x * 16 + (lane >> 4) + 4 * i][wc + y * 16 + (lane & 15)] = acc[x][y][i];
+                    Am[wc + y * 16 + (lane & 15)][wr + x * 16 + (lane >> 4) + 4 * i] = acc[x][y][i];
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < WIN; q++) {
             const int c = cw0 + q;
-            if (rok && c < nc && (h1 || c <= row)) a[q] = a[q] - Am[lane][c];
+            if (rok && c < nc && (h1 || c <= row)) a[q] = a[q] - Am[c][lane];
         }
         dsc = dsc + asum;
         if (!h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc;
         __syncthreads();                   // the panel's LDS image overwrites P from here
+        PANEL_STAMP(14);
     }
     if (tid < 8) S.prog[tid] = 0;
     if (tid == 0) tiny_sh = 0;

@@ -1,0 +1,101 @@
+// Host-only statistics of the factor plan (developer tool): gather work of
+// the dense-tail tiles and of the sparse units -- slots (k columns), the
+// useful multiply-adds (popcount(rmask) x popcount(cmask) per slot) against
+// the 64 x 64 per slot an MFMA tile performs.
+//   g++ -O2 -std=c++17 -I linear-programming-vanderbei_amd/csrc tools/plan_stats.cpp \
+//       linear-programming-vanderbei_amd/csrc/kkt_symbolic.cpp linear-programming-vanderbei_amd/csrc/lp_io.cpp \
+//       -o tools/plan_stats && tools/plan_stats tests/golden/netlib/dfl001.mps.gz
+#include <cstdio>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+#include "kkt_plan.h"
+#include "lp_io.h"
+
+using namespace ipo;
+
+int main(int argc, char** argv) {
+    MpsProblem mp;
+    std::string err;
+    if (read_mps(argv[1], mp, &err)) { std::printf("read: %s\n", err.c_str()); return 1; }
+    SolverForm sf;
+    to_solver_form(mp, sf);
+    std::vector<int> kAt, iAt;
+    std::vector<double> At;
+    csc_transpose(sf.m, sf.n, sf.kA.data(), sf.iA.data(), sf.A.data(), kAt, iAt, At);
+    KktPlan P = build_kkt_plan(sf.m, sf.n, sf.kA.data(), sf.iA.data(), kAt.data(), iAt.data());
+    std::printf("m %d n %d T %d nsup %d levels %d nt %d ntb %d\n", P.m, P.n, P.T, P.nsup, P.nlevels, P.nt, P.ntb);
+    // tail tiles
+    const int ntile = P.ntb * (P.ntb + 1) / 2;
+    long slots = 0, pad = 0, tasks = 0;
+    double useful = 0, mfma = 0;
+    std::vector<int> tslots(ntile);
+    for (int u = 0; u < ntile; u++) {
+        for (int i = P.tail_kslot_ptr[u]; i < P.tail_kslot_ptr[u + 1]; i++) {
+            const int sl = P.tail_kslot[i];
+            mfma += 64.0 * 64.0;
+            if (sl < 0) { pad++; continue; }
+            slots++;
+            tslots[u]++;
+            const TailTask& t = P.tail_tasks[sl >> 6];
+            useful += (double)__builtin_popcountll(t.rmask) * __builtin_popcountll(t.cmask);
+        }
+        tasks += P.tail_task_ptr[u + 1] - P.tail_task_ptr[u];
+    }
+    // MFMA fragments (16 x 16 outputs, 4 slots) that see a non-zero product
+    long frag_all = 0, frag_need = 0, frag_need_sorted = 0;
+    for (int u = 0; u < ntile; u++) {
+        std::vector<std::pair<int, int>> sig;   // (rfrag bits, cfrag bits) per slot
+        for (int i = P.tail_kslot_ptr[u]; i < P.tail_kslot_ptr[u + 1]; i++) {
+            const int sl = P.tail_kslot[i];
+            int rf = 0, cf = 0;
+            if (sl >= 0) {
+                const TailTask& t = P.tail_tasks[sl >> 6];
+                for (int f = 0; f < 4; f++) {
+                    if ((t.rmask >> (16 * f)) & 0xffffull) rf |= 1 << f;
+                    if ((t.cmask >> (16 * f)) & 0xffffull) cf |= 1 << f;
+                }
+            }
+            sig.push_back({rf, cf});
+        }
+        auto count = [&](const std::vector<std::pair<int, int>>& v) {
+            long need = 0;
+            for (size_t g = 0; g + 4 <= v.size(); g += 4)
+                for (int fr = 0; fr < 4; fr++)
+                    for (int fc = 0; fc < 4; fc++) {
+                        bool nz = false;
+                        for (int q = 0; q < 4; q++) nz |= ((v[g + q].first >> fr) & 1) && ((v[g + q].second >> fc) & 1);
+                        need += nz;
+                    }
+            return need;
+        };
+        frag_all += (long)(sig.size() / 4) * 16;
+        frag_need += count(sig);
+        std::stable_sort(sig.begin(), sig.end());
+        frag_need_sorted += count(sig);
+    }
+    std::printf("tail MFMA fragments: %ld, non-zero %ld (%.1f%%), with slots sorted by fragment signature %ld (%.1f%%)\n",
+                frag_all, frag_need, 100.0 * frag_need / frag_all, frag_need_sorted, 100.0 * frag_need_sorted / frag_all);
+    std::sort(tslots.begin(), tslots.end());
+    std::printf("tail: tiles %d tasks %ld slots %ld pad %ld  useful MAC %.3g  MFMA MAC %.3g (%.1f%%)\n", ntile, tasks,
+                slots, pad, useful, mfma, 100.0 * useful / mfma);
+    std::printf("tail slots per tile: min %d median %d p90 %d max %d\n", tslots[0], tslots[ntile / 2],
+                tslots[ntile * 9 / 10], tslots[ntile - 1]);
+    // sparse units
+    const int nu = (int)P.unit_sup.size();
+    long us = 0, upad = 0;
+    double uuse = 0, umf = 0;
+    for (int u = 0; u < nu; u++)
+        for (int i = P.kslot_ptr[u]; i < P.kslot_ptr[u + 1]; i++) {
+            const int sl = P.kslot[i];
+            umf += 64.0 * 64.0;
+            if (sl < 0) { upad++; continue; }
+            us++;
+            const TailTask& t = P.utasks[sl >> 6];
+            uuse += (double)__builtin_popcountll(t.rmask) * __builtin_popcountll(t.cmask);
+        }
+    std::printf("sparse: units %d slots %ld pad %ld useful MAC %.3g MFMA MAC %.3g (%.1f%%)\n", nu, us, upad, uuse, umf,
+                100.0 * uuse / umf);
+    return 0;
+}

@@ -63,17 +63,36 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(out[kind].data(), dS, bytes, hipMemcpyDeviceToHost));
         std::printf("kind %d: %.2f us per launch (nt %d, kb %d, bail %d)\n", kind, 1e3 * tot / reps, nt, kb, fl[1]);
     }
+    if (kb > 0) {   // look-ahead step kb: panel kb (with block kb - 1's pre-update) beside R(kb - 1)
+        double* dW2;
+        CK(hipMalloc(&dW2, (size_t)nt * 64 * 8));
+        CK(hipMemset(dW2, 0, (size_t)nt * 64 * 8));
+        float tot = 0;
+        for (int r = 0; r < reps + 2; r++) {
+            CK(hipMemcpy(dS, dS0, bytes, hipMemcpyDeviceToDevice));
+            CK(hipMemset(dflags, 0, 16));
+            CK(hipDeviceSynchronize());
+            CK(hipEventRecord(e0, 0));
+            ipo::launch_tail_step(pv, tv, kb, dW2, dW, 0);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r >= 2) tot += ms;
+        }
+        std::printf("tail step %d: %.2f us per launch\n", kb, 1e3 * tot / reps);
+    }
     size_t diff = 0;
     for (size_t i = 0; i < out[1].size(); i++) diff += out[1][i] != out[2][i];
     std::printf("entries differing between kinds: %zu\n", diff);
 #ifdef IPO_PANEL_STAMPS
     long long st[8][16];
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(ipo::g_stamps), sizeof(st)));
-    std::printf("k_panel_w workgroup 0 stamps (cycles since wave 0 entry); slots: 15 entry, 0 loaded, 1 after updates, 2 window done, 12 end, 13 done\n");
+    std::printf("k_panel_w workgroup 0 stamps (cycles since wave 0 entry); slots: 15 entry, 3 pre-update operands in LDS, 4 products formed, 14 pre-update done, 0 loaded, 1 after updates, 2 window done, 12 end, 13 done\n");
     const long long b = st[0][15];
     for (int w = 0; w < 8; w++) {
         std::printf("wave %d:", w);
-        for (int sl : {15, 0, 1, 2, 12, 13}) std::printf(" %d:%lld", sl, st[w][sl] - b);
+        for (int sl : {15, 3, 4, 14, 0, 1, 2, 12, 13}) std::printf(" %d:%lld", sl, st[w][sl] - b);
         std::printf("\n");
     }
 #endif
