@@ -901,6 +901,7 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     }
     // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
     double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
+    double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
     if (wpre) {
         // dense tail, block column kb > 0: block kb - 1's update of this
         // workgroup's rows, k_tail_syrk's MFMA fragments and order; the
@@ -979,7 +980,7 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
             if (rok && c < nc && (h1 || c <= row)) a[q] = a[q] - Am[c][lane];
         }
         dsc = dsc + asum;
-        if (!h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc;
+        dsc_pre = dsc;
         __syncthreads();                   // the panel's LDS image overwrites P from here
         PANEL_STAMP(14);
     }
@@ -1023,10 +1024,13 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
         }
         __builtin_amdgcn_s_setprio(0);
         PANEL_STAMP(2);
-        // this wave's rows out as soon as its window is done (a panel that
-        // bails is redone from the assembly on, so what it wrote is moot):
-        // half 1 its rows of L21 (and W = L21 D on the dense tail), half 0 of
-        // workgroup 0 the rows of R_s inside the first 64 rows
+        // this wave's rows out as soon as its window is done: half 1 its
+        // rows of L21 (and W = L21 D on the dense tail), half 0 of workgroup
+        // 0 the rows of R_s inside the first 64 rows.  A sparse panel that
+        // bails is redone from the assembly on, so what it wrote is moot; a
+        // dense-tail panel that bails is resumed from its block column
+        // (KktDevice::repair_tail), so its rows of S wait for the check
+        // below (W is rewritten by the repair).
         if (h1 ? rok : (j == 0 && lane >= nc && lane < h0)) {
             double dw[WIN];
             win_row(&dv[cw0], dw);        // one LDS round trip, not one per column
@@ -1034,7 +1038,7 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
             for (int q = 0; q < WIN; q++) {
                 const int c = cw0 + q;
                 if (c < nc) {
-                    panel[row + (size_t)c * ld] = a[q];
+                    if (fu_sup) panel[row + (size_t)c * ld] = a[q];
                     if (wbuf) wbuf[row + (size_t)c * ld] = a[q] * dw[q];
                 }
             }
@@ -1046,8 +1050,21 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     PANEL_STAMP(12);
     if (tiny_sh) {
-        if (tid == 0) atomicOr(&p.flags[1], fu_sup ? 2 : 4);   // bit: where it bailed (host statistics)
+        if (tid == 0) {
+            atomicOr(&p.flags[1], fu_sup ? 2 : 4);   // bit: where it bailed
+            if (!fu_sup) atomicMax(&p.flags[2], kb + 1);   // the dense-tail block column
+        }
         return;
+    }
+    if (!fu_sup) {
+        if (w < nwin && (h1 ? rok && tile : (j == 0 && lane >= nc && lane < h0))) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) {
+                const int c = cw0 + q;
+                if (c < nc) panel[row + (size_t)c * ld] = a[q];
+            }
+        }
+        if (wpre && j == 0 && !h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc_pre;
     }
     if (j != 0) return;
     // workgroup 0: L11' into the upper slot through an LDS transpose (Ct is
@@ -1169,6 +1186,11 @@ constexpr size_t kTailStepLds = kTailStepLds0 > sizeof(PreLds) ? kTailStepLds0 :
 __global__ void __launch_bounds__(PNT)
 k_tail_pr(PlanView p, TailView tv, int t, int gp, const double* __restrict__ Wprev, double* __restrict__ Wcur) {
     __shared__ __attribute__((aligned(16))) char lds[kTailStepLds];
+    // a panel of an earlier step bailed (flags[2] = 1 + its block column;
+    // not this launch's own, whose trailing tiles must complete): the host
+    // resumes the look-ahead from there
+    const int bailed = p.flags[2];
+    if (bailed && bailed - 1 < t) return;
     if ((int)blockIdx.x < gp) {
         panel_w_body(p, nullptr, nullptr, 0, tv, t, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), Wcur,
                      t > 0 ? Wprev : nullptr);
@@ -1177,6 +1199,15 @@ k_tail_pr(PlanView p, TailView tv, int t, int gp, const double* __restrict__ Wpr
     int tile = blockIdx.x - gp, bj = t + 1;
     while (tile >= tv.ntb - bj) { tile -= tv.ntb - bj; bj++; }
     syrk_tile512(p, tv, t - 1, bj + tile, bj, Wprev, *reinterpret_cast<SyrkLds*>(lds));
+}
+
+// Block t's update of block column t + 1 only (tiles (bi, t + 1), bi > t):
+// what the look-ahead panel of step t + 1 applies to its own rows, for the
+// repair path that resumes the look-ahead after a dependent pivot.
+__global__ void __launch_bounds__(PNT)
+k_tail_col(PlanView p, TailView tv, int t, const double* __restrict__ W) {
+    __shared__ __attribute__((aligned(16))) char lds[sizeof(SyrkLds)];
+    syrk_tile512(p, tv, t, t + 1 + blockIdx.x, t + 1, W, *reinterpret_cast<SyrkLds*>(lds));
 }
 
 // ------------------------------------------------------- small panels
@@ -1250,6 +1281,10 @@ void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const doubl
     const int gp = std::max(1, (h + TR - 1) / TR - 1);
     const int nr = t > 0 ? (tv.ntb - t - 1) * (tv.ntb - t) / 2 : 0;
     hipLaunchKernelGGL(k_tail_pr, dim3(gp + nr), dim3(PNT), 0, s, pv, tv, t, gp, Wprev, Wcur);
+}
+
+void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s) {
+    if (tv.ntb - t - 1 > 0) hipLaunchKernelGGL(k_tail_col, dim3(tv.ntb - t - 1), dim3(PNT), 0, s, pv, tv, t, W);
 }
 
 bool launch_tail_diag_coop(const PlanView& pv, const TailView& tv, int kb, double* gmax, int* gctr, hipStream_t s) {

@@ -43,6 +43,7 @@ struct KktTimers {
     long factors = 0, solves = 0, rawsolves = 0;
     long panel_redos = 0;     // factorisations redone without the fused panel kernels
     long redo_where[4] = {0, 0, 0, 0};   // ... by the kernel that bailed (k_panel, k_panel_w sparse / tail, k_panel_s)
+    long tail_repairs = 0;    // dense-tail block columns redone in place (look-ahead resumed after them)
 };
 
 class KktDevice {
@@ -179,6 +180,8 @@ class KktDevice {
     DevBuf<int> dsmall_sups_;
     bool use_panel_ = true;               // fused diagonal-block + panel kernels (IPO_HIP_PANEL=0: off)
     bool factor_pass(const double* dE, const double* dD, bool fused);
+    bool finish_pass(bool fused);
+    void repair_tail();
     std::vector<int> chunk_ptr_;          // per level: solve chunks [chunk_ptr_[l], chunk_ptr_[l+1])
     DevBuf<int> dchunk_sup_, dchunk_r0_, dsup_chunk0_;
     DevBuf<double> dPartial_;    // backward partial sums, one 64-vector per chunk
@@ -199,7 +202,7 @@ class KktDevice {
     DevBuf<double> dLx_, dDg_;
     DevBuf<int> dLive_;
     DevBuf<double> dDscale_;
-    DevBuf<int> dFlags_;           // [0] ndep, [1] inconsistent
+    DevBuf<int> dFlags_;           // [0] ndep, [1] fused bail bits, [2] 1 + bailed tail block, [4..] node sign
     DevBuf<double> dZ_, dDy_, dDx_, dRy_, dRx_;
     DevBuf<double> dPart_, dScal_;
     double* hScal_ = nullptr;      // pinned

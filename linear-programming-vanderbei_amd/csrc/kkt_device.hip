@@ -2035,11 +2035,12 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dLive_.alloc(T_ > 0 ? T_ : 1);
     dDscale_.alloc(T_ > 0 ? T_ : 1);
     if (const char* e = std::getenv("IPO_HIP_PIVTOL")) pivot_tol_ = std::atof(e);
-    // flags: [0] ndep, [1] fused panel bail-out, [2..2+T) node class sign per new index
-    dFlags_.alloc(2 + T_);
+    // flags: [0] ndep, [1] fused panel bail-out bits, [2] 1 + the dense-tail
+    // block column whose look-ahead panel bailed, [4..4+T) node class sign
+    dFlags_.alloc(4 + T_);
     {
-        std::vector<int> fl(2 + T_, 0);
-        for (int v = 0; v < T_; v++) fl[2 + v] = plan_.dsign[v];
+        std::vector<int> fl(4 + T_, 0);
+        for (int v = 0; v < T_; v++) fl[4 + v] = plan_.dsign[v];
         dFlags_.upload(fl, s);
     }
     dZ_.alloc(2 * (T_ > 0 ? T_ : 1));
@@ -2051,7 +2052,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dPart_.alloc(8 * kRedBlocks);
     dScal_.alloc(16);
     IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hScal_), 16 * sizeof(double), hipHostMallocDefault));
-    IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hFlags_), 4 * sizeof(int), hipHostMallocDefault));
+    IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hFlags_), 8 * sizeof(int), hipHostMallocDefault));
     IPO_HIP_CHECK(hipEventCreate(&ev0_));
     IPO_HIP_CHECK(hipEventCreate(&ev1_));
     IPO_HIP_CHECK(hipEventCreate(&ev2_));
@@ -2187,8 +2188,8 @@ KktDevice::~KktDevice() {
 #endif
     if (std::getenv("IPO_HIP_DEBUG_REDO"))
         std::fprintf(stderr, "kkt: %ld factorisations, %ld redone; bails k_panel %ld, k_panel_w sparse %ld, tail %ld, "
-                             "k_panel_s %ld\n", tm_.factors, tm_.panel_redos, tm_.redo_where[0], tm_.redo_where[1],
-                     tm_.redo_where[2], tm_.redo_where[3]);
+                             "k_panel_s %ld; tail block columns repaired %ld\n", tm_.factors, tm_.panel_redos,
+                     tm_.redo_where[0], tm_.redo_where[1], tm_.redo_where[2], tm_.redo_where[3], tm_.tail_repairs);
     if (hScal_) (void)hipHostFree(hScal_);
     if (hFlags_) (void)hipHostFree(hFlags_);
     if (ev0_) (void)hipEventDestroy(ev0_);
@@ -2210,7 +2211,7 @@ static PlanView make_view(const KktPlan&, const DevBuf<int>& col0, const DevBuf<
     v.task_i0 = t0.get(); v.task_i1 = t1.get(); v.upd_src = src.get(); v.upd_r0 = r0.get(); v.upd_r1 = r1.get();
     v.relptr = relptr.get(); v.rel = rel.get(); v.Lx = lx.get(); v.dg = dg.get(); v.live = live.get();
     v.flags = flags.get();
-    v.sign = flags.get() + 2;
+    v.sign = flags.get() + 4;
     return v;
 }
 
@@ -2246,7 +2247,12 @@ void KktDevice::factor(const double* dE, const double* dD) {
     if (!factor_pass(dE, dD, use_panel_)) {
         tm_.panel_redos++;
         for (int b = 0; b < 4; b++) tm_.redo_where[b] += (hFlags_[1] >> b) & 1;
-        factor_pass(dE, dD, false);
+        // only a look-ahead dense-tail panel bailed: everything before its
+        // block column stands, resume from there; else redo it all
+        const char* rp = std::getenv("IPO_HIP_TAIL_REPAIR");
+        const bool repair = !rp || std::atoi(rp) != 0;
+        if (repair && !xch_ && g_panel_kind == 2 && hFlags_[1] == 4 && hFlags_[4] > 0) repair_tail();
+        else factor_pass(dE, dD, false);
     }
     tm_.factors++;
     ndep_ = xch_ ? static_cast<int>(hScal_[1]) : hFlags_[0];
@@ -2261,7 +2267,7 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
     const PlanView pv = IPO_VIEW();
     const int nz = static_cast<int>(plan_.amap.size());
     IPO_HIP_CHECK(hipMemsetAsync(dLx_.get(), 0, dLx_.bytes(), s));
-    IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get(), 0, 2 * sizeof(int), s));
+    IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get(), 0, 3 * sizeof(int), s));
     if (nz > 0) hipLaunchKernelGGL(k_assemble_A, dim3(ceil_div(nz, NT)), dim3(NT), 0, s, nz, dA_.get(), damap_.get(), dLx_.get());
     hipLaunchKernelGGL(k_assemble_diag, dim3(ceil_div(T_, NT)), dim3(NT), 0, s, T_, m_, dperm_.get(), dE, dD, epsdiag_,
                        ddslot_.get(), dLx_.get(), dLive_.get(), dDscale_.get(), shard_minor() ? plan_.tail_c0 : T_);
@@ -2331,9 +2337,14 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
             }
         }
     }
+    return finish_pass(fused);
+}
+
+// min |d| over the factor (ldlt.c:293-306), the dependent-pivot count and
+// the fused kernels' bail-out flags, to the host
+bool KktDevice::finish_pass(bool fused) {
+    hipStream_t s = stream_;
     IPO_HIP_CHECK(hipGetLastError());
-    // min |d| over the factor (ldlt.c:293-306), the dependent-pivot count
-    // and the fused kernels' bail-out flag
     hipLaunchKernelGGL(k_min_abs_partial, dim3(kRedBlocks), dim3(NT), 0, s, dDg_.get(), T_, dPart_.get());
     hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), 1, 1u, dScal_.get());
     if (xch_) {   // every shard must take the same eps_diag / dependent-pivot / redo decisions
@@ -2343,6 +2354,7 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
     }
     IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 3 * sizeof(double), hipMemcpyDeviceToHost, s));
     IPO_HIP_CHECK(hipMemcpyAsync(hFlags_, dFlags_.get(), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 4, dFlags_.get() + 2, sizeof(int), hipMemcpyDeviceToHost, s));
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
     IPO_HIP_CHECK(hipStreamSynchronize(s));
     if (timing_) {
@@ -2354,6 +2366,49 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
     }
     const bool bail = xch_ ? hScal_[2] > 0 : hFlags_[1] != 0;
     return !(fused && bail);
+}
+
+// The look-ahead dense tail bailed at block column tb (a pivot failed the
+// zero test; steps after it did nothing): the sparse factor and block
+// columns < tb stand, column tb holds the updates of blocks <= tb - 2 (its
+// panel stores S only once it holds) and the columns right of it those of
+// blocks <= tb - 1.  Apply block tb - 1 to column tb, factor column tb with
+// the dependent-pivot kernels (its W into the look-ahead's buffer of that
+// parity), and resume the look-ahead at tb + 1 -- per entry the operations
+// of the full redo, which would take the same path (no pivot before tb
+// fails the test), so bitwise its factor.  Repeats while a later column
+// bails.
+void KktDevice::repair_tail() {
+    hipStream_t s = stream_;
+    const PlanView pv = IPO_VIEW();
+    const size_t wst = static_cast<size_t>(plan_.nt) * kPanelCols;
+    auto wbuf = [&](int t) { return dW_.get() + (t & 1) * wst; };
+    for (;;) {
+        const int tb = hFlags_[4] - 1;
+        tm_.tail_repairs++;
+        if (timing_) IPO_HIP_CHECK(hipEventRecord(ev0_, s));
+        IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get() + 1, 0, 2 * sizeof(int), s));
+        TailView tv = tail_view();
+        ph_begin(s);
+        if (tb > 0) launch_tail_colupdate(pv, tv, tb - 1, wbuf(tb - 1), s);
+        ph_end(kPhSyrk, tb > 0, s);
+        tv.W = wbuf(tb);
+        const int k0 = tb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0), below = plan_.nt - k0 - nc;
+        ph_begin(s);
+        if (!(coop_tail_ && launch_tail_diag_coop(pv, tv, tb, dCoopMax_.get(), dCoopCtr_.get(), s))) {
+            launch_diag(pv, nullptr, 0, 1, tv, tb, s);
+            if (below > 0) launch_trsm(pv, 0, -1, tv, tb, s);
+        }
+        ph_end(kPhDiag, 1, s);
+        for (int t = tb + 1; t < plan_.ntb; t++) {
+            ph_begin(s);
+            launch_tail_step(pv, tail_view(), t, wbuf(t + 1), wbuf(t), s);
+            ph_end(kPhDiag, 1, s);
+        }
+        if (finish_pass(true)) break;
+        if (hFlags_[1] != 4 || hFlags_[4] - 1 <= tb)   // cannot happen: a later tail column or nothing
+            throw std::runtime_error("kkt: dense-tail repair did not advance");
+    }
 }
 
 // Gather launches of one level (tail < 0) or of the dense tail (group =

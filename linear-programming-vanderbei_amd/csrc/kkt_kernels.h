@@ -31,7 +31,7 @@ struct PlanView {
     double* Lx;
     double* dg;
     int* live;
-    int* flags;      // [0] dependent pivots, [1] fused panel kernel bail-out
+    int* flags;      // [0] dependent pivots, [1] fused panel kernel bail-out, [2] 1 + bailed tail block
     const int* sign; // node class per new index: -1 y-node, +1 x-node
     double* dscale;  // sum of |terms| that formed each pivot (zero-pivot test)
     double tau;      // pivot d is "zero" when |d| <= tau * dscale
@@ -66,6 +66,8 @@ void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0
 // column, W of block t into Wcur, block t - 1's read from Wprev.
 void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const double* Wprev, double* Wcur,
                       hipStream_t s);
+// Block t's update of block column t + 1 alone (W = block t's L21 D).
+void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s);
 // Redo path: diagonal block + rows below of dense-tail block column kb with
 // the dependent-pivot rule, one cooperative launch (k_tail_diag_coop);
 // gmax: one double per 64-row tile, gctr: grid-barrier counter (cleared here).

@@ -85,3 +85,13 @@ def test_sync_free_sweeps_bitwise():
     the dfl001 HSD traces are identical."""
     texts = [_with_env("IPO_HIP_SF", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1] for v in ("0", "1")]
     assert texts[0] == texts[1]
+
+
+def test_tail_repair_bitwise():
+    """A dependent pivot in the look-ahead dense tail: resuming the look-ahead
+    after redoing only the bailed block column (default) against redoing the
+    whole factorisation with the per-phase kernels (IPO_HIP_TAIL_REPAIR=0) --
+    the dfl001 HSD solve meets such pivots in three factorisations; identical
+    traces."""
+    texts = [_with_env("IPO_HIP_TAIL_REPAIR", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1] for v in ("0", "1")]
+    assert texts[0] == texts[1]
