@@ -80,13 +80,14 @@ k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict
 
 // directions + ratio test (hsd.c:233-237, 249-256)
 __global__ void __launch_bounds__(NT)
-k_hsd_directions(int m, int n, double dphi, double delta, double mu, const double* __restrict__ fx,
+k_hsd_directions(int m, int n, const double* __restrict__ dphip, double delta, double mu, const double* __restrict__ fx,
                  const double* __restrict__ gx, const double* __restrict__ fy, const double* __restrict__ gy,
                  const double* __restrict__ x, const double* __restrict__ z, const double* __restrict__ y,
                  const double* __restrict__ w, const double* __restrict__ D, const double* __restrict__ E,
                  double* __restrict__ dx, double* __restrict__ dz, double* __restrict__ dy, double* __restrict__ dw,
                  double* __restrict__ part) {
     __shared__ double sh[4];
+    const double dphi = *dphip;
     double th = 0.0;
     for (int i = blockIdx.x * NT + threadIdx.x; i < m + n; i += kRedBlocks * NT) {
         if (i < n) {
@@ -109,12 +110,36 @@ k_hsd_directions(int m, int n, double dphi, double delta, double mu, const doubl
 }
 
 __global__ void __launch_bounds__(NT)
-k_step(int m, int n, double theta, double* __restrict__ x, const double* __restrict__ dx, double* __restrict__ z,
-       const double* __restrict__ dz, double* __restrict__ y, const double* __restrict__ dy, double* __restrict__ w,
-       const double* __restrict__ dw) {
+k_step(int m, int n, double theta_h, const double* __restrict__ thetap, double* __restrict__ x,
+       const double* __restrict__ dx, double* __restrict__ z, const double* __restrict__ dz, double* __restrict__ y,
+       const double* __restrict__ dy, double* __restrict__ w, const double* __restrict__ dw) {
+    const double theta = thetap ? *thetap : theta_h;     // device-computed step (hsd) or the host's
     const int i = blockIdx.x * NT + threadIdx.x;
     if (i < n) { x[i] = x[i] + theta * dx[i]; z[i] = z[i] + theta * dz[i]; }
     else if (i < n + m) { const int j = i - n; y[j] = y[j] + theta * dy[j]; w[j] = w[j] + theta * dw[j]; }
+}
+
+// hsd.c:226-231 on the device (same operations and order as the host code
+// it replaces): sc[0..3] = c'fx, b'fy, c'gx, b'gy -> sc[12] = dphi, sc[13] = dpsi
+__global__ void k_hsd_dphi(double* sc, double gamma, double delta, double mu, double phi, double psi) {
+    const double dphi = (sc[0] - sc[1] + gamma) / (sc[2] - sc[3] - psi / phi);
+    const double dpsi = delta * mu / phi - psi - (psi / phi) * dphi;
+    sc[12] = dphi;
+    sc[13] = dpsi;
+}
+
+// hsd.c:249-266: step length from the largest ratio sc[0] and dphi / dpsi;
+// sc[11] = theta, sc[14] / sc[15] = the next phi / psi (read by the host at
+// the next iteration's synchronisation)
+__global__ void k_hsd_theta(double* sc, double phi, double psi) {
+    const double dphi = sc[12], dpsi = sc[13];
+    double theta = sc[0];
+    if (theta < -dphi / phi) theta = -dphi / phi;
+    if (theta < -dpsi / psi) theta = -dpsi / psi;
+    theta = (0.95 / theta > 1.0) ? 1.0 : 0.95 / theta;
+    sc[11] = theta;
+    sc[14] = phi + theta * dphi;
+    sc[15] = psi + theta * dpsi;
 }
 
 __global__ void __launch_bounds__(NT)
@@ -377,6 +402,11 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
     }
     KktDevice& K = *kkt_;
     int status = 5, iter;
+    // one host synchronisation per iteration outside the KKT solver: the
+    // dots of mu (with phi / psi of the device step, hsd.c:264-265); the
+    // residual norms are only printed (read back without a wait), dphi /
+    // dpsi / theta / phi / psi are computed on the device (k_hsd_dphi,
+    // k_hsd_theta: the host's operations in the host's order)
     for (iter = 0; iter < opt.max_iter; iter++) {
         RedJobs j{};
         j.nj = 4;
@@ -384,7 +414,12 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
         j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = mcnt_; j.op[1] = 0;
         j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
         j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = mcnt_; j.op[3] = 0;
-        reduce(j, 4);
+        launch_reduce(j, part_.get(), scal_.get(), s);
+        xsum(scal_.get(), 4, RedOp::Sum);
+        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 4 * sizeof(double), hipMemcpyDeviceToHost, s));
+        if (iter > 0) IPO_HIP_CHECK(hipMemcpyAsync(hs_ + 14, scal_.get() + 14, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        if (iter > 0) { phi = hs_[14]; psi = hs_[15]; }
         const double mu = (hs_[0] + hs_[1] + phi * psi) / (ng_ + mg_ + 1);
         const double delta = (iter % 2 == 0) ? 0.0 : 1.0;
         const double pobj = hs_[2], dobj = hs_[3];
@@ -402,11 +437,12 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
                            lax());
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get());
         xsum(scal_.get(), 2, RedOp::Sum);
-        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
-        IPO_HIP_CHECK(hipStreamSynchronize(s));
-        const double normr = std::sqrt(hs_[0]) / phi;
-        const double norms = std::sqrt(hs_[1]) / phi;
+        IPO_HIP_CHECK(hipMemcpyAsync(hs_ + 8, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
         const double gamma = -(1 - delta) * (dobj - pobj + psi) + psi - delta * mu / phi;
+
+        K.factor(E_.get(), D_.get());        // synchronises the stream: hs_[8..9] have landed
+        const double normr = std::sqrt(hs_[8]) / phi;
+        const double norms = std::sqrt(hs_[9]) / phi;
         if (tr) {
             std::fprintf(tr, "%8d   %14.7e  %8.1e    %14.7e  %8.1e  %8.1e \n", iter, pobj / phi + f_, normr,
                          dobj / phi + f_, norms, mu);
@@ -414,10 +450,10 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
         }
         res->final_mu = mu; res->final_pobj = pobj / phi + f_; res->final_dobj = dobj / phi + f_;
         res->final_pinf = normr; res->final_dinf = norms;
-        if (full_trace_) std::fprintf(stderr, "FT %d %.17g %.17g %.17g %.17g %.17g %.17g\n", iter, pobj, dobj, mu, phi, psi, normr);
-
-        K.factor(E_.get(), D_.get());
-        if (full_trace_) std::fprintf(stderr, "FT   ndep=%d eps=%.1e\n", K.ndep(), K.epsdiag());
+        if (full_trace_) {
+            std::fprintf(stderr, "FT %d %.17g %.17g %.17g %.17g %.17g %.17g\n", iter, pobj, dobj, mu, phi, psi, normr);
+            std::fprintf(stderr, "FT   ndep=%d eps=%.1e\n", K.ndep(), K.epsdiag());
+        }
         // the two forwardbackward calls of hsd.c:218-224 / hsdls.c:194-203,
         // independent systems with one factor: sweeps batched
         K.solve2(E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get());
@@ -429,26 +465,17 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
         q.a[1] = b_.get(); q.b[1] = fy_.get(); q.len[1] = mcnt_; q.op[1] = 0;
         q.a[2] = c_.get(); q.b[2] = gx_.get(); q.len[2] = n; q.op[2] = 0;
         q.a[3] = b_.get(); q.b[3] = gy_.get(); q.len[3] = mcnt_; q.op[3] = 0;
-        reduce(q, 4);
-        const double dphi = (hs_[0] - hs_[1] + gamma) / (hs_[2] - hs_[3] - psi / phi);
-        const double dpsi = delta * mu / phi - psi - (psi / phi) * dphi;
-
-        hipLaunchKernelGGL(k_hsd_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dphi, delta, mu, fx_.get(),
-                           gx_.get(), fy_.get(), gy_.get(), x_.get(), z_.get(), y_.get(), w_.get(), D_.get(), E_.get(),
-                           dx_.get(), dz_.get(), dy_.get(), dw_.get(), part_.get());
+        launch_reduce(q, part_.get(), scal_.get(), s);
+        xsum(scal_.get(), 4, RedOp::Sum);
+        hipLaunchKernelGGL(k_hsd_dphi, dim3(1), dim3(1), 0, s, scal_.get(), gamma, delta, mu, phi, psi);
+        hipLaunchKernelGGL(k_hsd_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, scal_.get() + 12, delta, mu,
+                           fx_.get(), gx_.get(), fy_.get(), gy_.get(), x_.get(), z_.get(), y_.get(), w_.get(), D_.get(),
+                           E_.get(), dx_.get(), dz_.get(), dy_.get(), dw_.get(), part_.get());
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 1, 1u, scal_.get());
         xsum(scal_.get(), 1, RedOp::Max);
-        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
-        IPO_HIP_CHECK(hipStreamSynchronize(s));
-        double theta = hs_[0];
-        if (theta < -dphi / phi) theta = -dphi / phi;
-        if (theta < -dpsi / psi) theta = -dpsi / psi;
-        theta = (0.95 / theta > 1.0) ? 1.0 : 0.95 / theta;
-
-        hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, theta, x_.get(), dx_.get(), z_.get(), dz_.get(),
-                           y_.get(), dy_.get(), w_.get(), dw_.get());
-        phi = phi + theta * dphi;
-        psi = psi + theta * dpsi;
+        hipLaunchKernelGGL(k_hsd_theta, dim3(1), dim3(1), 0, s, scal_.get(), phi, psi);
+        hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, 0.0, scal_.get() + 11, x_.get(), dx_.get(),
+                           z_.get(), dz_.get(), y_.get(), dy_.get(), w_.get(), dw_.get());
     }
     hipLaunchKernelGGL(k_unscale, dim3(gv), dim3(NT), 0, s, m, n, phi, x_.get(), z_.get(), y_.get(), w_.get());
     IPO_HIP_CHECK(hipGetLastError());
@@ -546,7 +573,7 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
         theta = theta < tp ? theta : tp;
         if (theta < 1.0) theta *= 0.9999;
 
-        hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, theta, x_.get(), dx_.get(), z_.get(), dz_.get(),
+        hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, theta, static_cast<const double*>(nullptr), x_.get(), dx_.get(), z_.get(), dz_.get(),
                            y_.get(), dy_.get(), w_.get(), dw_.get());
         phi = phi + theta * dphi;
         psi = psi + theta * dpsi;
@@ -622,7 +649,7 @@ int IpmSolver::run_intpt(const IpmOptions& opt, IpmResult* res) {
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         double theta = hs_[0];
         theta = (r / theta > 1.0) ? 1.0 : r / theta;
-        hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, theta, x_.get(), dx_.get(), z_.get(), dz_.get(),
+        hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, theta, static_cast<const double*>(nullptr), x_.get(), dx_.get(), z_.get(), dz_.get(),
                            y_.get(), dy_.get(), w_.get(), dw_.get());
         normr0 = normr;
         norms0 = norms;
@@ -673,6 +700,8 @@ void vector_bench(int m, int n, const int* kA, const int* iA, const double* A, i
     double* V = vec.get();
     auto col = [&](int q) { return V + q * N; };      // n-vectors at col(q), m-vectors at col(q) + n
     double* part = V + 24 * N;
+    DevBuf<double> dphi03;
+    dphi03.upload(std::vector<double>{0.3}, s);
     hipEvent_t e0, e1;
     IPO_HIP_CHECK(hipEventCreate(&e0));
     IPO_HIP_CHECK(hipEventCreate(&e1));
@@ -686,11 +715,11 @@ void vector_bench(int m, int n, const int* kA, const int* iA, const double* A, i
                                    col(4) + n, col(5), 1.0, 0.5, 0.1, col(6) + n, col(7), col(8) + n, col(9),
                                    col(10) + n, col(11), part, m, m, static_cast<const double*>(nullptr));
             else if (kq == 1)
-                hipLaunchKernelGGL(k_hsd_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, 0.3, 0.5, 0.1, col(9),
+                hipLaunchKernelGGL(k_hsd_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dphi03.get(), 0.5, 0.1, col(9),
                                    col(11), col(8) + n, col(10) + n, col(2), col(5), col(3) + n, col(4) + n, col(7),
                                    col(6) + n, col(12), col(13), col(14) + n, col(15) + n, part);
             else
-                hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, 1e-9, col(16), col(12), col(17), col(13),
+                hipLaunchKernelGGL(k_step, dim3(gv), dim3(NT), 0, s, m, n, 1e-9, static_cast<const double*>(nullptr), col(16), col(12), col(17), col(13),
                                    col(18) + n, col(14) + n, col(19) + n, col(15) + n);
         }
         IPO_HIP_CHECK(hipEventRecord(e1, s));

@@ -188,8 +188,14 @@ class KktDevice {
     // split-K gather chunks per group (sparse level l, group nlevels = tail)
     std::vector<int> ck_ptr_, sp_ptr_;
     DevBuf<int> dck_u_, dck_b_, dck_e_, dck_part_, dsp_u_, dsp_p0_, dsp_n_;
+    DevBuf<int> dck_q_;          // split-unit index of each chunk (-1: unsplit)
+    DevBuf<int> dSplitCnt_;      // arrival counters of the split units (fused split-K), zero between launches
+    bool fused_splitk_ = true;   // IPO_HIP_SPLITK_FUSED=0: separate k_update_reduce launch
+    int gather_depth_ = 1;       // slabs of slot values in flight in k_update, sparse levels (IPO_HIP_GATHER_DEPTH = 1, 2, 4; deeper rings cost occupancy and measured slower)
+    int tail_gather_depth_ = 1;  // the same for the dense-tail gather (IPO_HIP_TAIL_GATHER_DEPTH)
     DevBuf<double> dPartialTile_;
     DevBuf<TaskSrc> dusrc_, dtsrc_;   // per gather task: source panel descriptor
+    DevBuf<SlotRec> dslot_rec_, dtail_slot_rec_;   // per gather k-slot record (sparse units, dense tail)
     DevBuf<int> dChainFlags_;    // dense-tail sweep chains: per block, epoch of the last completed sweep
     int chain_epoch_ = 0;      // forward-sweep update values, one per row of every R_s
     DevBuf<int> dtail_task_ptr_, dkslot_, dkslot_ptr_, dtail_kslot_, dtail_kslot_ptr_;

@@ -100,35 +100,19 @@ k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __rest
 typedef double double4_t __attribute__((ext_vector_type(4)));
 constexpr int KS = kSlab;
 
-// What a k-slot needs, resolved once per slot (wave-uniform): the source
-// column (rows of R_d), its d_k, and the task's row / column masks.
-struct SlotMeta {
-    uint64_t rmask, cmask;
-    const double* col;
-    const double* dk;
-    int rbase, cbase;
-};
-
-__device__ __forceinline__ void slot_meta(const PlanView& p, const TailTask* __restrict__ tasks,
-                                          const TaskSrc* __restrict__ srcs, int sl, SlotMeta& m) {
-    if (sl < 0) { m.rmask = m.cmask = 0; m.col = p.Lx; m.dk = p.dg; m.rbase = m.cbase = 0; return; }
-    const int t = sl >> 6, kl = sl & 63;
-    const TailTask tk = tasks[t];
-    const TaskSrc sd = srcs[t];
-    m.rmask = tk.rmask;
-    m.cmask = tk.cmask;
-    m.rbase = tk.rbase;
-    m.cbase = tk.cbase;
-    m.col = p.Lx + sd.colbase + (size_t)kl * sd.hd;
-    m.dk = p.dg + sd.cd0 + kl;
-}
-
-__device__ __forceinline__ void slot_vals(const SlotMeta& m, int lane, double& ra, double& rb) {
+// What a k-slot needs (SlotRec, kkt_plan.h: masks, the source column's
+// first row-set entry for the tile's rows, the column offset, d_k's index),
+// expanded per slot on the host so that one coalesced load per slot stages a
+// chunk's records in LDS; the values are then issued without a dependent
+// metadata round trip.  ra = L(row, k), rb = d_k * L(col, k) (the reference
+// form, ldlt.c:572,583), zero where the task leaves the tile entry untouched.
+__device__ __forceinline__ void slot_vals(const SlotRec& m, const double* __restrict__ Lx,
+                                          const double* __restrict__ dg, int lane, double& ra, double& rb) {
     const uint64_t below = (1ull << lane) - 1ull;
     ra = 0.0;
     rb = 0.0;
-    if ((m.rmask >> lane) & 1ull) ra = m.col[m.rbase + __popcll(m.rmask & below)];
-    if ((m.cmask >> lane) & 1ull) rb = *m.dk * m.col[m.cbase + __popcll(m.cmask & below)];
+    if ((m.rmask >> lane) & 1ull) ra = Lx[m.roff + __popcll(m.rmask & below)];
+    if ((m.cmask >> lane) & 1ull) rb = dg[m.dk] * Lx[m.roff + m.cdelta + __popcll(m.cmask & below)];
 }
 
 // Output tile of one gather unit: a 64-row tile of a sparse panel
@@ -172,12 +156,12 @@ __device__ __forceinline__ GatherTile unit_tile(const PlanView& p, const TailVie
 // MFMA accumulation of slots [kb, ke) into this thread's 16 tile entries
 // (acc[a][b][i] = entry (wr + 16a + (lane>>4) + 4i, wc + 16b + (lane&15)))
 // and, for lanes on a diagonal entry, the |terms| of that entry (dabs).
-__device__ void gather_acc(const PlanView& p, const TailTask* __restrict__ tasks, const TaskSrc* __restrict__ srcs,
-                           const int* __restrict__ kslot, int kb, int ke, int dcol, bool has_diag,
-                           double4_t (&acc)[2][2], double& dabs) {
+template <int GD>
+__device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, int kb, int ke, int dcol,
+                           bool has_diag, double4_t (&acc)[2][2], double& dabs) {
     __shared__ double As[2][TR][KS + 1];
     __shared__ double Bs[2][TR][KS + 1];
-    __shared__ int ks[kMaxChunkSlots];
+    __shared__ SlotRec rs[kMaxChunkSlots];
     const int tid = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
@@ -188,63 +172,61 @@ __device__ void gather_acc(const PlanView& p, const TailTask* __restrict__ tasks
         for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     dabs = 0.0;
     const int nk = ke - kb, nslab = nk / KS;
-    for (int i = tid; i < nk; i += NT) ks[i] = kslot[kb + i];
+    for (int i = tid; i < nk; i += NT) rs[i] = recs[kb + i];
     __syncthreads();
-    // three-stage pipeline: slot metadata two slabs ahead, values one ahead
-    double ra[KS / 4], rb[KS / 4];
-    SlotMeta mn[KS / 4];
+    // pipeline: the slot values of GD slabs in flight in a register ring
+    // (slab sb + GD issued while slab sb is multiplied; ring entry sb % GD),
+    // LDS double-buffered.  Same products, same MFMA order for every GD.
+    double ra[GD][KS / 4], rb[GD][KS / 4];
+    const double* __restrict__ Lx = p.Lx;
+    const double* __restrict__ dg = p.dg;
+    auto issue = [&](int slab, double (&xa)[KS / 4], double (&xb)[KS / 4]) {
 #pragma unroll
-    for (int j = 0; j < KS / 4; j++) slot_meta(p, tasks, srcs, __builtin_amdgcn_readfirstlane(ks[wv * (KS / 4) + j]), mn[j]);
+        for (int j = 0; j < KS / 4; j++) slot_vals(rs[slab * KS + wv * (KS / 4) + j], Lx, dg, lane, xa[j], xb[j]);
+    };
 #pragma unroll
-    for (int j = 0; j < KS / 4; j++) slot_vals(mn[j], lane, ra[j], rb[j]);
-    if (nslab > 1) {
+    for (int r = 0; r < GD; r++)
+        if (r < nslab) issue(r, ra[r], rb[r]);
 #pragma unroll
-        for (int j = 0; j < KS / 4; j++)
-            slot_meta(p, tasks, srcs, __builtin_amdgcn_readfirstlane(ks[KS + wv * (KS / 4) + j]), mn[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < KS / 4; j++) { As[0][lane][wv * (KS / 4) + j] = ra[j]; Bs[0][lane][wv * (KS / 4) + j] = rb[j]; }
+    for (int j = 0; j < KS / 4; j++) { As[0][lane][wv * (KS / 4) + j] = ra[0][j]; Bs[0][lane][wv * (KS / 4) + j] = rb[0][j]; }
     __syncthreads();
-    for (int sb = 0; sb < nslab; sb++) {
-        const int cur = sb & 1;
-        if (sb + 1 < nslab) {
+    for (int sb0 = 0; sb0 < nslab; sb0 += GD) {
 #pragma unroll
-            for (int j = 0; j < KS / 4; j++) slot_vals(mn[j], lane, ra[j], rb[j]);
-            if (sb + 2 < nslab) {
+        for (int ph = 0; ph < GD; ph++) {
+            const int sb = sb0 + ph;
+            if (sb >= nslab) break;
+            const int cur = sb & 1;
+            if (sb + GD < nslab) issue(sb + GD, ra[ph], rb[ph]);
 #pragma unroll
-                for (int j = 0; j < KS / 4; j++)
-                    slot_meta(p, tasks, srcs, __builtin_amdgcn_readfirstlane(ks[(sb + 2) * KS + wv * (KS / 4) + j]),
-                              mn[j]);
+            for (int kk = 0; kk < KS; kk += 4) {
+                double av[2], bv[2];
+#pragma unroll
+                for (int a = 0; a < 2; a++) av[a] = As[cur][wr + a * 16 + li][kk + lk];
+#pragma unroll
+                for (int b = 0; b < 2; b++) bv[b] = Bs[cur][wc + b * 16 + li][kk + lk];
+#pragma unroll
+                for (int a = 0; a < 2; a++)
+#pragma unroll
+                    for (int b = 0; b < 2; b++)
+                        acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
             }
-        }
+            if (has_diag) {
 #pragma unroll
-        for (int kk = 0; kk < KS; kk += 4) {
-            double av[2], bv[2];
-#pragma unroll
-            for (int a = 0; a < 2; a++) av[a] = As[cur][wr + a * 16 + li][kk + lk];
-#pragma unroll
-            for (int b = 0; b < 2; b++) bv[b] = Bs[cur][wc + b * 16 + li][kk + lk];
-#pragma unroll
-            for (int a = 0; a < 2; a++)
-#pragma unroll
-                for (int b = 0; b < 2; b++)
-                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
-        }
-        if (has_diag) {
-#pragma unroll
-            for (int j = 0; j < KS / 4; j++) {
-                const int k = wv * (KS / 4) + j;
-                dabs += fabs(As[cur][lane][k] * Bs[cur][dcol][k]);
+                for (int j = 0; j < KS / 4; j++) {
+                    const int k = wv * (KS / 4) + j;
+                    dabs += fabs(As[cur][lane][k] * Bs[cur][dcol][k]);
+                }
             }
-        }
-        if (sb + 1 < nslab) {
+            if (sb + 1 < nslab) {
+                const int nx = (ph + 1) % GD;
 #pragma unroll
-            for (int j = 0; j < KS / 4; j++) {
-                As[cur ^ 1][lane][wv * (KS / 4) + j] = ra[j];
-                Bs[cur ^ 1][lane][wv * (KS / 4) + j] = rb[j];
+                for (int j = 0; j < KS / 4; j++) {
+                    As[cur ^ 1][lane][wv * (KS / 4) + j] = ra[nx][j];
+                    Bs[cur ^ 1][lane][wv * (KS / 4) + j] = rb[nx][j];
+                }
             }
+            __syncthreads();
         }
-        __syncthreads();
     }
 }
 
@@ -286,68 +268,31 @@ __device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], 
     }
 }
 
-// Gather chunks: chunk c covers slots [ck_b[c], ck_e[c]) of unit ck_u[c].
-// ck_part[c] < 0: the unit's only chunk, subtract directly; else store the
-// partial tile (thread-fragment order) and dabs at partial slot ck_part[c].
-// tail >= 0: units are dense-tail tiles.
-__global__ void __launch_bounds__(NT)
-k_update(PlanView p, TailView tv, int tail, const TailTask* __restrict__ tasks, const TaskSrc* __restrict__ srcs,
-         const int* __restrict__ kslot,
-         const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
-         const int* __restrict__ ck_part, int c0, double* __restrict__ partial) {
-    const int c = c0 + blockIdx.x;
-    const int u = ck_u[c], kb = ck_b[c], ke = ck_e[c], pi = ck_part[c];
-    const GatherTile g = unit_tile(p, tv, u, tail);
-    const int lane = threadIdx.x & 63;
-    const int dcol = g.row0 + lane - g.col0;
-    const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
-    double4_t acc[2][2];
-    double dabs;
-    gather_acc(p, tasks, srcs, kslot, kb, ke, dcol, has_diag, acc, dabs);
-    if (pi < 0) {
-        gather_store(g, acc, dabs, has_diag, dcol);
-        return;
-    }
-    double* dst = partial + (size_t)pi * (TR * TR + 4 * TR);
+// Sum the np partial tiles of a split unit (slots p0.., thread-fragment
+// order) in chunk order: acc = ((0 + P_0) + P_1) + ...  SC: the partials
+// were handed off inside this launch (sc1 loads, bypassing the CU's L1).
+template <bool SC, int NF>
+__device__ __forceinline__ void split_sum(const double* __restrict__ partial, int p0, int np, double4_t (&acc)[2][2],
+                                          double& dabs) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int b = 0; b < 2; b++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) dst[((a * 2 + b) * 4 + i) * NT + tid] = acc[a][b][i];
-    dst[TR * TR + tid] = dabs;
-}
-
-// Split units: sum their chunks' partial tiles in chunk order, then store.
-__global__ void __launch_bounds__(NT)
-k_update_reduce(PlanView p, TailView tv, int tail, const int* __restrict__ sp_u, const int* __restrict__ sp_p0,
-                const int* __restrict__ sp_n, int s0, const double* __restrict__ partial) {
-    const int q = s0 + blockIdx.x;
-    const int u = sp_u[q], p0 = sp_p0[q], np = sp_n[q];
-    const GatherTile g = unit_tile(p, tv, u, tail);
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int dcol = g.row0 + lane - g.col0;
-    const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
-    double4_t acc[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
-    double dabs = 0.0;
-    // loads of four chunks in flight, sums still in chunk order
+    dabs = 0.0;
+    // loads of NF chunks in flight, sums still in chunk order
     int j = 0;
-    for (; j + 4 <= np; j += 4) {
-        double v[4][17];
+    for (; j + NF <= np; j += NF) {
+        double v[NF][17];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < NF; u++) {
             const double* src = partial + (size_t)(p0 + j + u) * (TR * TR + 4 * TR);
 #pragma unroll
-            for (int e = 0; e < 16; e++) v[u][e] = src[e * NT + tid];
-            v[u][16] = src[TR * TR + tid];
+            for (int e = 0; e < 16; e++) v[u][e] = ld_h<SC>(src + e * NT + tid);
+            v[u][16] = ld_h<SC>(src + TR * TR + tid);
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < NF; u++) {
 #pragma unroll
             for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -359,14 +304,99 @@ k_update_reduce(PlanView p, TailView tv, int tail, const int* __restrict__ sp_u,
     }
     for (; j < np; j++) {
         const double* src = partial + (size_t)(p0 + j) * (TR * TR + 4 * TR);
+        double v[17];
+#pragma unroll
+        for (int e = 0; e < 16; e++) v[e] = ld_h<SC>(src + e * NT + tid);
+        v[16] = ld_h<SC>(src + TR * TR + tid);
 #pragma unroll
         for (int a = 0; a < 2; a++)
 #pragma unroll
             for (int b = 0; b < 2; b++)
 #pragma unroll
-                for (int i = 0; i < 4; i++) acc[a][b][i] += src[((a * 2 + b) * 4 + i) * NT + tid];
-        dabs += src[TR * TR + tid];
+                for (int i = 0; i < 4; i++) acc[a][b][i] += v[(a * 2 + b) * 4 + i];
+        dabs += v[16];
     }
+}
+
+// Gather chunks: chunk c covers slots [ck_b[c], ck_e[c]) of unit ck_u[c].
+// ck_part[c] < 0: the unit's only chunk, subtract directly; else store the
+// partial tile (thread-fragment order) and dabs at partial slot ck_part[c].
+// tail >= 0: units are dense-tail tiles.
+// split_cnt != null (fused split-K): the chunks of split unit q = ck_q[c]
+// store their partials write-through (sc1), drain them, and one lane adds
+// to the unit's arrival counter; the chunk whose add comes last sums all
+// partials in chunk order (sc1 loads) and stores the tile, exactly as
+// k_update_reduce would (MI355X_MICROARCH.md hand-off table row 1:
+// last arriver told by its own add's return value).  It resets the counter
+// for the next factorisation.
+template <int GD, int NF>
+__global__ void __launch_bounds__(NT)
+k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
+         const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
+         const int* __restrict__ ck_part, int c0, double* __restrict__ partial,
+         const int* __restrict__ ck_q, const int* __restrict__ sp_p0, const int* __restrict__ sp_n,
+         int* __restrict__ split_cnt) {
+    const int c = c0 + blockIdx.x;
+    const int u = ck_u[c], kb = ck_b[c], ke = ck_e[c], pi = ck_part[c];
+    const GatherTile g = unit_tile(p, tv, u, tail);
+    const int lane = threadIdx.x & 63;
+    const int dcol = g.row0 + lane - g.col0;
+    const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
+    double4_t acc[2][2];
+    double dabs;
+    gather_acc<GD>(p, recs, kb, ke, dcol, has_diag, acc, dabs);
+    if (pi < 0) {
+        gather_store(g, acc, dabs, has_diag, dcol);
+        return;
+    }
+    double* dst = partial + (size_t)pi * (TR * TR + 4 * TR);
+    const int tid = threadIdx.x;
+    if (!split_cnt) {
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) dst[((a * 2 + b) * 4 + i) * NT + tid] = acc[a][b][i];
+        dst[TR * TR + tid] = dabs;
+        return;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) sc1_store(dst + ((a * 2 + b) * 4 + i) * NT + tid, acc[a][b][i]);
+    sc1_store(dst + TR * TR + tid, dabs);
+    __shared__ int last;
+    const int q = ck_q[c];
+    const int np = sp_n[q];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const int prev = __hip_atomic_fetch_add(split_cnt + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == np - 1;
+        if (prev == np - 1) __hip_atomic_store(split_cnt + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    split_sum<true, NF>(partial, sp_p0[q], np, acc, dabs);
+    gather_store(g, acc, dabs, has_diag, dcol);
+}
+
+// Split units: sum their chunks' partial tiles in chunk order, then store.
+__global__ void __launch_bounds__(NT)
+k_update_reduce(PlanView p, TailView tv, int tail, const int* __restrict__ sp_u, const int* __restrict__ sp_p0,
+                const int* __restrict__ sp_n, int s0, const double* __restrict__ partial) {
+    const int q = s0 + blockIdx.x;
+    const int u = sp_u[q], p0 = sp_p0[q], np = sp_n[q];
+    const GatherTile g = unit_tile(p, tv, u, tail);
+    const int lane = threadIdx.x & 63;
+    const int dcol = g.row0 + lane - g.col0;
+    const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
+    double4_t acc[2][2];
+    double dabs;
+    split_sum<false, 4>(partial, p0, np, acc, dabs);
     gather_store(g, acc, dabs, has_diag, dcol);
 }
 
@@ -1780,6 +1810,10 @@ k_min_abs_partial(const double* __restrict__ d, int T, double* __restrict__ part
 }
 
 __global__ void k_scale_scalar(double* e, double f) { e[0] *= f; }
+// n ints copied bit for bit into the doubles at out (one host read-back with them)
+__global__ void k_pack_ints(const int* f, int n, double* out) {
+    if (static_cast<int>(threadIdx.x) < n) reinterpret_cast<int*>(out)[threadIdx.x] = f[threadIdx.x];
+}
 __global__ void k_flag_to_scalar(const int* f, double* d) { d[0] = static_cast<double>(f[0]); }
 
 }  // namespace
@@ -1881,16 +1915,19 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dkslot_.upload(plan_.kslot, s);
     dkslot_ptr_.upload(plan_.kslot_ptr, s);
     {   // gather chunks (split K): groups = sparse levels, then the dense tail
-        std::vector<int> cu, cb, ce, cp, su, sp0, sn;
+        std::vector<int> cu, cb, ce, cp, cq, su, sp0, sn;
         ck_ptr_.assign(plan_.nlevels + 2, 0);
         sp_ptr_.assign(plan_.nlevels + 2, 0);
         size_t max_part = 0;
+        int wg_target = 512, min_chunk = 64;
+        if (const char* e = std::getenv("IPO_HIP_GATHER_WGS")) wg_target = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("IPO_HIP_GATHER_MINCHUNK")) min_chunk = std::max(kSlab, std::atoi(e) / kSlab * kSlab);
         auto group = [&](int u0, int u1, const std::vector<int>& kptr) {
             long sumk = 0;
             for (int u = u0; u < u1; u++) sumk += kptr[u + 1] - kptr[u];
-            // aim at >= 512 workgroups per launch, chunks of 64..512 slots
-            long kmax = (sumk / 512 + kSlab - 1) / kSlab * kSlab;
-            kmax = std::max<long>(64, std::min<long>(kMaxChunkSlots, kmax));
+            // aim at >= wg_target workgroups per launch, chunks of min_chunk..512 slots
+            long kmax = (sumk / wg_target + kSlab - 1) / kSlab * kSlab;
+            kmax = std::max<long>(min_chunk, std::min<long>(kMaxChunkSlots, kmax));
             int np = 0;
             for (int u = u0; u < u1; u++) {
                 const int kb = kptr[u], ke = kptr[u + 1];
@@ -1902,6 +1939,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
                     cb.push_back(kb + static_cast<int>(j * kmax));
                     ce.push_back(std::min<int>(ke, kb + static_cast<int>((j + 1) * kmax)));
                     cp.push_back(nch > 1 ? np++ : -1);
+                    cq.push_back(nch > 1 ? static_cast<int>(su.size()) - 1 : -1);
                 }
             }
             max_part = std::max<size_t>(max_part, np);
@@ -1921,6 +1959,12 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dsp_u_.upload(su, s);
         dsp_p0_.upload(sp0, s);
         dsp_n_.upload(sn, s);
+        dck_q_.upload(cq, s);
+        dSplitCnt_.alloc(std::max<size_t>(1, su.size()));
+        IPO_HIP_CHECK(hipMemsetAsync(dSplitCnt_.get(), 0, std::max<size_t>(1, su.size()) * sizeof(int), s));
+        if (const char* e = std::getenv("IPO_HIP_SPLITK_FUSED")) fused_splitk_ = std::atoi(e) != 0;
+        if (const char* e = std::getenv("IPO_HIP_GATHER_DEPTH")) gather_depth_ = std::atoi(e);
+        if (const char* e = std::getenv("IPO_HIP_TAIL_GATHER_DEPTH")) tail_gather_depth_ = std::atoi(e);
         dPartialTile_.alloc(std::max<size_t>(1, max_part) * (kTileRows * kTileRows + 4 * kTileRows));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
     }
@@ -2000,6 +2044,28 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         };
         build(plan_.utasks, dusrc_);
         if (plan_.nt > 0) build(plan_.tail_tasks, dtsrc_);
+        // per k-slot records of the gather (SlotRec), expanded from the
+        // slot -> task -> source panel indirection
+        auto expand = [&](const std::vector<int>& kslot, const std::vector<TailTask>& ts, DevBuf<SlotRec>& dst) {
+            std::vector<SlotRec> v(kslot.size());
+            for (size_t i = 0; i < kslot.size(); i++) {
+                const int sl = kslot[i];
+                SlotRec& r = v[i];
+                if (sl < 0) { r.rmask = r.cmask = 0; r.roff = 0; r.cdelta = 0; r.dk = 0; continue; }
+                const TailTask& t = ts[sl >> 6];
+                const int kl = sl & 63, d = t.src, ncd = plan_.col0[d + 1] - plan_.col0[d];
+                const int64_t hd = ncd + (plan_.rowptr[d + 1] - plan_.rowptr[d]);
+                r.rmask = t.rmask;
+                r.cmask = t.cmask;
+                r.roff = plan_.off[d] + ncd + kl * hd + t.rbase;
+                r.cdelta = t.cbase - t.rbase;
+                r.dk = plan_.col0[d] + kl;
+            }
+            dst.upload(v, s);
+            IPO_HIP_CHECK(hipStreamSynchronize(s));
+        };
+        expand(plan_.kslot, plan_.utasks, dslot_rec_);
+        if (plan_.nt > 0) expand(plan_.tail_kslot, plan_.tail_tasks, dtail_slot_rec_);
     }
     dutasks_.upload(reinterpret_cast<const uint64_t*>(plan_.utasks.data()), plan_.utasks.size() * 4, s);
     if (plan_.nt > 0) {
@@ -2352,11 +2418,18 @@ bool KktDevice::finish_pass(bool fused) {
         hipLaunchKernelGGL(k_flag_to_scalar, dim3(1), dim3(1), 0, s, dFlags_.get() + 1, dScal_.get() + 2);
         xsum(dScal_.get(), 3, RedOp::Max);
     }
-    IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 3 * sizeof(double), hipMemcpyDeviceToHost, s));
-    IPO_HIP_CHECK(hipMemcpyAsync(hFlags_, dFlags_.get(), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
-    IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 4, dFlags_.get() + 2, sizeof(int), hipMemcpyDeviceToHost, s));
+    // min|d| (and the shards' maxima) and the three flags in one read-back
+    hipLaunchKernelGGL(k_pack_ints, dim3(1), dim3(3), 0, s, dFlags_.get(), 3, dScal_.get() + 3);
+    IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 5 * sizeof(double), hipMemcpyDeviceToHost, s));
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
     IPO_HIP_CHECK(hipStreamSynchronize(s));
+    {
+        int f[3];
+        std::memcpy(f, hScal_ + 3, sizeof(f));
+        hFlags_[0] = f[0];
+        hFlags_[1] = f[1];
+        hFlags_[4] = f[2];
+    }
     if (timing_) {
         float ms = 0;
         IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
@@ -2416,13 +2489,20 @@ void KktDevice::repair_tail() {
 int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, int group, hipStream_t s) {
     const int c0 = ck_ptr_[group], c1 = ck_ptr_[group + 1];
     if (c1 <= c0) return 0;
-    const TailTask* tasks = tail < 0 ? reinterpret_cast<const TailTask*>(dutasks_.get())
-                                     : reinterpret_cast<const TailTask*>(dtail_tasks_.get());
-    const int* kslot = tail < 0 ? dkslot_.get() : dtail_kslot_.get();
-    const TaskSrc* srcs = tail < 0 ? dusrc_.get() : dtsrc_.get();
-    hipLaunchKernelGGL(k_update, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, tasks, srcs, kslot, dck_u_.get(), dck_b_.get(),
-                       dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get());
+    const SlotRec* recs = tail < 0 ? dslot_rec_.get() : dtail_slot_rec_.get();
     const int s0 = sp_ptr_[group], s1 = sp_ptr_[group + 1];
+    // fused: split units combined by their last-arriving chunk (one launch)
+    const bool fused = fused_splitk_ && s1 > s0;
+    // slabs in flight / partials in flight of the combine: deep for the
+    // sparse levels (<= ~2 workgroups per CU), shallow for the many
+    // workgroups of the dense-tail gather (occupancy)
+    const int gd = tail < 0 ? gather_depth_ : tail_gather_depth_;
+    auto kern = gd <= 1 ? k_update<1, 1> : gd == 2 ? k_update<2, 4> : k_update<4, 4>;
+    hipLaunchKernelGGL(kern, dim3(c1 - c0),
+                       dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
+                       dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(), dsp_n_.get(),
+                       fused ? dSplitCnt_.get() : static_cast<int*>(nullptr));
+    if (fused) return 1;
     if (s1 > s0)
         hipLaunchKernelGGL(k_update_reduce, dim3(s1 - s0), dim3(NT), 0, s, pv, tv, tail, dsp_u_.get(), dsp_p0_.get(),
                            dsp_n_.get(), s0, dPartialTile_.get());
@@ -2659,15 +2739,14 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
             j.a[2 * r] = dfx[r]; j.b[2 * r] = nullptr; j.len[2 * r] = n; j.op[2 * r] = 1;
             j.a[2 * r + 1] = dfy[r]; j.b[2 * r + 1] = nullptr; j.len[2 * r + 1] = m; j.op[2 * r + 1] = 1;
         }
-        launch_reduce(j, dPart_.get(), dScal_.get(), s);
-        xsum(dScal_.get(), 2 * R, RedOp::Max);
-        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 2 * R * sizeof(double), hipMemcpyDeviceToHost, s));
+        // read back with the first pass's residuals (no wait of its own)
+        launch_reduce(j, dPart_.get(), dScal_.get() + 8, s);
+        xsum(dScal_.get() + 8, 2 * R, RedOp::Max);
+        IPO_HIP_CHECK(hipMemcpyAsync(hScal_ + 8, dScal_.get() + 8, 2 * R * sizeof(double), hipMemcpyDeviceToHost, s));
     }
-    IPO_HIP_CHECK(hipStreamSynchronize(s));
-    double maxbc[2], rs[2] = {HUGE_VAL, HUGE_VAL}, rs_old[2] = {HUGE_VAL, HUGE_VAL};
+    double maxbc[2] = {0.0, 0.0}, rs[2] = {HUGE_VAL, HUGE_VAL}, rs_old[2] = {HUGE_VAL, HUGE_VAL};
     int pass[2] = {0, 0};
     bool active[2] = {R > 0, R > 1};
-    for (int r = 0; r < R; r++) maxbc[r] = (hScal_[2 * r] > hScal_[2 * r + 1] ? hScal_[2 * r] : hScal_[2 * r + 1]) + 1;
     auto zv = [&](int r) { return dZ_.get() + (size_t)r * T; };
     auto dyv = [&](int r) { return dDy_.get() + (size_t)r * m; };
     auto dxv = [&](int r) { return dDx_.get() + (size_t)r * n; };
@@ -2704,9 +2783,14 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), nq, (1u << nq) - 1u,
                            dScal_.get());
         xsum(dScal_.get(), nq, RedOp::Max);
-        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), nq * sizeof(double), hipMemcpyDeviceToHost, s));
-        IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 2, dIncons_.get(), 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+        // residuals and the consistency flags in one read-back
+        hipLaunchKernelGGL(k_pack_ints, dim3(1), dim3(2), 0, s, dIncons_.get(), 2, dScal_.get() + 6);
+        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 7 * sizeof(double), hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
+        if (pass[0] + pass[1] == 0)
+            for (int r = 0; r < R; r++)
+                maxbc[r] = (hScal_[8 + 2 * r] > hScal_[8 + 2 * r + 1] ? hScal_[8 + 2 * r] : hScal_[8 + 2 * r + 1]) + 1;
+        std::memcpy(hFlags_ + 2, hScal_ + 6, 2 * sizeof(int));
         int q = 0;
         for (int r = 0; r < R; r++) {
             if (!active[r]) continue;
@@ -2724,9 +2808,13 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
         IPO_HIP_CHECK(hipMemcpyAsync(dfy[r], dyv(r), sizeof(double) * m, hipMemcpyDeviceToDevice, s));
         IPO_HIP_CHECK(hipMemcpyAsync(dfx[r], dxv(r), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
     }
-    if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
-    IPO_HIP_CHECK(hipStreamSynchronize(s));
-    if (timing_) { float ms = 0; IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_)); tm_.solve_ms += ms; }
+    if (timing_) {   // otherwise the caller's next read-back orders the copies
+        IPO_HIP_CHECK(hipEventRecord(ev1_, s));
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+        float ms = 0;
+        IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
+        tm_.solve_ms += ms;
+    }
     tm_.solves += R;
     last_passes_ = pass[0] + pass[1];
     for (int r = 0; r < R; r++) ok[r] = incons[r] ? 0 : 1;

@@ -66,6 +66,16 @@ struct TaskSrc {
     int hd, cd0;
 };
 
+// One gather k-slot, resolved on the host (32 B): L(row, k) of the tile's
+// r-th marked row is Lx[roff + popcount(rmask below r)], L(col, k) of its
+// c-th marked column Lx[roff + cdelta + popcount(cmask below c)], d_k = dg[dk].
+// Padding slots: masks 0.
+struct SlotRec {
+    uint64_t rmask, cmask;
+    int64_t roff;
+    int cdelta, dk;
+};
+
 constexpr int kMaxChunkSlots = 512;   // largest split-K chunk of the gather
 
 struct KktPlan {

@@ -97,5 +97,26 @@ int main(int argc, char** argv) {
         }
     std::printf("sparse: units %d slots %ld pad %ld useful MAC %.3g MFMA MAC %.3g (%.1f%%)\n", nu, us, upad, uuse, umf,
                 100.0 * uuse / umf);
+    // per level: units, slots, and the chunking of KktDevice's gather plan
+    // (>= 512 workgroups per launch, chunks of 64 .. kMaxChunkSlots slots)
+    std::printf("level units slots maxslots kmax chunks split_units slabs_per_chunk_max\n");
+    auto level_row = [&](const char* name, int l, int u0, int u1, const std::vector<int>& kptr) {
+        long sumk = 0, mx = 0;
+        for (int u = u0; u < u1; u++) { sumk += kptr[u + 1] - kptr[u]; mx = std::max<long>(mx, kptr[u + 1] - kptr[u]); }
+        long kmax = (sumk / 512 + kSlab - 1) / kSlab * kSlab;
+        kmax = std::max<long>(64, std::min<long>(kMaxChunkSlots, kmax));
+        long ch = 0, sp = 0;
+        for (int u = u0; u < u1; u++) {
+            const long k = kptr[u + 1] - kptr[u];
+            if (!k) continue;
+            const long c = (k + kmax - 1) / kmax;
+            ch += c;
+            sp += c > 1;
+        }
+        std::printf("%s%3d %6d %8ld %6ld %4ld %6ld %5ld %4ld\n", name, l, u1 - u0, sumk, mx, kmax, ch, sp,
+                    std::min(mx, kmax) / kSlab);
+    };
+    for (int l = 1; l < P.nlevels; l++) level_row("L", l, P.unit_level_ptr[l], P.unit_level_ptr[l + 1], P.kslot_ptr);
+    if (P.nt > 0) level_row("T", 0, 0, ntile, P.tail_kslot_ptr);
     return 0;
 }
