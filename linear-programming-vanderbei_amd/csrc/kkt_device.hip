@@ -161,7 +161,6 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
                            bool has_diag, double4_t (&acc)[2][2], double& dabs) {
     __shared__ double As[2][TR][KS + 1];
     __shared__ double Bs[2][TR][KS + 1];
-    __shared__ SlotRec rs[kMaxChunkSlots];
     const int tid = threadIdx.x;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
@@ -172,21 +171,28 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
         for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     dabs = 0.0;
     const int nk = ke - kb, nslab = nk / KS;
-    for (int i = tid; i < nk; i += NT) rs[i] = recs[kb + i];
-    __syncthreads();
     // pipeline: the slot values of GD slabs in flight in a register ring
     // (slab sb + GD issued while slab sb is multiplied; ring entry sb % GD),
-    // LDS double-buffered.  Same products, same MFMA order for every GD.
+    // the wave-uniform records of the next slab to issue one step ahead of
+    // its values (scalar loads, no LDS), LDS double-buffered.  Same
+    // products, same MFMA order for every GD.
     double ra[GD][KS / 4], rb[GD][KS / 4];
     const double* __restrict__ Lx = p.Lx;
     const double* __restrict__ dg = p.dg;
-    auto issue = [&](int slab, double (&xa)[KS / 4], double (&xb)[KS / 4]) {
+    const SlotRec* __restrict__ wrec = recs + kb + wv * (KS / 4);
+    SlotRec mn[KS / 4];
+    auto fetch = [&](int slab) {
 #pragma unroll
-        for (int j = 0; j < KS / 4; j++) slot_vals(rs[slab * KS + wv * (KS / 4) + j], Lx, dg, lane, xa[j], xb[j]);
+        for (int j = 0; j < KS / 4; j++) mn[j] = wrec[slab * KS + j];
+    };
+    auto issue = [&](double (&xa)[KS / 4], double (&xb)[KS / 4]) {
+#pragma unroll
+        for (int j = 0; j < KS / 4; j++) slot_vals(mn[j], Lx, dg, lane, xa[j], xb[j]);
     };
 #pragma unroll
     for (int r = 0; r < GD; r++)
-        if (r < nslab) issue(r, ra[r], rb[r]);
+        if (r < nslab) { fetch(r); issue(ra[r], rb[r]); }
+    if (GD < nslab) fetch(GD);
 #pragma unroll
     for (int j = 0; j < KS / 4; j++) { As[0][lane][wv * (KS / 4) + j] = ra[0][j]; Bs[0][lane][wv * (KS / 4) + j] = rb[0][j]; }
     __syncthreads();
@@ -196,7 +202,10 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
             const int sb = sb0 + ph;
             if (sb >= nslab) break;
             const int cur = sb & 1;
-            if (sb + GD < nslab) issue(sb + GD, ra[ph], rb[ph]);
+            if (sb + GD < nslab) {
+                issue(ra[ph], rb[ph]);
+                if (sb + GD + 1 < nslab) fetch(sb + GD + 1);
+            }
 #pragma unroll
             for (int kk = 0; kk < KS; kk += 4) {
                 double av[2], bv[2];
@@ -329,8 +338,8 @@ __device__ __forceinline__ void split_sum(const double* __restrict__ partial, in
 // k_update_reduce would (MI355X_MICROARCH.md hand-off table row 1:
 // last arriver told by its own add's return value).  It resets the counter
 // for the next factorisation.
-template <int GD, int NF>
-__global__ void __launch_bounds__(NT)
+template <int GD, int NF, int WPE>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
          const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
          const int* __restrict__ ck_part, int c0, double* __restrict__ partial,
@@ -1965,6 +1974,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         if (const char* e = std::getenv("IPO_HIP_SPLITK_FUSED")) fused_splitk_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("IPO_HIP_GATHER_DEPTH")) gather_depth_ = std::atoi(e);
         if (const char* e = std::getenv("IPO_HIP_TAIL_GATHER_DEPTH")) tail_gather_depth_ = std::atoi(e);
+        if (const char* e = std::getenv("IPO_HIP_GATHER_WPE")) gather_wpe_ = std::atoi(e);
         dPartialTile_.alloc(std::max<size_t>(1, max_part) * (kTileRows * kTileRows + 4 * kTileRows));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
     }
@@ -2497,7 +2507,8 @@ int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, i
     // sparse levels (<= ~2 workgroups per CU), shallow for the many
     // workgroups of the dense-tail gather (occupancy)
     const int gd = tail < 0 ? gather_depth_ : tail_gather_depth_;
-    auto kern = gd <= 1 ? k_update<1, 1> : gd == 2 ? k_update<2, 4> : k_update<4, 4>;
+    auto kern = gd <= 1 ? (gather_wpe_ >= 4 ? k_update<1, 1, 4> : k_update<1, 1, 1>)
+                        : gd == 2 ? k_update<2, 4, 1> : k_update<4, 4, 1>;
     hipLaunchKernelGGL(kern, dim3(c1 - c0),
                        dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
                        dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(), dsp_n_.get(),
