@@ -96,7 +96,9 @@ class IpmSolver {
     std::unique_ptr<KktDevice> kkt_;
     DevBuf<double> b_, c_, x_, y_, w_, z_;
     DevBuf<double> rho_, sig_, D_, E_, fx_, fy_, gx_, gy_, dx_, dy_, dz_, dw_;
-    DevBuf<double> part_, scal_, lax_;
+    DevBuf<double> part_, part2_, scal_, lax_;
+    hipStream_t side_ = nullptr;            // mu / residuals beside the factorisation (run_hsd)
+    hipEvent_t ev_step_ = nullptr, ev_side_ = nullptr;
     double* hs_ = nullptr;       // pinned scalars
     bool full_trace_ = false;    // IPO_HIP_TRACE_FULL: full-precision scalars per iteration on stderr
 };

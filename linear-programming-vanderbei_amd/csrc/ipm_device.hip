@@ -43,11 +43,16 @@ __global__ void __launch_bounds__(kResThreads)
 k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
                 const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
                 const double* __restrict__ b, const double* __restrict__ c, const double* __restrict__ x,
-                const double* __restrict__ y, const double* __restrict__ w, const double* __restrict__ z, double phi,
-                double delta, double mu, double* __restrict__ E, double* __restrict__ D, double* __restrict__ fy,
+                const double* __restrict__ y, const double* __restrict__ w, const double* __restrict__ z, double phi_h,
+                double delta, double mu_h, double* __restrict__ E, double* __restrict__ D, double* __restrict__ fy,
                 double* __restrict__ fx, double* __restrict__ gy, double* __restrict__ gx, double* __restrict__ part,
-                int mrow, int mcnt, const double* __restrict__ lax) {
+                int mrow, int mcnt, const double* __restrict__ lax, const double* __restrict__ phimu) {
     __shared__ double sh[kResThreads / 64];
+    // phimu: {phi, mu} computed on the device (the overlapped HSD iteration;
+    // E and D are then written by k_hsd_scaling ahead of the factorisation)
+    const double phi = phimu ? phimu[0] : phi_h;
+    const double mu = phimu ? phimu[1] : mu_h;
+    const bool wde = phimu == nullptr;
     double sr = 0.0, ss = 0.0;
     for (int i = blockIdx.x * kResThreads + threadIdx.x; i < m + n; i += kRedBlocks * kResThreads) {
         if (i < m) {
@@ -58,7 +63,7 @@ k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict
             const double r1 = ax - b[i] * phi + w[i];
             if (i < mcnt) sr += r1 * r1;
             const double rho = -(1 - delta) * r1 + w[i] - delta * mu / y[i];
-            E[i] = w[i] / y[i];
+            if (wde) E[i] = w[i] / y[i];
             fy[i] = rho;
             gy[i] = -b[i];
         } else {
@@ -68,7 +73,7 @@ k_hsd_residuals(int m, int n, const int* __restrict__ kAt, const int* __restrict
             const double s1 = -aty + c[j] * phi + z[j];
             ss += s1 * s1;
             const double sg = -(1 - delta) * s1 + z[j] - delta * mu / x[j];
-            D[j] = z[j] / x[j];
+            if (wde) D[j] = z[j] / x[j];
             fx[j] = -sg;
             gx[j] = -c[j];
         }
@@ -117,6 +122,24 @@ k_step(int m, int n, double theta_h, const double* __restrict__ thetap, double* 
     const int i = blockIdx.x * NT + threadIdx.x;
     if (i < n) { x[i] = x[i] + theta * dx[i]; z[i] = z[i] + theta * dz[i]; }
     else if (i < n + m) { const int j = i - n; y[j] = y[j] + theta * dy[j]; w[j] = w[j] + theta * dw[j]; }
+}
+
+// E = w / y, D = z / x (hsd.c:188-189; the same divisions as k_hsd_residuals)
+__global__ void __launch_bounds__(NT)
+k_hsd_scaling(int m, int n, const double* __restrict__ x, const double* __restrict__ y, const double* __restrict__ w,
+              const double* __restrict__ z, double* __restrict__ E, double* __restrict__ D) {
+    const int i = blockIdx.x * NT + threadIdx.x;
+    if (i < m) E[i] = w[i] / y[i];
+    else if (i < m + n) { const int j = i - m; D[j] = z[j] / x[j]; }
+}
+
+// mu of hsd.c:168 on the device, the host's expression: sc[0..3] = z'x,
+// w'y, c'x, b'y; phi / psi from sc[14..15] (dev != 0) or the arguments;
+// out: sc[6] = phi, sc[7] = mu (the residual kernel's phimu)
+__global__ void k_hsd_mu(double* sc, double denom, double phi_h, double psi_h, int dev) {
+    const double phi = dev ? sc[14] : phi_h, psi = dev ? sc[15] : psi_h;
+    sc[6] = phi;
+    sc[7] = (sc[0] + sc[1] + phi * psi) / denom;
 }
 
 // hsd.c:226-231 on the device (same operations and order as the host code
@@ -332,7 +355,11 @@ IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A
     if (m == 0) b_.alloc(1);
     if (n == 0) c_.alloc(1);
     part_.alloc(8 * kRedBlocks);
+    part2_.alloc(8 * kRedBlocks);
     scal_.alloc(16);
+    IPO_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    IPO_HIP_CHECK(hipEventCreateWithFlags(&ev_step_, hipEventDisableTiming));
+    IPO_HIP_CHECK(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
     lax_.alloc(nforced_ > 0 ? nforced_ : 1);
     IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hs_), 16 * sizeof(double), hipHostMallocDefault));
     IPO_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -340,7 +367,11 @@ IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A
 }
 
 IpmSolver::~IpmSolver() {
+    if (side_) (void)hipStreamSynchronize(side_);
     if (hs_) (void)hipHostFree(hs_);
+    if (ev_step_) (void)hipEventDestroy(ev_step_);
+    if (ev_side_) (void)hipEventDestroy(ev_side_);
+    if (side_) (void)hipStreamDestroy(side_);
     kkt_.reset();
     if (own_stream_) (void)hipStreamDestroy(stream_);
 }
@@ -386,6 +417,10 @@ int IpmSolver::run(const IpmOptions& opt, IpmResult* res) {
 
 int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
     full_trace_ = std::getenv("IPO_HIP_TRACE_FULL") != nullptr;
+    // mu, residuals and right-hand sides on a side stream beside the
+    // factorisation (one GPU, no exchange); IPO_HIP_OVERLAP=0 turns it off
+    bool overlap = xch_ == nullptr;
+    if (const char* e = std::getenv("IPO_HIP_OVERLAP")) overlap = overlap && std::atoi(e) != 0;
     const int m = m_, n = n_;
     hipStream_t s = stream_;
     const int gv = ceil_div(m + n, NT);
@@ -414,14 +449,39 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
         j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = mcnt_; j.op[1] = 0;
         j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
         j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = mcnt_; j.op[3] = 0;
-        launch_reduce(j, part_.get(), scal_.get(), s);
-        xsum(scal_.get(), 4, RedOp::Sum);
-        IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 4 * sizeof(double), hipMemcpyDeviceToHost, s));
-        if (iter > 0) IPO_HIP_CHECK(hipMemcpyAsync(hs_ + 14, scal_.get() + 14, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
-        IPO_HIP_CHECK(hipStreamSynchronize(s));
-        if (iter > 0) { phi = hs_[14]; psi = hs_[15]; }
-        const double mu = (hs_[0] + hs_[1] + phi * psi) / (ng_ + mg_ + 1);
         const double delta = (iter % 2 == 0) ? 0.0 : 1.0;
+        if (overlap) {
+            // side stream: the dots of mu, mu, the residuals and their norms
+            // (device phi / mu) beside the factorisation on the main stream
+            IPO_HIP_CHECK(hipEventRecord(ev_step_, s));
+            IPO_HIP_CHECK(hipStreamWaitEvent(side_, ev_step_, 0));
+            launch_reduce(j, part2_.get(), scal_.get(), side_);
+            hipLaunchKernelGGL(k_hsd_mu, dim3(1), dim3(1), 0, side_, scal_.get(), static_cast<double>(ng_ + mg_ + 1), phi,
+                               psi, iter > 0 ? 1 : 0);
+            hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, side_, m, n, K.kAt(), K.iAt(),
+                               K.At(), K.kA(), K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(),
+                               phi, delta, 0.0, E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(),
+                               part2_.get(), mrow(), mcnt_, lax(), static_cast<const double*>(scal_.get() + 6));
+            hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, side_, part2_.get(), 2, 0u, scal_.get() + 8);
+            IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 16 * sizeof(double), hipMemcpyDeviceToHost, side_));
+            IPO_HIP_CHECK(hipEventRecord(ev_side_, side_));
+            hipLaunchKernelGGL(k_hsd_scaling, dim3(gv), dim3(NT), 0, s, m, n, x_.get(), y_.get(), w_.get(), z_.get(),
+                               E_.get(), D_.get());
+            K.factor(E_.get(), D_.get());    // speculative on the last iteration (mu < 1e-12 found below)
+            IPO_HIP_CHECK(hipEventSynchronize(ev_side_));
+            if (iter > 0) { phi = hs_[14]; psi = hs_[15]; }
+        } else {
+            launch_reduce(j, part_.get(), scal_.get(), s);
+            xsum(scal_.get(), 4, RedOp::Sum);
+            IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 4 * sizeof(double), hipMemcpyDeviceToHost, s));
+            if (iter > 0)
+                IPO_HIP_CHECK(hipMemcpyAsync(hs_ + 14, scal_.get() + 14, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+            IPO_HIP_CHECK(hipStreamSynchronize(s));
+            if (iter > 0) { phi = hs_[14]; psi = hs_[15]; }
+        }
+        const double mu = (hs_[0] + hs_[1] + phi * psi) / (ng_ + mg_ + 1);
+        if (overlap && !(mu == hs_[7] && phi == hs_[6]))
+            throw std::runtime_error("hsd: device mu / phi differ from the host's");
         const double pobj = hs_[2], dobj = hs_[3];
         if (mu < 1.0e-12) {
             if (phi > psi) status = 0;
@@ -430,17 +490,21 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
             else { if (tr) std::fprintf(tr, "Trouble in river city \n"); status = 4; }
             break;
         }
-        link_ax(x_.get());
-        hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
-                           K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), phi, delta, mu,
-                           E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get(), mrow(), mcnt_,
-                           lax());
-        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get());
-        xsum(scal_.get(), 2, RedOp::Sum);
-        IPO_HIP_CHECK(hipMemcpyAsync(hs_ + 8, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+        if (!overlap) {
+            link_ax(x_.get());
+            hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, K.kAt(), K.iAt(), K.At(),
+                               K.kA(), K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), phi,
+                               delta, mu, E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get(),
+                               mrow(), mcnt_, lax(), static_cast<const double*>(nullptr));
+            hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get());
+            xsum(scal_.get(), 2, RedOp::Sum);
+            IPO_HIP_CHECK(hipMemcpyAsync(hs_ + 8, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+            K.factor(E_.get(), D_.get());    // synchronises the stream: hs_[8..9] have landed
+        } else {
+            IPO_HIP_CHECK(hipStreamWaitEvent(s, ev_side_, 0));   // fy fx gy gx before the solves
+        }
         const double gamma = -(1 - delta) * (dobj - pobj + psi) + psi - delta * mu / phi;
 
-        K.factor(E_.get(), D_.get());        // synchronises the stream: hs_[8..9] have landed
         const double normr = std::sqrt(hs_[8]) / phi;
         const double norms = std::sqrt(hs_[9]) / phi;
         if (tr) {
@@ -527,7 +591,7 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
         hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, K.kAt(), K.iAt(), K.At(), K.kA(),
                            K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(), phi, delta, mu,
                            E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(), part_.get(), mrow(), mcnt_,
-                           lax());
+                           lax(), static_cast<const double*>(nullptr));
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get());
         xsum(scal_.get(), 2, RedOp::Sum);
         IPO_HIP_CHECK(hipMemcpyAsync(hs_, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -713,7 +777,8 @@ void vector_bench(int m, int n, const int* kA, const int* iA, const double* A, i
                 hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, dkAt.get(), diAt.get(),
                                    dAt.get(), dkA.get(), diA.get(), dA.get(), col(0) + n, col(1), col(2), col(3) + n,
                                    col(4) + n, col(5), 1.0, 0.5, 0.1, col(6) + n, col(7), col(8) + n, col(9),
-                                   col(10) + n, col(11), part, m, m, static_cast<const double*>(nullptr));
+                                   col(10) + n, col(11), part, m, m, static_cast<const double*>(nullptr),
+                                   static_cast<const double*>(nullptr));
             else if (kq == 1)
                 hipLaunchKernelGGL(k_hsd_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dphi03.get(), 0.5, 0.1, col(9),
                                    col(11), col(8) + n, col(10) + n, col(2), col(5), col(3) + n, col(4) + n, col(7),

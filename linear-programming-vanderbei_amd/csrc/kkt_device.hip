@@ -2142,7 +2142,8 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
 // work items, per-supernode arrival counts and parents.  Called from the
 // constructor after the solve chunks are built.
 void KktDevice::build_sync_free_plan() {
-    constexpr int kSfWidth = 64;
+    int kSfWidth = 64;
+    if (const char* e = std::getenv("IPO_HIP_SF_WIDTH")) kSfWidth = std::max(1, std::atoi(e));
     hipStream_t s = stream_;
     const KktPlan& P = plan_;
     const int ns = P.nsup;
