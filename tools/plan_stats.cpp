@@ -118,5 +118,20 @@ int main(int argc, char** argv) {
     };
     for (int l = 1; l < P.nlevels; l++) level_row("L", l, P.unit_level_ptr[l], P.unit_level_ptr[l + 1], P.kslot_ptr);
     if (P.nt > 0) level_row("T", 0, 0, ntile, P.tail_kslot_ptr);
+    // dense-tail gather slots by the level of their source supernode (the
+    // part a source-level split could gather beside the upper sparse levels)
+    if (P.nt > 0) {
+        std::vector<long> by(P.nlevels + 1, 0);
+        for (int i = 0; i < (int)P.tail_kslot.size(); i++) {
+            const int sl = P.tail_kslot[i];
+            if (sl < 0) continue;
+            by[P.level[P.tail_tasks[sl >> 6].src]]++;
+        }
+        long cum = 0, tot = 0;
+        for (long v : by) tot += v;
+        std::printf("tail slots by source level (cumulative %%):");
+        for (int l = 0; l < P.nlevels; l++) { cum += by[l]; std::printf(" %d:%.0f", l, 100.0 * cum / tot); }
+        std::printf("\n");
+    }
     return 0;
 }
