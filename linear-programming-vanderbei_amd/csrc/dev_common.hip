@@ -51,11 +51,23 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
     const int op = jobs.op[j];
     const int tid = threadIdx.x;
     if (op != 0) {
+        // maxima are order-free: eight loads in flight per thread
         __shared__ double sh[4];
         double acc = 0.0;
-        for (int i = tid; i < len; i += kOrdThreads) {
-            if (op == 1) acc = fmax(acc, ref_abs(a[i]));
-            else acc = fmax(acc, -a[i] / b[i]);
+        for (int i0 = 0; i0 < len; i0 += 8 * kOrdThreads) {
+            double va[8], vb[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = i0 + u * kOrdThreads + tid;
+                va[u] = i < len ? a[i] : 0.0;
+                vb[u] = op == 2 && i < len ? b[i] : 1.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                if (i0 + u * kOrdThreads + tid >= len) continue;
+                if (op == 1) acc = fmax(acc, ref_abs(va[u]));
+                else acc = fmax(acc, -va[u] / vb[u]);
+            }
         }
         acc = block_max(acc, sh);
         if (tid == 0) out[j] = acc;

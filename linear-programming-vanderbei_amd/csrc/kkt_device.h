@@ -193,6 +193,8 @@ class KktDevice {
     bool fused_splitk_ = true;   // IPO_HIP_SPLITK_FUSED=0: separate k_update_reduce launch
     int gather_depth_ = 1;       // slabs of slot values in flight in k_update, sparse levels (IPO_HIP_GATHER_DEPTH = 1, 2, 4; deeper rings cost occupancy and measured slower)
     int tail_gather_depth_ = 1;  // the same for the dense-tail gather (IPO_HIP_TAIL_GATHER_DEPTH)
+    bool eps_cleared_ = false;   // solve_multi's k_perm_in has zeroed the sweep's eps slots
+    bool frag_skip_ = false;     // IPO_HIP_FRAG_SKIP=1: k_update skips 16 x 16 MFMA fragments with only zero products (180 VGPRs, measured slower)
     int gather_wpe_ = 1;         // IPO_HIP_GATHER_WPE=4: depth-1 k_update built for 4 waves per SIMD (<= 128 VGPRs)
     DevBuf<double> dPartialTile_;
     DevBuf<TaskSrc> dusrc_, dtsrc_;   // per gather task: source panel descriptor

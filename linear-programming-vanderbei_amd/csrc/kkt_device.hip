@@ -73,8 +73,10 @@ k_assemble_A(int nz, const double* __restrict__ A, const int64_t* __restrict__ a
 __global__ void __launch_bounds__(NT)
 k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __restrict__ E,
                 const double* __restrict__ D, double eps, const int64_t* __restrict__ dslot,
-                double* __restrict__ Lx, int* __restrict__ live, double* __restrict__ dscale, int tail_from) {
+                double* __restrict__ Lx, int* __restrict__ live, double* __restrict__ dscale, int tail_from,
+                int* __restrict__ flags) {
     const int v = blockIdx.x * NT + threadIdx.x;
+    if (v < 3) flags[v] = 0;      // the factorisation's flags (no fill launch of their own)
     if (v >= T) return;
     const int old = perm[v];
     // columns >= tail_from: replicated linking rows of a non-leading shard,
@@ -156,7 +158,7 @@ __device__ __forceinline__ GatherTile unit_tile(const PlanView& p, const TailVie
 // MFMA accumulation of slots [kb, ke) into this thread's 16 tile entries
 // (acc[a][b][i] = entry (wr + 16a + (lane>>4) + 4i, wc + 16b + (lane&15)))
 // and, for lanes on a diagonal entry, the |terms| of that entry (dabs).
-template <int GD>
+template <int GD, bool FS>
 __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, int kb, int ke, int dcol,
                            bool has_diag, double4_t (&acc)[2][2], double& dabs) {
     __shared__ double As[2][TR][KS + 1];
@@ -185,16 +187,35 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
 #pragma unroll
         for (int j = 0; j < KS / 4; j++) mn[j] = wrec[slab * KS + j];
     };
-    auto issue = [&](double (&xa)[KS / 4], double (&xb)[KS / 4]) {
+    // FS: each wave also publishes which 16-row / 16-column groups of the
+    // tile its k-step (its four slots) touches; a 16 x 16 MFMA fragment
+    // whose row group or column group is untouched by all four slots has
+    // only zero products and is skipped (same sums: acc + 0)
+    __shared__ uint8_t fsum[2][4];
+    uint32_t sm[GD];
+    auto issue = [&](double (&xa)[KS / 4], double (&xb)[KS / 4], uint32_t& smr) {
 #pragma unroll
         for (int j = 0; j < KS / 4; j++) slot_vals(mn[j], Lx, dg, lane, xa[j], xb[j]);
+        if constexpr (FS) {
+            uint64_t rm = 0, cm = 0;
+#pragma unroll
+            for (int j = 0; j < KS / 4; j++) { rm |= mn[j].rmask; cm |= mn[j].cmask; }
+            uint32_t f = 0;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                if ((rm >> (16 * g)) & 0xffffull) f |= 1u << g;
+                if ((cm >> (16 * g)) & 0xffffull) f |= 16u << g;
+            }
+            smr = f;
+        }
     };
 #pragma unroll
     for (int r = 0; r < GD; r++)
-        if (r < nslab) { fetch(r); issue(ra[r], rb[r]); }
+        if (r < nslab) { fetch(r); issue(ra[r], rb[r], sm[r]); }
     if (GD < nslab) fetch(GD);
 #pragma unroll
     for (int j = 0; j < KS / 4; j++) { As[0][lane][wv * (KS / 4) + j] = ra[0][j]; Bs[0][lane][wv * (KS / 4) + j] = rb[0][j]; }
+    if (FS && lane == 0) fsum[0][wv] = static_cast<uint8_t>(sm[0]);
     __syncthreads();
     for (int sb0 = 0; sb0 < nslab; sb0 += GD) {
 #pragma unroll
@@ -203,9 +224,11 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
             if (sb >= nslab) break;
             const int cur = sb & 1;
             if (sb + GD < nslab) {
-                issue(ra[ph], rb[ph]);
+                issue(ra[ph], rb[ph], sm[ph]);
                 if (sb + GD + 1 < nslab) fetch(sb + GD + 1);
             }
+            uint32_t f4 = 0xffffffffu;
+            if constexpr (FS) f4 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(fsum[cur]));
 #pragma unroll
             for (int kk = 0; kk < KS; kk += 4) {
                 double av[2], bv[2];
@@ -213,11 +236,13 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
                 for (int a = 0; a < 2; a++) av[a] = As[cur][wr + a * 16 + li][kk + lk];
 #pragma unroll
                 for (int b = 0; b < 2; b++) bv[b] = Bs[cur][wc + b * 16 + li][kk + lk];
+                const uint32_t f = f4 >> (2 * kk);      // k-step kk / 4's byte
 #pragma unroll
                 for (int a = 0; a < 2; a++)
 #pragma unroll
                     for (int b = 0; b < 2; b++)
-                        acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+                        if (!FS || (((f >> ((wr >> 4) + a)) & 1u) && ((f >> (4 + (wc >> 4) + b)) & 1u)))
+                            acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
             }
             if (has_diag) {
 #pragma unroll
@@ -233,6 +258,7 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
                     As[cur ^ 1][lane][wv * (KS / 4) + j] = ra[nx][j];
                     Bs[cur ^ 1][lane][wv * (KS / 4) + j] = rb[nx][j];
                 }
+                if (FS && lane == 0) fsum[cur ^ 1][wv] = static_cast<uint8_t>(sm[nx]);
             }
             __syncthreads();
         }
@@ -338,7 +364,7 @@ __device__ __forceinline__ void split_sum(const double* __restrict__ partial, in
 // k_update_reduce would (MI355X_MICROARCH.md hand-off table row 1:
 // last arriver told by its own add's return value).  It resets the counter
 // for the next factorisation.
-template <int GD, int NF, int WPE>
+template <int GD, int NF, int WPE, bool FS>
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
          const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
@@ -353,7 +379,7 @@ k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
     const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
     double4_t acc[2][2];
     double dabs;
-    gather_acc<GD>(p, recs, kb, ke, dcol, has_diag, acc, dabs);
+    gather_acc<GD, FS>(p, recs, kb, ke, dcol, has_diag, acc, dabs);
     if (pi < 0) {
         gather_store(g, acc, dabs, has_diag, dcol);
         return;
@@ -1753,8 +1779,11 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
 // z[v] = rhs(perm[v]) with rhs = (fy | fx)
 __global__ void __launch_bounds__(NT)
 k_perm_in(int T, int m, const int* __restrict__ perm, const double* __restrict__ fy, const double* __restrict__ fx,
-          double* __restrict__ z) {
+          double* __restrict__ z, int* __restrict__ zi, double* __restrict__ zd) {
     const int v = blockIdx.x * NT + threadIdx.x;
+    // a pass's first permutation also clears the consistency flags and the
+    // dropped-column eps of its sweep (zi[0..1], zd[0..1]; no fill launches)
+    if (v < 2 && zi) { zi[v] = 0; zd[v] = 0.0; }
     if (v >= T) return;
     const int o = perm[v];
     z[v] = o < m ? fy[o] : fx[o - m];
@@ -1975,6 +2004,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         if (const char* e = std::getenv("IPO_HIP_GATHER_DEPTH")) gather_depth_ = std::atoi(e);
         if (const char* e = std::getenv("IPO_HIP_TAIL_GATHER_DEPTH")) tail_gather_depth_ = std::atoi(e);
         if (const char* e = std::getenv("IPO_HIP_GATHER_WPE")) gather_wpe_ = std::atoi(e);
+        if (const char* e = std::getenv("IPO_HIP_FRAG_SKIP")) frag_skip_ = std::atoi(e) != 0;
         dPartialTile_.alloc(std::max<size_t>(1, max_part) * (kTileRows * kTileRows + 4 * kTileRows));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
     }
@@ -2344,10 +2374,10 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
     const PlanView pv = IPO_VIEW();
     const int nz = static_cast<int>(plan_.amap.size());
     IPO_HIP_CHECK(hipMemsetAsync(dLx_.get(), 0, dLx_.bytes(), s));
-    IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get(), 0, 3 * sizeof(int), s));
     if (nz > 0) hipLaunchKernelGGL(k_assemble_A, dim3(ceil_div(nz, NT)), dim3(NT), 0, s, nz, dA_.get(), damap_.get(), dLx_.get());
     hipLaunchKernelGGL(k_assemble_diag, dim3(ceil_div(T_, NT)), dim3(NT), 0, s, T_, m_, dperm_.get(), dE, dD, epsdiag_,
-                       ddslot_.get(), dLx_.get(), dLive_.get(), dDscale_.get(), shard_minor() ? plan_.tail_c0 : T_);
+                       ddslot_.get(), dLx_.get(), dLive_.get(), dDscale_.get(), shard_minor() ? plan_.tail_c0 : T_,
+                       dFlags_.get());
     const TailView tv = tail_view();
     for (int l = 0; l < plan_.nlevels; l++) {
         const int u0 = plan_.unit_level_ptr[l], u1 = plan_.unit_level_ptr[l + 1];
@@ -2508,8 +2538,9 @@ int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, i
     // sparse levels (<= ~2 workgroups per CU), shallow for the many
     // workgroups of the dense-tail gather (occupancy)
     const int gd = tail < 0 ? gather_depth_ : tail_gather_depth_;
-    auto kern = gd <= 1 ? (gather_wpe_ >= 4 ? k_update<1, 1, 4> : k_update<1, 1, 1>)
-                        : gd == 2 ? k_update<2, 4, 1> : k_update<4, 4, 1>;
+    auto kern = gd <= 1 ? (gather_wpe_ >= 4 ? k_update<1, 1, 4, false>
+                                            : frag_skip_ ? k_update<1, 1, 1, true> : k_update<1, 1, 1, false>)
+                        : gd == 2 ? k_update<2, 4, 1, false> : k_update<4, 4, 1, false>;
     hipLaunchKernelGGL(kern, dim3(c1 - c0),
                        dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
                        dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(), dsp_n_.get(),
@@ -2719,7 +2750,7 @@ void KktDevice::rawsolve(double* dz, int R) {
         launch_reduce(j, dPart_.get(), epsp, s);
         for (int r = 0; r < R; r++) hipLaunchKernelGGL(k_scale_scalar, dim3(1), dim3(1), 0, s, epsp + r, 1.0e-6);
         xsum(epsp, R, RedOp::Max);
-    } else {
+    } else if (!eps_cleared_) {
         IPO_HIP_CHECK(hipMemsetAsync(epsp, 0, R * sizeof(double), s));
     }
     if (plan_.nt > 0 && plan_.ntb > kChainMaxBlocks) {
@@ -2769,13 +2800,18 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
     // right-hand-side slot q of an active system is read back after it
     int incons[2] = {0, 0};
     while (active[0] || active[1]) {
-        IPO_HIP_CHECK(hipMemsetAsync(dIncons_.get(), 0, 2 * sizeof(int), s));
+        bool first = true;
         for (int r = 0; r < R; r++)
-            if (active[r])
+            if (active[r]) {
                 hipLaunchKernelGGL(k_perm_in, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, dperm_.get(),
-                                   pass[r] == 0 ? dfy[r] : ryv(r), pass[r] == 0 ? dfx[r] : rxv(r), zv(r));
+                                   pass[r] == 0 ? dfy[r] : ryv(r), pass[r] == 0 ? dfx[r] : rxv(r), zv(r),
+                                   first ? dIncons_.get() : static_cast<int*>(nullptr), dScal_.get() + 4);
+                first = false;
+            }
+        eps_cleared_ = true;
         if (active[0] && active[1]) rawsolve(zv(0), 2);
         else rawsolve(zv(active[0] ? 0 : 1), 1);
+        eps_cleared_ = false;
         int nq = 0;
         for (int r = 0; r < R; r++) {
             if (!active[r]) continue;

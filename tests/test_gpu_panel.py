@@ -95,3 +95,24 @@ def test_tail_repair_bitwise():
     traces."""
     texts = [_with_env("IPO_HIP_TAIL_REPAIR", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1] for v in ("0", "1")]
     assert texts[0] == texts[1]
+
+
+def _solve_env(var, val):
+    status, text, st = _with_env(var, val, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))
+    return status, text, {k: st[k] for k in sorted(st) if k.startswith("final") or k == "iters"}
+
+
+def test_fused_split_k_bitwise():
+    """Split-K gather units combined by their last-arriving chunk inside
+    k_update (default) against the separate k_update_reduce launch
+    (IPO_HIP_SPLITK_FUSED=0): the same partial sums in chunk order, so the
+    dfl001 HSD solves agree to the last bit of the final iterate's values."""
+    assert _solve_env("IPO_HIP_SPLITK_FUSED", "0") == _solve_env("IPO_HIP_SPLITK_FUSED", "1")
+
+
+def test_hsd_overlap_bitwise():
+    """mu, residuals and right-hand sides on a side stream beside the
+    factorisation (default) against the sequential iteration
+    (IPO_HIP_OVERLAP=0): the device mu / phi / psi / theta are the host's
+    operations in the host's order, so the solves are identical."""
+    assert _solve_env("IPO_HIP_OVERLAP", "0") == _solve_env("IPO_HIP_OVERLAP", "1")
