@@ -1848,6 +1848,19 @@ k_min_abs_partial(const double* __restrict__ d, int T, double* __restrict__ part
 }
 
 __global__ void k_scale_scalar(double* e, double f) { e[0] *= f; }
+// dst[2r] <- src[2r] (m values), dst[2r+1] <- src[2r+1] (n values), r < R
+struct CopyOut {
+    const double* src[4];
+    double* dst[4];
+    int m, n, R;
+};
+__global__ void __launch_bounds__(NT) k_copy_out(CopyOut c) {
+    const int i = blockIdx.x * NT + threadIdx.x, per = c.m + c.n;
+    if (i >= c.R * per) return;
+    const int r = i / per, k = i - r * per;
+    if (k < c.m) c.dst[2 * r][k] = c.src[2 * r][k];
+    else c.dst[2 * r + 1][k - c.m] = c.src[2 * r + 1][k - c.m];
+}
 // n ints copied bit for bit into the doubles at out (one host read-back with them)
 __global__ void k_pack_ints(const int* f, int n, double* out) {
     if (static_cast<int>(threadIdx.x) < n) reinterpret_cast<int*>(out)[threadIdx.x] = f[threadIdx.x];
@@ -2782,10 +2795,9 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
             j.a[2 * r] = dfx[r]; j.b[2 * r] = nullptr; j.len[2 * r] = n; j.op[2 * r] = 1;
             j.a[2 * r + 1] = dfy[r]; j.b[2 * r + 1] = nullptr; j.len[2 * r + 1] = m; j.op[2 * r + 1] = 1;
         }
-        // read back with the first pass's residuals (no wait of its own)
+        // read back with the first pass's residuals (no copy or wait of its own)
         launch_reduce(j, dPart_.get(), dScal_.get() + 8, s);
         xsum(dScal_.get() + 8, 2 * R, RedOp::Max);
-        IPO_HIP_CHECK(hipMemcpyAsync(hScal_ + 8, dScal_.get() + 8, 2 * R * sizeof(double), hipMemcpyDeviceToHost, s));
     }
     double maxbc[2] = {0.0, 0.0}, rs[2] = {HUGE_VAL, HUGE_VAL}, rs_old[2] = {HUGE_VAL, HUGE_VAL};
     int pass[2] = {0, 0};
@@ -2833,7 +2845,8 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
         xsum(dScal_.get(), nq, RedOp::Max);
         // residuals and the consistency flags in one read-back
         hipLaunchKernelGGL(k_pack_ints, dim3(1), dim3(2), 0, s, dIncons_.get(), 2, dScal_.get() + 6);
-        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 7 * sizeof(double), hipMemcpyDeviceToHost, s));
+        IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), (pass[0] + pass[1] == 0 ? 8 + 2 * R : 7) * sizeof(double),
+                                     hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         if (pass[0] + pass[1] == 0)
             for (int r = 0; r < R; r++)
@@ -2849,13 +2862,20 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
             active[r] = rs[r] > 1.0e-10 * maxbc[r] && rs[r] < rs_old[r] / 2;
         }
     }
+    CopyOut co{};
     for (int r = 0; r < R; r++) {
         if (rs[r] > rs_old[r] && pass[r] > 1)
             hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), zv(r), dyv(r),
                                dxv(r), 2);
-        IPO_HIP_CHECK(hipMemcpyAsync(dfy[r], dyv(r), sizeof(double) * m, hipMemcpyDeviceToDevice, s));
-        IPO_HIP_CHECK(hipMemcpyAsync(dfx[r], dxv(r), sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+        co.src[2 * r] = dyv(r); co.dst[2 * r] = dfy[r];
+        co.src[2 * r + 1] = dxv(r); co.dst[2 * r + 1] = dfx[r];
     }
+    // the solutions back into the callers' vectors: one launch for all
+    // 2R copies (four copy-engine calls cost four host round trips)
+    co.m = m;
+    co.n = n;
+    co.R = R;
+    if (R > 0 && m + n > 0) hipLaunchKernelGGL(k_copy_out, dim3(ceil_div(R * (m + n), NT)), dim3(NT), 0, s, co);
     if (timing_) {   // otherwise the caller's next read-back orders the copies
         IPO_HIP_CHECK(hipEventRecord(ev1_, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
