@@ -116,3 +116,10 @@ def test_hsd_overlap_bitwise():
     (IPO_HIP_OVERLAP=0): the device mu / phi / psi / theta are the host's
     operations in the host's order, so the solves are identical."""
     assert _solve_env("IPO_HIP_OVERLAP", "0") == _solve_env("IPO_HIP_OVERLAP", "1")
+
+
+def test_frag_skip_bitwise():
+    """The gather's optional MFMA fragment skip (IPO_HIP_FRAG_SKIP=1: 16 x 16
+    fragments whose row or column group no slot of the k-step touches are not
+    issued) adds only exact zeros when on: identical dfl001 HSD solves."""
+    assert _solve_env("IPO_HIP_FRAG_SKIP", "0") == _solve_env("IPO_HIP_FRAG_SKIP", "1")
