@@ -405,6 +405,7 @@ int IpmSolver::run(const IpmOptions& opt, IpmResult* res) {
     *res = IpmResult();
     res->t_setup_s = t_setup_;
     kkt_->enable_timing(opt.timing);
+    kkt_->set_epsdiag(1.0e-14);   // ldlt.c:31: every solve starts from the reference's eps_diag
     const double t0 = now_s();
     const int st = opt.method == Method::Intpt   ? run_intpt(opt, res)
                    : opt.method == Method::Hsdls ? run_hsdls(opt, res)
