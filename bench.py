@@ -52,8 +52,8 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 METRIC = "IPM iterations/sec (ADA^T factor+solve) on netlib dfl001; duality gap ≤1e-8"
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, AMD spec (the guide has no fp64 row)
-PHASE_KERNELS = {"gather": "k_update+k_update_reduce",
-                 "diag": "k_panel_w|k_panel_s|k_tail_pr|k_panel|k_diag|k_tail_diag_coop", "trsm": "k_trsm",
+PHASE_KERNELS = {"gather": "k_update",
+                 "diag": "k_panel_w|k_panel_s|k_tail_pr|k_diag|k_tail_diag_coop", "trsm": "k_trsm",
                  "tail_syrk": "k_tail_syrk",
                  "forward": "k_forward|k_fwd_diag|k_fwd_gemv|k_fwd_sf|k_tail_gather|k_tail_fwd|k_tail_fwd_chain",
                  "backward": "k_backward|k_bwd_partial|k_bwd_finish|k_bwd_sf|k_tail_dscale|k_tail_bwd|k_tail_bwd_chain"}
@@ -66,65 +66,35 @@ def dist_env():
 
 
 class Dist:
-    """barrier / max-reduce over ranks; a no-op for a single process."""
+    """barrier / max / min / sum over ranks and rank 0's bytes everywhere,
+    through ipo_amd.hostcomm (TCP star around rank 0; no torch in the
+    process, see hostcomm's docstring); a no-op for a single process."""
 
-    def __init__(self, backend=None):
+    def __init__(self):
+        from ipo_amd.hostcomm import HostComm
         self.rank, self.world, self.local = dist_env()
-        self.dist = None
-        if self.world > 1:
-            import torch
-            import torch.distributed as dist
-            if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
-            if backend == "nccl":
-                torch.cuda.set_device(self.local)
-            dist.init_process_group(backend=backend)
-            self.dist, self.torch, self.backend = dist, torch, backend
-
-    def _t(self, v):
-        t = self.torch.tensor([float(v)], dtype=self.torch.float64)
-        return t.cuda() if self.backend == "nccl" else t
+        self.comm = HostComm(self.rank, self.world)
 
     def barrier(self):
-        if self.dist:
-            self.dist.all_reduce(self._t(0.0))
+        self.comm.barrier()
 
     def max(self, v):
-        if not self.dist:
-            return v
-        t = self._t(v)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return self.comm.reduce_scalar(v, "max")
 
     def min(self, v):
-        if not self.dist:
-            return v
-        t = self._t(v)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
-        return float(t.item())
+        return self.comm.reduce_scalar(v, "min")
 
     def sum(self, v):
-        if not self.dist:
-            return v
-        t = self._t(v)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+        return self.comm.reduce_scalar(v, "sum")
 
     def bcast_bytes(self, data, n):
         """rank 0's n bytes on every rank"""
-        if not self.dist:
-            return data
-        t = self.torch.zeros(n, dtype=self.torch.uint8)
-        if self.rank == 0:
-            t.copy_(self.torch.frombuffer(bytearray(data), dtype=self.torch.uint8))
-        if self.backend == "nccl":
-            t = t.cuda()
-        self.dist.broadcast(t, 0)
-        return bytes(t.cpu().numpy().tobytes())
+        out = self.comm.bcast_bytes(bytes(data) if self.rank == 0 else None)
+        assert len(out) == n
+        return out
 
     def close(self):
-        if self.dist:
-            self.dist.destroy_process_group()
+        self.comm.close()
 
 
 def timed_replicas(d: Dist, run_step_block, sync):
@@ -157,7 +127,6 @@ def block_angular_leg(d, args, sync):
     t_gen = time.perf_counter() - t0
     uid = None
     if d.world > 1:
-        ipo_amd.set_device(d.local)
         uid = d.bcast_bytes(ipo_amd.rccl_unique_id() if d.rank == 0 else None, 128)
     ctx = ipo_amd.ShardContext(loc, d.world, d.rank, rccl_id=uid)
     try:
@@ -260,13 +229,31 @@ def cpu_baseline(mps, iters):
             "host_cpus": os.cpu_count()}
 
 
+def end_to_end(p, golden, sync):
+    """SURVEY.md 8(d)'s literal definition: wall time from solver() entry to
+    return (ipo_hip_solve, the same solve_impl as the `solver` symbol:
+    host symbolic analysis, upload, the HSD loop, download), divided by the
+    iterations printed.  One call, problem on the host at entry."""
+    import ipo_amd
+    sync()
+    t0 = time.perf_counter()
+    r = ipo_amd.solver(p, "hsd")
+    el = time.perf_counter() - t0
+    st = r["stats"]
+    ok = r["status"] == 0 and (golden is None or abs(st["iters"] - golden) <= 1)
+    return {"definition": "solver() entry to return (symbolic + upload + solve + download), host arrays in",
+            "value": st["iters"] / el if ok else None, "unit": "iterations/s", "seconds": el,
+            "iterations": st["iters"], "setup_s": st["t_setup_s"], "solve_s": st["t_solve_s"],
+            "status": ipo_amd.STATUS_TEXT.get(r["status"], r["status"])}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5, help="timed steps: complete HSD solves to convergence (117 iterations each on dfl001)")
     ap.add_argument("--warmup", type=int, default=1, help="untimed complete solves before the timed ones")
     ap.add_argument("--problem", default="dfl001")
-    ap.add_argument("--cpu-iters", type=int, default=3, help="HSD iterations of the CPU oracle sample (0 = skip)")
+    ap.add_argument("--cpu-iters", type=int, default=8, help="HSD iterations of the CPU oracle sample (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="skip the instrumented second solve (no roofline)")
     ap.add_argument("--block-angular", choices=["on", "off"], default="on",
                     help="also run BASELINE configs[4] sharded over the ranks (reported under block_angular)")
@@ -281,15 +268,9 @@ def main():
     import ipo_amd
     from conftest import mps_path
     ipo_amd.require_gpu()
-    try:
-        import torch
-        if torch.cuda.is_available():
-            torch.cuda.set_device(d.local)
-            sync = torch.cuda.synchronize
-        else:
-            sync = lambda: None  # noqa: E731
-    except ImportError:
-        sync = lambda: None  # noqa: E731
+    if d.world > 1:
+        ipo_amd.set_device(d.local)       # one process per GPU
+    sync = ipo_amd.device_synchronize
 
     path = mps_path(args.problem)
     p = ipo_amd.load_mps(path)
@@ -380,6 +361,11 @@ def main():
         except Exception as e:  # the GPU number stands on its own
             out["cpu_baseline"] = {"error": str(e)}
     ctx.close()
+    if d.rank == 0:
+        try:
+            out["end_to_end"] = end_to_end(p, golden, sync)
+        except Exception as e:  # noqa: BLE001 -- the headline number stands on its own
+            out["end_to_end"] = {"error": repr(e)}
     if args.hbm == "on" and d.rank == 0:
         try:
             out["hbm_roofline"] = hbm_roofline_leg(20)

@@ -180,6 +180,9 @@ int ipo_hip_synth_block_angular(int nblocks, int mb, int nb, int per_col, int ba
                                 double *b, double *c, double *xs, double *ys, double *ws, double *zs);
 
 int ipo_hip_device_count(void);
+/* hipDeviceSynchronize on the calling thread's device (bench.py brackets its
+ * timed region with it); 0 on success. */
+int ipo_hip_device_synchronize(void);
 const char *ipo_hip_last_error(void);
 const char *ipo_hip_version(void);
 

@@ -532,6 +532,15 @@ int ipo_hip_device_count(void) {
     return n;
 }
 
+int ipo_hip_device_synchronize(void) {
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        set_err(std::string("hipDeviceSynchronize: ") + hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
 const char* ipo_hip_last_error(void) { return g_err.c_str(); }
 const char* ipo_hip_version(void) { return "ipo-hip 0.1 (gfx950)"; }
 

@@ -14,6 +14,8 @@
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
+#include <exception>
 #include <stdexcept>
 #include <vector>
 
@@ -405,6 +407,7 @@ int IpmSolver::run(const IpmOptions& opt, IpmResult* res) {
     *res = IpmResult();
     res->t_setup_s = t_setup_;
     kkt_->enable_timing(opt.timing);
+    kkt_->reset_timers();         // the counters and phase times of this solve only
     kkt_->set_epsdiag(1.0e-14);   // ldlt.c:31: every solve starts from the reference's eps_diag
     const double t0 = now_s();
     const int st = opt.method == Method::Intpt   ? run_intpt(opt, res)
@@ -451,6 +454,8 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
         j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
         j.a[3] = b_.get(); j.b[3] = y_.get(); j.len[3] = mcnt_; j.op[3] = 0;
         const double delta = (iter % 2 == 0) ? 0.0 : 1.0;
+        KktDevice::HostState spec{};
+        std::exception_ptr spec_err;
         if (overlap) {
             // side stream: the dots of mu, mu, the residuals and their norms
             // (device phi / mu) beside the factorisation on the main stream
@@ -468,7 +473,16 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
             IPO_HIP_CHECK(hipEventRecord(ev_side_, side_));
             hipLaunchKernelGGL(k_hsd_scaling, dim3(gv), dim3(NT), 0, s, m, n, x_.get(), y_.get(), w_.get(), z_.get(),
                                E_.get(), D_.get());
-            K.factor(E_.get(), D_.get());    // speculative on the last iteration (mu < 1e-12 found below)
+            // speculative: the host learns mu (and so whether hsd.c:155 stops
+            // here, where the reference does not factor) only after it; its
+            // host-side effects are undone and an error it raised is held
+            // back unless the iteration goes on to use the factor
+            spec = K.host_state();
+            try {
+                K.factor(E_.get(), D_.get());
+            } catch (...) {
+                spec_err = std::current_exception();
+            }
             IPO_HIP_CHECK(hipEventSynchronize(ev_side_));
             if (iter > 0) { phi = hs_[14]; psi = hs_[15]; }
         } else {
@@ -481,10 +495,13 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
             if (iter > 0) { phi = hs_[14]; psi = hs_[15]; }
         }
         const double mu = (hs_[0] + hs_[1] + phi * psi) / (ng_ + mg_ + 1);
-        if (overlap && !(mu == hs_[7] && phi == hs_[6]))
+        // the device's mu / phi must be the host's bit for bit (NaNs included:
+        // a diverging solve then takes the sequential path's status route)
+        if (overlap && (std::memcmp(&mu, &hs_[7], sizeof mu) != 0 || std::memcmp(&phi, &hs_[6], sizeof phi) != 0))
             throw std::runtime_error("hsd: device mu / phi differ from the host's");
         const double pobj = hs_[2], dobj = hs_[3];
         if (mu < 1.0e-12) {
+            if (overlap) K.restore_host_state(spec);     // the speculative factorisation is not used
             if (phi > psi) status = 0;
             else if (dobj < 0.0) status = 2;
             else if (pobj > 0.0) status = 4;
@@ -502,6 +519,7 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
             IPO_HIP_CHECK(hipMemcpyAsync(hs_ + 8, scal_.get(), 2 * sizeof(double), hipMemcpyDeviceToHost, s));
             K.factor(E_.get(), D_.get());    // synchronises the stream: hs_[8..9] have landed
         } else {
+            if (spec_err) std::rethrow_exception(spec_err);
             IPO_HIP_CHECK(hipStreamWaitEvent(s, ev_side_, 0));   // fy fx gy gx before the solves
         }
         const double gamma = -(1 - delta) * (dobj - pobj + psi) + psi - delta * mu / phi;

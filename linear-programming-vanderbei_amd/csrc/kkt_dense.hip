@@ -460,195 +460,17 @@ k_tail_diag_coop(PlanView p, TailView tv, int kb, double* __restrict__ gmax, int
 
 // ------------------------------------------------------------ fused panel
 // Diagonal block and the rows below it in one launch: the fast path of
-// k_diag + k_trsm.  Workgroup j of a panel (512 threads, 8 waves) holds
-//   half 0 (waves 0-3): panel rows 0..63 -- the diagonal block and, on a
-//          sparse panel with nc < 64, the first rows of R_s -- factored
-//          right-looking as factor_diag_fast does it;
-//   half 1 (waves 4-7): panel rows 64 (j + 1) .. 64 (j + 1) + 63, solved
-//          against the diagonal block column by column while it is factored.
-// Thread (row = lane, part q0 = wave & 3) keeps the entries (row, 4q + q0).
-// Every workgroup of a panel factors the diagonal block redundantly (same
-// data, same code, bitwise the same result), so no workgroup waits for
-// another; workgroup 0 stores it.  One barrier per column: before it the
-// pivot wave of half 0 publishes l(., k) and l(., k) d_k, and the half-1
-// wave owning column k publishes its rows' a(row, k); after it every half-1
-// wave forms l(row, k) = a(row, k) / d_k itself.  Per entry the operations
-// and their order are those of factor_diag_fast and solve_rows (reference
-// form l = w / d, w -= l (l11 d)), so the factor is bitwise the one of the
-// two-kernel path.  A pivot that fails the zero test stops every workgroup
-// of the panel before it writes anything and raises flags[1]: the host then
-// redoes the whole factorisation with k_diag / k_trsm, which own the
-// dependent-pivot rule (ldlt.c:600-614).
+// k_diag + k_trsm (k_panel_w below).  A pivot that fails the zero test stops
+// every workgroup of the panel before it writes anything and raises
+// flags[1]: the host then redoes the factorisation with k_diag / k_trsm,
+// which own the dependent-pivot rule (ldlt.c:600-614).  (Round 1's 8-wave
+// one-barrier-per-column k_panel, bitwise the same, measured slower and is
+// gone.)
 constexpr int PNT = 512;
 
-__global__ void __launch_bounds__(PNT)
-k_panel(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j, int f0, TailView tv, int kb) {
-    __shared__ double colk[2][PC];        // l(r, k) of half 0's rows
-    __shared__ double cold[3][PC];        // l(c, k) d_k
-    __shared__ double colk1[2][PC];       // l(row, k) of half 1's rows
-    __shared__ int tinys[2];
-    __shared__ double dv[PC];
-    __shared__ double B[PC][PC + 1];
-    double* panel;
-    double* wbuf = nullptr;
-    int ld, nc, h, c0, j;
-    if (fu_sup) {
-        const int s = fu_sup[f0 + blockIdx.x];
-        j = fu_j[f0 + blockIdx.x];
-        c0 = p.col0[s];
-        nc = p.col0[s + 1] - c0;
-        h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
-        ld = h;
-        panel = p.Lx + p.off[s];
-    } else {
-        const int k0 = kb * PC;
-        j = blockIdx.x;
-        nc = min(PC, tv.nt - k0);
-        h = tv.nt - k0;
-        ld = tv.nt;
-        c0 = tv.tc + k0;
-        panel = tv.S + k0 + (size_t)k0 * tv.nt;
-        wbuf = tv.W;                      // rows relative to the block column, ld nt
-    }
-    // wave index through readfirstlane: the compiler then knows it (and every
-    // branch on it) to be wave-uniform -- scalar branches instead of EXEC masks
-    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), q0 = wv & 3;
-    const bool h1 = wv >= 4;
-    const int h0 = min(PC, h);                      // half 0's rows
-    const int row = h1 ? TR * (j + 1) + lane : lane;
-    const bool rok = h1 ? row < h : row < h0;
-    double a[16];
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const int c = 4 * q + q0;
-        const bool ok = rok && c < nc && c <= row;
-        const double t = panel[ok ? row + (size_t)c * ld : 0];
-        a[q] = ok ? t : 0.0;
-    }
-    double dsc = (!h1 && lane < nc && (lane & 3) == q0) ? p.dscale[c0 + lane] : 0.0;
-    // Software pipeline, one barrier per column k:
-    //  * half 0 publishes pivot k one iteration early: the wave owning
-    //    column k + 1 forms it right after its step-k update, in the same
-    //    straight-line code as the rest of that update (all waves compute it,
-    //    the owner publishes), so the division overlaps the update;
-    //  * half 1 lags one step: in iteration k it applies step k - 1 (with the
-    //    l(row, k - 1) its owner wave published) and the owner of column k
-    //    forms l(row, k) = a(row, k) / d_k for the next iteration.
-    // cold[] is read by half 0 in iteration k and by half 1 in k + 1 while
-    // pivot k + 2 is being written: three buffers.
-    bool tiny = false;
-    if (!h1 && q0 == 0) {                 // pivot 0
-        const double dk = lane_bcast(a[0], 0);
-        const double dsk = lane_bcast(dsc, 0);
-        const bool tz = fabs(dk) <= p.tau * dsk;
-        const bool below = !tz && lane > 0 && lane < h0;
-        const double l = below ? a[0] / dk : 0.0;
-        if (below) a[0] = l;
-        colk[0][lane] = l;
-        cold[0][lane] = l * dk;
-        if (lane == 0) { tinys[0] = tz; dv[0] = dk; }
-    }
-#pragma unroll
-    for (int qk = 0; qk < 16; qk++) {
-        for (int pk = 0; pk < 4; pk++) {
-            const int k = 4 * qk + pk;
-            if (k >= nc || tiny) break;
-            __syncthreads();
-            const int b2 = k & 1, b3 = k % 3;
-            // every LDS read of the step is issued before the zero-pivot
-            // branch: one LDS round trip per column instead of two.  Half 1
-            // applies step k - 1 (cold buffer (k - 1) mod 3).
-            const double lr = h1 ? colk1[b2 ^ 1][lane] : colk[b2][lane];
-            double ck[16];
-#pragma unroll
-            for (int q = qk; q < 16; q++) ck[q] = cold[h1 ? (k + 2) % 3 : b3][4 * q + q0];
-            const double cr = cold[b3][lane];
-            const double dvk = dv[k];
-            const int tzk = tinys[b2];
-            if (tzk) { tiny = true; break; }
-            const int kn = k + 1;
-            const bool own_next = kn < nc && q0 == (kn & 3);
-            if (!h1) {
-                // step k on rows > k.  Rows <= k read l = 0 and only touch
-                // entries right of their diagonal, which nothing reads.
-                a[qk] = q0 > pk ? a[qk] - lr * ck[qk] : a[qk];      // column 4 qk + q0 > k
-#pragma unroll
-                for (int q = qk + 1; q < 16; q++) a[q] = a[q] - lr * ck[q];
-                dsc = (lane & 3) == q0 ? dsc + fabs(lr * cr) : dsc;   // |term| of the diagonal entry
-                // pivot k + 1 (column kn: register qk in wave pk + 1, or qk + 1 in wave 0)
-                const double an = pk < 3 ? a[qk] : a[qk < 15 ? qk + 1 : qk];
-                const int kl = kn < 64 ? kn : 63;
-                const double dk = lane_bcast(an, kl);
-                const double dsk = lane_bcast(dsc, kl);
-                const bool tz = fabs(dk) <= p.tau * dsk;
-                const bool below = !tz && lane > kn && lane < h0;
-                const double l = below ? an / dk : 0.0;
-                if (own_next) {
-                    if (pk < 3) a[qk] = below ? l : a[qk];
-                    else if (qk < 15) a[qk + 1] = below ? l : a[qk + 1];
-                    colk[b2 ^ 1][lane] = l;
-                    cold[kn % 3][lane] = l * dk;
-                    if (lane == 0) { tinys[b2 ^ 1] = tz; dv[kn] = dk; }
-                }
-            } else {
-                if (k > 0) {                  // step k - 1 on columns > k - 1
-                    a[qk] = q0 >= pk ? a[qk] - lr * ck[qk] : a[qk];
-#pragma unroll
-                    for (int q = qk + 1; q < 16; q++) a[q] = a[q] - lr * ck[q];
-                }
-                // l(row, k) = a(row, k) / d_k by the owner of column k
-                const double l = rok ? a[qk] / dvk : 0.0;
-                if (q0 == pk) {
-                    a[qk] = l;
-                    colk1[b2][lane] = l;
-                }
-            }
-        }
-    }
-    if (tiny) {
-        if (tid == 0) atomicOr(&p.flags[1], 1);
-        return;
-    }
-    // half 1: its rows of L21 (and W = L21 D on the dense tail)
-    if (h1 && rok) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const int c = 4 * q + q0;
-            if (c < nc) {
-                panel[row + (size_t)c * ld] = a[q];
-                if (wbuf) wbuf[row + (size_t)c * ld] = a[q] * dv[c];
-            }
-        }
-    }
-    if (j != 0) return;
-    // workgroup 0, half 0: rows of R_s inside the first 64 rows, then L11'
-    // into the upper slot through an LDS transpose, D and mark
-    if (!h1 && lane >= nc && lane < h0) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const int c = 4 * q + q0;
-            if (c < nc) {
-                panel[lane + (size_t)c * ld] = a[q];
-                if (wbuf) wbuf[lane + (size_t)c * ld] = a[q] * dv[c];
-            }
-        }
-    }
-    __syncthreads();
-    if (!h1) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) B[lane][4 * q + q0] = a[q];
-    }
-    __syncthreads();
-    if (!h1) {
-        for (int rr = q0; rr < nc; rr += 4)
-            if (lane < rr) panel[lane + (size_t)rr * ld] = B[rr][lane];
-    }
-    if (tid < nc) { p.dg[c0 + tid] = dv[tid]; p.live[c0 + tid] = 1; }
-}
-
 // ------------------------------------------------------- windowed panel
-// The same fused diagonal block + panel rows as k_panel, with the column
-// chain cut into four 16-column windows instead of 64 barrier steps.  Wave
+// Fused diagonal block + panel rows, the column chain cut into four
+// 16-column windows (one workgroup barrier per window).  Wave
 // w of half 0 (waves 0-3) keeps window w (columns 16w..16w+15) of the
 // block's 64 rows, wave w of half 1 (waves 4-7) window w of tile j + 1.
 // Phase t (one workgroup barrier each):
@@ -1273,8 +1095,6 @@ k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count) {
 
 }  // namespace
 
-int g_panel_kind = 2;
-
 void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const double* Wprev, double* Wcur,
                       hipStream_t s) {
     const int h = tv.nt - t * PC;
@@ -1312,16 +1132,13 @@ void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, 
 
 void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,
                   int kb, hipStream_t s) {
-    const bool w = g_panel_kind == 2;
     if (fu_sup) {
         if (count <= 0) return;
-        if (w) hipLaunchKernelGGL(k_panel_w, dim3(count), dim3(PNT), 0, s, pv, fu_sup, fu_j, f0, tv, -1);
-        else hipLaunchKernelGGL(k_panel, dim3(count), dim3(PNT), 0, s, pv, fu_sup, fu_j, f0, tv, -1);
+        hipLaunchKernelGGL(k_panel_w, dim3(count), dim3(PNT), 0, s, pv, fu_sup, fu_j, f0, tv, -1);
     } else {
         const int h = tv.nt - kb * PC;
         const int g = std::max(1, (h + TR - 1) / TR - 1);
-        if (w) hipLaunchKernelGGL(k_panel_w, dim3(g), dim3(PNT), 0, s, pv, nullptr, nullptr, 0, tv, kb);
-        else hipLaunchKernelGGL(k_panel, dim3(g), dim3(PNT), 0, s, pv, nullptr, nullptr, 0, tv, kb);
+        hipLaunchKernelGGL(k_panel_w, dim3(g), dim3(PNT), 0, s, pv, nullptr, nullptr, 0, tv, kb);
     }
 }
 

@@ -87,6 +87,18 @@ class KktDevice {
     // One unrefined sweep L D L' z = rhs on R permuted device vectors at dz + r K.
     void rawsolve(double* dz, int R = 1);
 
+    // What a factorisation changes on the host side (eps_diag growth,
+    // dependent-pivot count, timers and counters): saved before a
+    // speculative factorisation and put back when the caller ends up not
+    // using it (the overlapped HSD iteration that finds mu < 1e-12).
+    struct HostState {
+        double epsdiag;
+        int ndep;
+        KktTimers tm;
+    };
+    HostState host_state() const { return {epsdiag_, ndep_, tm_}; }
+    void restore_host_state(const HostState& h) { epsdiag_ = h.epsdiag; ndep_ = h.ndep; tm_ = h.tm; }
+
     double epsdiag() const { return epsdiag_; }
     void set_pivot_tolerance(double t) { pivot_tol_ = t; }
     void set_epsdiag(double e) { epsdiag_ = e; }
@@ -95,6 +107,7 @@ class KktDevice {
     int last_passes() const { return last_passes_; }
     const KktTimers& timers() const { return tm_; }
     void enable_timing(bool on) { timing_ = on; }
+    void reset_timers() { tm_ = KktTimers(); }
 
     // Diagnostics: copy numeric factor to host (panels + D), for tests.
     void download_factor(double* lx, double* d) const;
@@ -102,6 +115,9 @@ class KktDevice {
     double* device_diag() const { return dDg_.get(); }
 
   private:
+    void factor_core(const double* dE, const double* dD);
+    void dump_factor(const double* dE, const double* dD, double eps_in);
+    int dump_count_ = 0;
     TailView tail_view() const;
     template <int R>
     void sweep(double* dz, const double* epsp);
@@ -190,12 +206,7 @@ class KktDevice {
     DevBuf<int> dck_u_, dck_b_, dck_e_, dck_part_, dsp_u_, dsp_p0_, dsp_n_;
     DevBuf<int> dck_q_;          // split-unit index of each chunk (-1: unsplit)
     DevBuf<int> dSplitCnt_;      // arrival counters of the split units (fused split-K), zero between launches
-    bool fused_splitk_ = true;   // IPO_HIP_SPLITK_FUSED=0: separate k_update_reduce launch
-    int gather_depth_ = 1;       // slabs of slot values in flight in k_update, sparse levels (IPO_HIP_GATHER_DEPTH = 1, 2, 4; deeper rings cost occupancy and measured slower)
-    int tail_gather_depth_ = 1;  // the same for the dense-tail gather (IPO_HIP_TAIL_GATHER_DEPTH)
     bool eps_cleared_ = false;   // solve_multi's k_perm_in has zeroed the sweep's eps slots
-    bool frag_skip_ = false;     // IPO_HIP_FRAG_SKIP=1: k_update skips 16 x 16 MFMA fragments with only zero products (180 VGPRs, measured slower)
-    int gather_wpe_ = 1;         // IPO_HIP_GATHER_WPE=4: depth-1 k_update built for 4 waves per SIMD (<= 128 VGPRs)
     DevBuf<double> dPartialTile_;
     DevBuf<TaskSrc> dusrc_, dtsrc_;   // per gather task: source panel descriptor
     DevBuf<SlotRec> dslot_rec_, dtail_slot_rec_;   // per gather k-slot record (sparse units, dense tail)

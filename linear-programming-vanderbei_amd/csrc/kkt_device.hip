@@ -158,7 +158,11 @@ __device__ __forceinline__ GatherTile unit_tile(const PlanView& p, const TailVie
 // MFMA accumulation of slots [kb, ke) into this thread's 16 tile entries
 // (acc[a][b][i] = entry (wr + 16a + (lane>>4) + 4i, wc + 16b + (lane&15)))
 // and, for lanes on a diagonal entry, the |terms| of that entry (dabs).
-template <int GD, bool FS>
+// Pipeline: the slot values of slab sb + 1 are issued while slab sb is
+// multiplied, the wave-uniform records of the slab after that one step
+// ahead of its values (scalar loads, no LDS), LDS double-buffered.  (Deeper
+// register rings, fragment skipping and a 4-waves-per-SIMD build were
+// measured slower in round 2 and are gone: DESIGN.md section 6.)
 __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, int kb, int ke, int dcol,
                            bool has_diag, double4_t (&acc)[2][2], double& dabs) {
     __shared__ double As[2][TR][KS + 1];
@@ -173,12 +177,7 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
         for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     dabs = 0.0;
     const int nk = ke - kb, nslab = nk / KS;
-    // pipeline: the slot values of GD slabs in flight in a register ring
-    // (slab sb + GD issued while slab sb is multiplied; ring entry sb % GD),
-    // the wave-uniform records of the next slab to issue one step ahead of
-    // its values (scalar loads, no LDS), LDS double-buffered.  Same
-    // products, same MFMA order for every GD.
-    double ra[GD][KS / 4], rb[GD][KS / 4];
+    double ra[KS / 4], rb[KS / 4];
     const double* __restrict__ Lx = p.Lx;
     const double* __restrict__ dg = p.dg;
     const SlotRec* __restrict__ wrec = recs + kb + wv * (KS / 4);
@@ -187,81 +186,49 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
 #pragma unroll
         for (int j = 0; j < KS / 4; j++) mn[j] = wrec[slab * KS + j];
     };
-    // FS: each wave also publishes which 16-row / 16-column groups of the
-    // tile its k-step (its four slots) touches; a 16 x 16 MFMA fragment
-    // whose row group or column group is untouched by all four slots has
-    // only zero products and is skipped (same sums: acc + 0)
-    __shared__ uint8_t fsum[2][4];
-    uint32_t sm[GD];
-    auto issue = [&](double (&xa)[KS / 4], double (&xb)[KS / 4], uint32_t& smr) {
+    auto issue = [&]() {
 #pragma unroll
-        for (int j = 0; j < KS / 4; j++) slot_vals(mn[j], Lx, dg, lane, xa[j], xb[j]);
-        if constexpr (FS) {
-            uint64_t rm = 0, cm = 0;
-#pragma unroll
-            for (int j = 0; j < KS / 4; j++) { rm |= mn[j].rmask; cm |= mn[j].cmask; }
-            uint32_t f = 0;
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                if ((rm >> (16 * g)) & 0xffffull) f |= 1u << g;
-                if ((cm >> (16 * g)) & 0xffffull) f |= 16u << g;
-            }
-            smr = f;
-        }
+        for (int j = 0; j < KS / 4; j++) slot_vals(mn[j], Lx, dg, lane, ra[j], rb[j]);
     };
+    if (nslab > 0) { fetch(0); issue(); }
+    if (1 < nslab) fetch(1);
 #pragma unroll
-    for (int r = 0; r < GD; r++)
-        if (r < nslab) { fetch(r); issue(ra[r], rb[r], sm[r]); }
-    if (GD < nslab) fetch(GD);
-#pragma unroll
-    for (int j = 0; j < KS / 4; j++) { As[0][lane][wv * (KS / 4) + j] = ra[0][j]; Bs[0][lane][wv * (KS / 4) + j] = rb[0][j]; }
-    if (FS && lane == 0) fsum[0][wv] = static_cast<uint8_t>(sm[0]);
+    for (int j = 0; j < KS / 4; j++) { As[0][lane][wv * (KS / 4) + j] = ra[j]; Bs[0][lane][wv * (KS / 4) + j] = rb[j]; }
     __syncthreads();
-    for (int sb0 = 0; sb0 < nslab; sb0 += GD) {
-#pragma unroll
-        for (int ph = 0; ph < GD; ph++) {
-            const int sb = sb0 + ph;
-            if (sb >= nslab) break;
-            const int cur = sb & 1;
-            if (sb + GD < nslab) {
-                issue(ra[ph], rb[ph], sm[ph]);
-                if (sb + GD + 1 < nslab) fetch(sb + GD + 1);
-            }
-            uint32_t f4 = 0xffffffffu;
-            if constexpr (FS) f4 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(fsum[cur]));
-#pragma unroll
-            for (int kk = 0; kk < KS; kk += 4) {
-                double av[2], bv[2];
-#pragma unroll
-                for (int a = 0; a < 2; a++) av[a] = As[cur][wr + a * 16 + li][kk + lk];
-#pragma unroll
-                for (int b = 0; b < 2; b++) bv[b] = Bs[cur][wc + b * 16 + li][kk + lk];
-                const uint32_t f = f4 >> (2 * kk);      // k-step kk / 4's byte
-#pragma unroll
-                for (int a = 0; a < 2; a++)
-#pragma unroll
-                    for (int b = 0; b < 2; b++)
-                        if (!FS || (((f >> ((wr >> 4) + a)) & 1u) && ((f >> (4 + (wc >> 4) + b)) & 1u)))
-                            acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
-            }
-            if (has_diag) {
-#pragma unroll
-                for (int j = 0; j < KS / 4; j++) {
-                    const int k = wv * (KS / 4) + j;
-                    dabs += fabs(As[cur][lane][k] * Bs[cur][dcol][k]);
-                }
-            }
-            if (sb + 1 < nslab) {
-                const int nx = (ph + 1) % GD;
-#pragma unroll
-                for (int j = 0; j < KS / 4; j++) {
-                    As[cur ^ 1][lane][wv * (KS / 4) + j] = ra[nx][j];
-                    Bs[cur ^ 1][lane][wv * (KS / 4) + j] = rb[nx][j];
-                }
-                if (FS && lane == 0) fsum[cur ^ 1][wv] = static_cast<uint8_t>(sm[nx]);
-            }
-            __syncthreads();
+    for (int sb = 0; sb < nslab; sb++) {
+        const int cur = sb & 1;
+        if (sb + 1 < nslab) {
+            issue();
+            if (sb + 2 < nslab) fetch(sb + 2);
         }
+#pragma unroll
+        for (int kk = 0; kk < KS; kk += 4) {
+            double av[2], bv[2];
+#pragma unroll
+            for (int a = 0; a < 2; a++) av[a] = As[cur][wr + a * 16 + li][kk + lk];
+#pragma unroll
+            for (int b = 0; b < 2; b++) bv[b] = Bs[cur][wc + b * 16 + li][kk + lk];
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+        }
+        if (has_diag) {
+#pragma unroll
+            for (int j = 0; j < KS / 4; j++) {
+                const int k = wv * (KS / 4) + j;
+                dabs += fabs(As[cur][lane][k] * Bs[cur][dcol][k]);
+            }
+        }
+        if (sb + 1 < nslab) {
+#pragma unroll
+            for (int j = 0; j < KS / 4; j++) {
+                As[cur ^ 1][lane][wv * (KS / 4) + j] = ra[j];
+                Bs[cur ^ 1][lane][wv * (KS / 4) + j] = rb[j];
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -304,9 +271,8 @@ __device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], 
 }
 
 // Sum the np partial tiles of a split unit (slots p0.., thread-fragment
-// order) in chunk order: acc = ((0 + P_0) + P_1) + ...  SC: the partials
-// were handed off inside this launch (sc1 loads, bypassing the CU's L1).
-template <bool SC, int NF>
+// order) in chunk order: acc = ((0 + P_0) + P_1) + ...  The partials were
+// handed off inside this launch (sc1 loads, bypassing the CU's L1).
 __device__ __forceinline__ void split_sum(const double* __restrict__ partial, int p0, int np, double4_t (&acc)[2][2],
                                           double& dabs) {
     const int tid = threadIdx.x;
@@ -315,34 +281,12 @@ __device__ __forceinline__ void split_sum(const double* __restrict__ partial, in
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     dabs = 0.0;
-    // loads of NF chunks in flight, sums still in chunk order
-    int j = 0;
-    for (; j + NF <= np; j += NF) {
-        double v[NF][17];
-#pragma unroll
-        for (int u = 0; u < NF; u++) {
-            const double* src = partial + (size_t)(p0 + j + u) * (TR * TR + 4 * TR);
-#pragma unroll
-            for (int e = 0; e < 16; e++) v[u][e] = ld_h<SC>(src + e * NT + tid);
-            v[u][16] = ld_h<SC>(src + TR * TR + tid);
-        }
-#pragma unroll
-        for (int u = 0; u < NF; u++) {
-#pragma unroll
-            for (int a = 0; a < 2; a++)
-#pragma unroll
-                for (int b = 0; b < 2; b++)
-#pragma unroll
-                    for (int i = 0; i < 4; i++) acc[a][b][i] += v[u][(a * 2 + b) * 4 + i];
-            dabs += v[u][16];
-        }
-    }
-    for (; j < np; j++) {
+    for (int j = 0; j < np; j++) {
         const double* src = partial + (size_t)(p0 + j) * (TR * TR + 4 * TR);
         double v[17];
 #pragma unroll
-        for (int e = 0; e < 16; e++) v[e] = ld_h<SC>(src + e * NT + tid);
-        v[16] = ld_h<SC>(src + TR * TR + tid);
+        for (int e = 0; e < 16; e++) v[e] = sc1_load(src + e * NT + tid);
+        v[16] = sc1_load(src + TR * TR + tid);
 #pragma unroll
         for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -354,18 +298,15 @@ __device__ __forceinline__ void split_sum(const double* __restrict__ partial, in
 }
 
 // Gather chunks: chunk c covers slots [ck_b[c], ck_e[c]) of unit ck_u[c].
-// ck_part[c] < 0: the unit's only chunk, subtract directly; else store the
-// partial tile (thread-fragment order) and dabs at partial slot ck_part[c].
+// ck_part[c] < 0: the unit's only chunk, subtract directly.  Else the chunks
+// of split unit q = ck_q[c] store their partial tiles (thread-fragment
+// order) and dabs write-through (sc1) at partial slot ck_part[c], drain them,
+// and one lane adds to the unit's arrival counter; the chunk whose add comes
+// last sums all partials in chunk order (sc1 loads) and stores the tile
+// (MI355X_MICROARCH.md hand-off table row 1: last arriver told by its own
+// add's return value).  It resets the counter for the next factorisation.
 // tail >= 0: units are dense-tail tiles.
-// split_cnt != null (fused split-K): the chunks of split unit q = ck_q[c]
-// store their partials write-through (sc1), drain them, and one lane adds
-// to the unit's arrival counter; the chunk whose add comes last sums all
-// partials in chunk order (sc1 loads) and stores the tile, exactly as
-// k_update_reduce would (MI355X_MICROARCH.md hand-off table row 1:
-// last arriver told by its own add's return value).  It resets the counter
-// for the next factorisation.
-template <int GD, int NF, int WPE, bool FS>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE)))
+__global__ void __launch_bounds__(NT)
 k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
          const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
          const int* __restrict__ ck_part, int c0, double* __restrict__ partial,
@@ -379,23 +320,13 @@ k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
     const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
     double4_t acc[2][2];
     double dabs;
-    gather_acc<GD, FS>(p, recs, kb, ke, dcol, has_diag, acc, dabs);
+    gather_acc(p, recs, kb, ke, dcol, has_diag, acc, dabs);
     if (pi < 0) {
         gather_store(g, acc, dabs, has_diag, dcol);
         return;
     }
     double* dst = partial + (size_t)pi * (TR * TR + 4 * TR);
     const int tid = threadIdx.x;
-    if (!split_cnt) {
-#pragma unroll
-        for (int a = 0; a < 2; a++)
-#pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) dst[((a * 2 + b) * 4 + i) * NT + tid] = acc[a][b][i];
-        dst[TR * TR + tid] = dabs;
-        return;
-    }
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -415,23 +346,7 @@ k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
     }
     __syncthreads();
     if (!last) return;
-    split_sum<true, NF>(partial, sp_p0[q], np, acc, dabs);
-    gather_store(g, acc, dabs, has_diag, dcol);
-}
-
-// Split units: sum their chunks' partial tiles in chunk order, then store.
-__global__ void __launch_bounds__(NT)
-k_update_reduce(PlanView p, TailView tv, int tail, const int* __restrict__ sp_u, const int* __restrict__ sp_p0,
-                const int* __restrict__ sp_n, int s0, const double* __restrict__ partial) {
-    const int q = s0 + blockIdx.x;
-    const int u = sp_u[q], p0 = sp_p0[q], np = sp_n[q];
-    const GatherTile g = unit_tile(p, tv, u, tail);
-    const int lane = threadIdx.x & 63;
-    const int dcol = g.row0 + lane - g.col0;
-    const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
-    double4_t acc[2][2];
-    double dabs;
-    split_sum<false, 4>(partial, p0, np, acc, dabs);
+    split_sum(partial, sp_p0[q], np, acc, dabs);
     gather_store(g, acc, dabs, has_diag, dcol);
 }
 
@@ -1906,7 +1821,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dupd_r1_.upload(plan_.upd_r1, s);
     drel_.upload(plan_.rel, s);
     dlevel_sups_.upload(plan_.level_sups, s);
-    {   // fused panel units (k_panel): per supernode max(1, tiles - 1) workgroups,
+    {   // fused panel units (k_panel_w): per supernode max(1, tiles - 1) workgroups,
         // workgroup j holding the diagonal block and 64-row tile j + 1
         // (supernodes of at most 16 columns and 64 rows go to the one-wave
         // small-panel kernel instead: list small_sups_, per level small_ptr_)
@@ -1929,10 +1844,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dfu_j_.upload(fj, s);
         dsmall_sups_.upload(ss, s);
         IPO_HIP_CHECK(hipStreamSynchronize(s));
-        if (const char* e = std::getenv("IPO_HIP_PANEL")) {
-            use_panel_ = std::atoi(e) != 0;
-            if (use_panel_) g_panel_kind = std::atoi(e) == 1 ? 1 : 2;
-        }
+        // IPO_HIP_PANEL=0: per-phase kernels only (k_diag + k_trsm + k_tail_syrk,
+        // the dependent-pivot path), the bitwise reference of the fused ones
+        if (const char* e = std::getenv("IPO_HIP_PANEL")) use_panel_ = std::atoi(e) != 0;
     }
     {   // solve chunks: levels holding a panel with more than kChunkRows rows below
         // its diagonal block are solved in 64-row chunks (two launches each way)
@@ -1970,9 +1884,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         ck_ptr_.assign(plan_.nlevels + 2, 0);
         sp_ptr_.assign(plan_.nlevels + 2, 0);
         size_t max_part = 0;
-        int wg_target = 512, min_chunk = 64;
-        if (const char* e = std::getenv("IPO_HIP_GATHER_WGS")) wg_target = std::max(1, std::atoi(e));
-        if (const char* e = std::getenv("IPO_HIP_GATHER_MINCHUNK")) min_chunk = std::max(kSlab, std::atoi(e) / kSlab * kSlab);
+        const int wg_target = 512, min_chunk = 64;
         auto group = [&](int u0, int u1, const std::vector<int>& kptr) {
             long sumk = 0;
             for (int u = u0; u < u1; u++) sumk += kptr[u + 1] - kptr[u];
@@ -2013,11 +1925,6 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dck_q_.upload(cq, s);
         dSplitCnt_.alloc(std::max<size_t>(1, su.size()));
         IPO_HIP_CHECK(hipMemsetAsync(dSplitCnt_.get(), 0, std::max<size_t>(1, su.size()) * sizeof(int), s));
-        if (const char* e = std::getenv("IPO_HIP_SPLITK_FUSED")) fused_splitk_ = std::atoi(e) != 0;
-        if (const char* e = std::getenv("IPO_HIP_GATHER_DEPTH")) gather_depth_ = std::atoi(e);
-        if (const char* e = std::getenv("IPO_HIP_TAIL_GATHER_DEPTH")) tail_gather_depth_ = std::atoi(e);
-        if (const char* e = std::getenv("IPO_HIP_GATHER_WPE")) gather_wpe_ = std::atoi(e);
-        if (const char* e = std::getenv("IPO_HIP_FRAG_SKIP")) frag_skip_ = std::atoi(e) != 0;
         dPartialTile_.alloc(std::max<size_t>(1, max_part) * (kTileRows * kTileRows + 4 * kTileRows));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
     }
@@ -2069,7 +1976,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         work_flops[kPhGather] = gf; work_bytes[kPhGather] = gb;
         work_flops[kPhDiag] = df; work_bytes[kPhDiag] = db;
         work_flops[kPhTrsm] = tf; work_bytes[kPhTrsm] = tb;
-        if (use_panel_) {   // k_panel does both: the diag phase carries the trsm work
+        if (use_panel_) {   // k_panel_w does both: the diag phase carries the trsm work
             work_flops[kPhDiag] += tf; work_bytes[kPhDiag] += tb;
             work_flops[kPhTrsm] = work_bytes[kPhTrsm] = 0;
         }
@@ -2185,8 +2092,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
 // work items, per-supernode arrival counts and parents.  Called from the
 // constructor after the solve chunks are built.
 void KktDevice::build_sync_free_plan() {
-    int kSfWidth = 64;
-    if (const char* e = std::getenv("IPO_HIP_SF_WIDTH")) kSfWidth = std::max(1, std::atoi(e));
+    const int kSfWidth = 64;
     hipStream_t s = stream_;
     const KktPlan& P = plan_;
     const int ns = P.nsup;
@@ -2307,7 +2213,7 @@ KktDevice::~KktDevice() {
     if (!h_sf_items_f_.empty()) dump_sf_stamps(h_sf_items_f_, plan_);
 #endif
     if (std::getenv("IPO_HIP_DEBUG_REDO"))
-        std::fprintf(stderr, "kkt: %ld factorisations, %ld redone; bails k_panel %ld, k_panel_w sparse %ld, tail %ld, "
+        std::fprintf(stderr, "kkt: %ld factorisations, %ld redone; bails (unused) %ld, k_panel_w sparse %ld, tail %ld, "
                              "k_panel_s %ld; tail block columns repaired %ld\n", tm_.factors, tm_.panel_redos,
                      tm_.redo_where[0], tm_.redo_where[1], tm_.redo_where[2], tm_.redo_where[3], tm_.tail_repairs);
     if (hScal_) (void)hipHostFree(hScal_);
@@ -2360,7 +2266,48 @@ TailView KktDevice::tail_view() const {
     return t;
 }
 
+// Developer diagnostics (IPO_HIP_DUMP_DIR=dir): every factorisation's input
+// (E, D, eps_diag) and outcome (live marks, D, |terms| sums, ndep) to
+// dir/fNNNN.bin, for tools/dep_compare.py, which refactors the same input
+// with the oracle and compares the dependent-pivot classification.
+// Layout: int32 m, n, T, ndep; f64 eps_in, eps_out; f64 E[m], D[n];
+// int32 perm[T]; int32 live[T]; f64 dg[T]; f64 dscale[T] (new order).
+void KktDevice::dump_factor(const double* dE, const double* dD, double eps_in) {
+    const char* dir = std::getenv("IPO_HIP_DUMP_DIR");
+    if (!dir) return;
+    std::vector<double> E(m_), D(n_), dg(T_), dsc(T_);
+    std::vector<int> live(T_);
+    IPO_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (m_) IPO_HIP_CHECK(hipMemcpy(E.data(), dE, m_ * sizeof(double), hipMemcpyDeviceToHost));
+    if (n_) IPO_HIP_CHECK(hipMemcpy(D.data(), dD, n_ * sizeof(double), hipMemcpyDeviceToHost));
+    dLive_.download(live.data(), T_, stream_);
+    dDg_.download(dg.data(), T_, stream_);
+    dDscale_.download(dsc.data(), T_, stream_);
+    IPO_HIP_CHECK(hipStreamSynchronize(stream_));
+    char path[4096];
+    std::snprintf(path, sizeof path, "%s/f%04d.bin", dir, dump_count_++);
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return;
+    const int hdr[4] = {m_, n_, T_, ndep_};
+    const double eps[2] = {eps_in, epsdiag_};
+    std::fwrite(hdr, sizeof(int), 4, f);
+    std::fwrite(eps, sizeof(double), 2, f);
+    std::fwrite(E.data(), sizeof(double), m_, f);
+    std::fwrite(D.data(), sizeof(double), n_, f);
+    std::fwrite(plan_.perm.data(), sizeof(int), T_, f);
+    std::fwrite(live.data(), sizeof(int), T_, f);
+    std::fwrite(dg.data(), sizeof(double), T_, f);
+    std::fwrite(dsc.data(), sizeof(double), T_, f);
+    std::fclose(f);
+}
+
 void KktDevice::factor(const double* dE, const double* dD) {
+    const double eps_in = epsdiag_;
+    factor_core(dE, dD);
+    dump_factor(dE, dD, eps_in);
+}
+
+void KktDevice::factor_core(const double* dE, const double* dD) {
     // fast path: fused diagonal-block + panel kernels; a pivot that fails
     // the zero test makes them stop unwritten, and the factorisation is
     // redone with the per-phase kernels, which own the dependent-pivot rule
@@ -2371,7 +2318,7 @@ void KktDevice::factor(const double* dE, const double* dD) {
         // block column stands, resume from there; else redo it all
         const char* rp = std::getenv("IPO_HIP_TAIL_REPAIR");
         const bool repair = !rp || std::atoi(rp) != 0;
-        if (repair && !xch_ && g_panel_kind == 2 && hFlags_[1] == 4 && hFlags_[4] > 0) repair_tail();
+        if (repair && !xch_ && hFlags_[1] == 4 && hFlags_[4] > 0) repair_tail();
         else factor_pass(dE, dD, false);
     }
     tm_.factors++;
@@ -2422,7 +2369,7 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
         // shards: S = sum of every shard's assembled + gathered tail (exchange.h)
         xsum(tv.S, static_cast<size_t>(plan_.nt) * plan_.nt, RedOp::Sum);
         xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
-        if (fused && g_panel_kind == 2) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
+        if (fused) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
             const size_t wst = static_cast<size_t>(plan_.nt) * kPanelCols;
             for (int t = 0; t < plan_.ntb; t++) {
                 double* wc = dW_.get() + (t & 1) * wst;
@@ -2538,31 +2485,16 @@ void KktDevice::repair_tail() {
     }
 }
 
-// Gather launches of one level (tail < 0) or of the dense tail (group =
-// nlevels): the chunks, then the in-order reduction of the split units.
+// Gather launch of one level (tail < 0) or of the dense tail (group =
+// nlevels): every chunk; split units combined by their last-arriving chunk.
 int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, int group, hipStream_t s) {
     const int c0 = ck_ptr_[group], c1 = ck_ptr_[group + 1];
     if (c1 <= c0) return 0;
     const SlotRec* recs = tail < 0 ? dslot_rec_.get() : dtail_slot_rec_.get();
-    const int s0 = sp_ptr_[group], s1 = sp_ptr_[group + 1];
-    // fused: split units combined by their last-arriving chunk (one launch)
-    const bool fused = fused_splitk_ && s1 > s0;
-    // slabs in flight / partials in flight of the combine: deep for the
-    // sparse levels (<= ~2 workgroups per CU), shallow for the many
-    // workgroups of the dense-tail gather (occupancy)
-    const int gd = tail < 0 ? gather_depth_ : tail_gather_depth_;
-    auto kern = gd <= 1 ? (gather_wpe_ >= 4 ? k_update<1, 1, 4, false>
-                                            : frag_skip_ ? k_update<1, 1, 1, true> : k_update<1, 1, 1, false>)
-                        : gd == 2 ? k_update<2, 4, 1, false> : k_update<4, 4, 1, false>;
-    hipLaunchKernelGGL(kern, dim3(c1 - c0),
-                       dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
+    hipLaunchKernelGGL(k_update, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
                        dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(), dsp_n_.get(),
-                       fused ? dSplitCnt_.get() : static_cast<int*>(nullptr));
-    if (fused) return 1;
-    if (s1 > s0)
-        hipLaunchKernelGGL(k_update_reduce, dim3(s1 - s0), dim3(NT), 0, s, pv, tv, tail, dsp_u_.get(), dsp_p0_.get(),
-                           dsp_n_.get(), s0, dPartialTile_.get());
-    return s1 > s0 ? 2 : 1;
+                       dSplitCnt_.get());
+    return 1;
 }
 
 hipEvent_t KktDevice::next_event() {

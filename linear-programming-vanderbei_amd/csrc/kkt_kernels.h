@@ -76,9 +76,5 @@ bool launch_tail_diag_coop(const PlanView& pv, const TailView& tv, int kb, doubl
 // Fused panel of supernodes sups[q0 .. q0+count) that have at most 16
 // columns and 64 rows (one wave each, k_panel_s); same bail-out contract.
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s);
-// which fused panel kernel launch_panel runs: 1 = k_panel (8 waves, one
-// barrier per column), 2 = k_panel_w (one wave, no barrier; default);
-// IPO_HIP_PANEL=0 turns the fused path off, =1 / =2 choose the kernel
-extern int g_panel_kind;
 
 }  // namespace ipo

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <iterator>
 #include <cmath>
+#include <cstdint>
 #include <stdexcept>
 
 namespace ipo {
@@ -147,9 +148,24 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
     const int dense_deg = 3;
     const int penalty = T;
 
+    // deg[v]: live neighbours of v.  Eliminated nodes are not erased from
+    // the survivors' lists as they leave (an O(degree) find + shift per
+    // survivor and pivot); they stay as dead entries, skipped where a list
+    // is read, and a list is compacted (order kept) once it is mostly dead.
+    // Every decision reads the same live neighbours in the same order as the
+    // eager form, so the ordering is unchanged.
+    std::vector<int> deg(T), ndead(T, 0);
+    std::vector<char> dead(T, 0);
+    for (int v = 0; v < T; v++) deg[v] = static_cast<int>(nb[v].size());
+    auto compact = [&](int w) {
+        auto& lst = nb[w];
+        lst.erase(std::remove_if(lst.begin(), lst.end(), [&](int q) { return dead[q] != 0; }), lst.end());
+        ndead[w] = 0;
+    };
+
     std::vector<int> key(T);
     for (int v = 0; v < T; v++) {
-        int d = static_cast<int>(nb[v].size());
+        int d = deg[v];
         if (d > dense_deg && tier[v] == 0) tier[v] = 1;
         key[v] = d + tier[v] * penalty;
     }
@@ -173,12 +189,17 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
 
     int stamp = 0, step = 0, denwin = T;
     const int Tfree = T - nforced;
+    constexpr int kBitsNodes = 8192;
+    int bw = 0;                                  // words per bit-matrix row (0: lists only)
+    std::vector<uint64_t> bits;
+    std::vector<int> cidx(T, -1), cg;
     while (step < Tfree) {
         const int piv = hp.slot[1];
-        const int dg = static_cast<int>(nb[piv].size());
+        const int dg = deg[piv];
         if (dg >= T - 1 - step) denwin = step;
         perm[step] = piv;
         iperm[piv] = step;
+        if (ndead[piv]) compact(piv);
 
         // neighbours are tagged with the current step; twins (same degree,
         // same tier, neighbourhood inside piv's closed neighbourhood) are
@@ -188,9 +209,10 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
         for (int w : nb[piv]) iperm[w] = step;
         for (int w : nb[piv]) {
             bool twin = false;
-            if (static_cast<int>(nb[w].size()) == dg && tier[w] == tier[piv]) {
+            if (deg[w] == dg && tier[w] == tier[piv]) {
                 twin = true;
-                for (int q : nb[w]) if (iperm[q] < step) { twin = false; break; }
+                for (int q : nb[w])
+                    if (!dead[q] && iperm[q] < step) { twin = false; break; }
             }
             if (twin) { perm[next] = w; iperm[w] = next; next++; }
             else group.push_back(w);
@@ -201,24 +223,17 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
             const int v = perm[s];
             o.Lp[s + 1] = o.Lp[s] + width;
             for (int w : nb[v]) {
+                if (dead[w]) continue;
                 int r = iperm[w];
                 if (r > s || (r == step && w != piv)) lrows.push_back(w);
             }
             width--;
         }
 
-        for (int w : group) {                    // drop piv from the survivors
-            auto& lst = nb[w];
-            lst.erase(std::find(lst.begin(), lst.end(), piv));
-        }
-        if (next > step + 1) {                   // ... and the twins
-            for (int w : group) {
-                auto& lst = nb[w];
-                lst.erase(std::remove_if(lst.begin(), lst.end(),
-                                         [&](int q) { return iperm[q] > step; }),
-                          lst.end());
-            }
-        }
+        // piv and its twins leave the survivors' lists (as dead entries)
+        const int nel = next - step;
+        for (int s = step; s < next; s++) dead[perm[s]] = 1;
+        for (int w : group) { deg[w] -= nel; ndead[w] += nel; }
         for (int s = step; s < next; s++) {      // leave the heap
             const int v = perm[s];
             const int pos = hp.at[v];
@@ -229,22 +244,66 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
             if (old_key < key[hp.slot[pos]]) hp.sink(pos);
             else hp.swim(pos);
         }
-        for (size_t a = 0; a < group.size(); a++) {   // clique on the survivors
-            const int w = group[a];
-            ++stamp;
-            for (int q : nb[w]) seen[q] = stamp;
-            for (size_t b = a + 1; b < group.size(); b++) {
-                const int w2 = group[b];
-                if (seen[w2] != stamp) { nb[w].push_back(w2); nb[w2].push_back(w); }
+        // clique on the survivors: w gains, in group order, every member of
+        // the group it is not adjacent to yet (the pairwise loop below appends
+        // exactly that sequence to every list)
+        if (bw > 0) {
+            cg.resize(group.size());
+            for (size_t a = 0; a < group.size(); a++) cg[a] = cidx[group[a]];
+            for (size_t a = 0; a < group.size(); a++) {
+                const int w = group[a], cw = cg[a];
+                uint64_t* row = bits.data() + static_cast<size_t>(cw) * bw;
+                for (size_t b = a + 1; b < group.size(); b++) {
+                    const int c2 = cg[b];
+                    if (!((row[c2 >> 6] >> (c2 & 63)) & 1ull)) {
+                        const int w2 = group[b];
+                        nb[w].push_back(w2); nb[w2].push_back(w); deg[w]++; deg[w2]++;
+                        row[c2 >> 6] |= 1ull << (c2 & 63);
+                        bits[static_cast<size_t>(c2) * bw + (cw >> 6)] |= 1ull << (cw & 63);
+                    }
+                }
+            }
+        } else {
+            for (size_t a = 0; a < group.size(); a++) {
+                const int w = group[a];
+                if (ndead[w] > deg[w]) compact(w);
+                ++stamp;
+                for (int q : nb[w]) seen[q] = stamp;
+                for (size_t b = a + 1; b < group.size(); b++) {
+                    const int w2 = group[b];
+                    if (seen[w2] != stamp) { nb[w].push_back(w2); nb[w2].push_back(w); deg[w]++; deg[w2]++; }
+                }
             }
         }
         for (int w : group) {
-            key[w] = static_cast<int>(nb[w].size()) + (tier[w] != 0 ? tier[w] * penalty : 0);
+            key[w] = deg[w] + (tier[w] != 0 ? tier[w] * penalty : 0);
             hp.swim(hp.at[w]);
             hp.sink(hp.at[w]);
         }
         for (int s = step; s < next; s++) { std::vector<int>().swap(nb[perm[s]]); }
         step = next;
+        // once few nodes remain (the graph turns dense towards the reference's
+        // dense window), adjacency tests go to a bit matrix over the
+        // survivors: the clique step then costs |group|^2 bit tests instead of
+        // a scan of every survivor's list
+        if (bw == 0 && Tfree - step <= kBitsNodes && Tfree - step > 0) {
+            const int R = Tfree - step;
+            bw = (R + 63) / 64;
+            bits.assign(static_cast<size_t>(R) * bw, 0ull);
+            int c = 0;
+            for (int k = 1; k <= hp.count; k++) {
+                const int v = hp.slot[k];
+                if (v >= mf && v < m) continue;          // forced rows: outside the graph
+                cidx[v] = c++;
+            }
+            for (int k = 1; k <= hp.count; k++) {
+                const int v = hp.slot[k];
+                if (cidx[v] < 0) continue;
+                uint64_t* row = bits.data() + static_cast<size_t>(cidx[v]) * bw;
+                for (int q : nb[v])
+                    if (!dead[q] && cidx[q] >= 0) row[cidx[q] >> 6] |= 1ull << (cidx[q] & 63);
+            }
+        }
     }
     o.denwin = denwin;
     o.Li.resize(lrows.size());
@@ -360,10 +419,17 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
         }
         P.tail_r0[d] = i - b;       // R_d[tail_r0 ..] are tail rows
     }
-    std::stable_sort(pairs.begin(), pairs.end(), [](const Pair& a, const Pair& b) { return a.tgt < b.tgt; });
+    // grouped by target, sources in ascending order inside a group (a
+    // stable counting sort of the source-ordered list)
     P.upd_ptr.assign(ns + 1, 0);
     for (const Pair& q : pairs) P.upd_ptr[q.tgt + 1]++;
     for (int s = 0; s < ns; s++) P.upd_ptr[s + 1] += P.upd_ptr[s];
+    {
+        std::vector<Pair> sorted(pairs.size());
+        std::vector<int> fill(P.upd_ptr.begin(), P.upd_ptr.end() - 1);
+        for (const Pair& q : pairs) sorted[fill[q.tgt]++] = q;
+        pairs.swap(sorted);
+    }
     const size_t np = pairs.size();
     P.upd_src.resize(np); P.upd_r0.resize(np); P.upd_r1.resize(np); P.relptr.assign(np + 1, 0);
     for (size_t q = 0; q < np; q++) {

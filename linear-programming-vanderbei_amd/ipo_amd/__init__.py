@@ -71,7 +71,7 @@ EXPORTED = [
     "ipo_hip_solve", "ipo_hip_run_mps", "ipo_hip_mps_dims", "ipo_hip_mps_load",
     "ipo_hip_kkt_create", "ipo_hip_kkt_destroy", "ipo_hip_kkt_factor", "ipo_hip_kkt_solve",
     "ipo_hip_kkt_info", "ipo_hip_kkt_perm", "ipo_hip_symbolic",
-    "ipo_hip_device_count", "ipo_hip_last_error", "ipo_hip_version",
+    "ipo_hip_device_count", "ipo_hip_device_synchronize", "ipo_hip_last_error", "ipo_hip_version",
     "ipo_hip_ctx_create", "ipo_hip_ctx_run", "ipo_hip_ctx_download", "ipo_hip_ctx_destroy",
     "ipo_hip_ctx_setup_seconds", "ipo_hip_kkt_set_epsdiag",
     "ipo_hip_synth_random", "ipo_hip_synth_block_angular", "ipo_hip_symbolic_forced",
@@ -156,6 +156,7 @@ def lib() -> C.CDLL:
     L.ipo_hip_ctx_create_shard.argtypes = [_I, _I, _P, _P, _P, _P, _P, _D, _I, _I, _I, C.c_long, _I, _I, _P, _P, _P]
     L.ipo_hip_ctx_create_shard.restype = _P
     L.ipo_hip_device_count.restype = _I
+    L.ipo_hip_device_synchronize.restype = _I
     L.ipo_hip_last_error.restype = C.c_char_p
     L.ipo_hip_version.restype = C.c_char_p
     _lib = L
@@ -177,6 +178,12 @@ def last_error() -> str:
 
 def device_count() -> int:
     return lib().ipo_hip_device_count()
+
+
+def device_synchronize() -> None:
+    """Wait for every stream of this process's device (hipDeviceSynchronize)."""
+    if lib().ipo_hip_device_synchronize():
+        raise IpoHipError("device_synchronize: " + last_error())
 
 
 def require_gpu() -> None:

@@ -103,6 +103,7 @@ void orc_kkt_diag(const orc_kkt *k, double *d);     /* [N]   numeric D after fac
 double orc_kkt_epsdiag(const orc_kkt *k);
 void   orc_kkt_set_epsdiag(orc_kkt *k, double e);   /* tests: start from a captured state */
 int  orc_kkt_ndep(const orc_kkt *k);
+void orc_kkt_live(const orc_kkt *k, int *live);      /* [N] "mark" (new order) after factor */
 int  orc_kkt_last_passes(const orc_kkt *k);
 
 /* ---------- solver() restatements (identical ABI to solve.c:24-26) ---------- */

@@ -486,4 +486,5 @@ void orc_kkt_diag(const orc_kkt *K, double *p) { memcpy(p, K->d, sizeof(double) 
 double orc_kkt_epsdiag(const orc_kkt *K) { return K->epsdiag; }
 void orc_kkt_set_epsdiag(orc_kkt *K, double e) { K->epsdiag = e; }
 int  orc_kkt_ndep(const orc_kkt *K) { return K->ndep; }
+void orc_kkt_live(const orc_kkt *K, int *p) { memcpy(p, K->live, sizeof(int) * (size_t)K->T); }
 int  orc_kkt_last_passes(const orc_kkt *K) { return K->passes; }

@@ -60,6 +60,7 @@ def lib():
         L.orc_kkt_epsdiag.argtypes = [P]
         L.orc_kkt_perm.argtypes = [P, P]
         L.orc_kkt_diag.argtypes = [P, P]
+        L.orc_kkt_live.argtypes = [P, P]
         L.orc_kkt_set_epsdiag.argtypes = [P, D]
         _lib = L
     return _lib
@@ -102,6 +103,11 @@ class OracleKkt:
         p = np.zeros(self.m + self.n, np.int32)
         lib().orc_kkt_perm(self.h, p.ctypes.data)
         return p
+
+    def live(self):
+        v = np.zeros(self.m + self.n, np.int32)
+        lib().orc_kkt_live(self.h, v.ctypes.data)
+        return v
 
     def diag(self):
         d = np.zeros(self.m + self.n, np.float64)

@@ -207,3 +207,71 @@ def test_dfl001_hsd_headline():
     assert rows[-1][5] < 1e-11
     assert rel(rows[-1][1], grows[-1][1]) <= 1e-4
     assert rel(rows[-1][3], grows[-1][3]) <= 1e-4
+
+
+def test_solver_symbol_abi_trace_and_buffers():
+    """The literal drop-in symbol: `solver(m, n, nz, iA, kA, A, b, c, f, x, y,
+    w, z)` (solve.c:24-26) called through ctypes with the caller-allocated,
+    zeroed buffers of solve.c:194-197 (x, y: n + m; w: m; z: n).  Its stdout
+    from the hsd.c:117 dimension line to the last iteration line must be the
+    golden trace's (afiro is rounding-stable and matches line for line on the
+    GPU); w and z stay the caller's (the reference frees them, hsd.c:290-291,
+    a use-after-free for writesol) and hold the complementary slacks."""
+    import ctypes as C
+    import tempfile
+
+    import numpy as np
+    p = ipo_amd.load_mps(mps_path("afiro"))
+    m, n = p.m, p.n
+    x, y = np.zeros(n + m), np.zeros(n + m)
+    w, z = np.zeros(m), np.zeros(n)
+    kA, iA = np.ascontiguousarray(p.kA, np.int32), np.ascontiguousarray(p.iA, np.int32)
+    A, b, c = p.A.copy(), p.b.copy(), p.c.copy()
+    L = ipo_amd.lib()
+    libc = C.CDLL(None)
+    libc.fflush.argtypes = [C.c_void_p]
+    with tempfile.TemporaryFile(mode="w+") as tmp:
+        libc.fflush(None)
+        saved = os.dup(1)
+        os.dup2(tmp.fileno(), 1)
+        try:
+            st = L.solver(m, n, p.nz, iA.ctypes.data, kA.ctypes.data, A.ctypes.data, b.ctypes.data, c.ctypes.data,
+                          float(p.f), x.ctypes.data, y.ctypes.data, w.ctypes.data, z.ctypes.data)
+            libc.fflush(None)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+        tmp.seek(0)
+        out = tmp.read()
+    assert st == 0
+    gold = golden_trace("afiro").splitlines()
+    start = next(i for i, ln in enumerate(gold) if ln.startswith(f"m = {m},n = {n}"))
+    want = gold[start:-1]                     # dimension line .. last iteration (main.c prints the status)
+    got = out.splitlines()
+    got = got[next(i for i, ln in enumerate(got) if ln.startswith(f"m = {m},n = {n}")):]
+    assert got == want
+    assert (w >= 0).all() and (z >= 0).all() and w.max() > 0 and z.max() > 0
+    assert abs(float(np.dot(x[:n], z)) + float(np.dot(y[:m], w))) < 1e-6 * (1 + abs(float(np.dot(c, x[:n]))))
+    # the inputs are read-only (solve.c:225-235)
+    assert np.array_equal(A, p.A) and np.array_equal(b, p.b) and np.array_equal(c, p.c)
+
+
+def test_back_to_back_solves_on_one_context_identical():
+    """bench.py times consecutive solves on one Context: every solve starts
+    from the reference's eps_diag (ldlt.c:31) and the all-ones point, so two
+    back-to-back HSD solves print identical traces and end bitwise equal."""
+    import numpy as np
+    p = ipo_amd.load_mps(mps_path("25fv47"))
+    ctx = ipo_amd.Context(p)
+    try:
+        s1, st1, t1 = ctx.run("hsd", trace=True)
+        sol1 = ctx.solution()
+        s2, st2, t2 = ctx.run("hsd", trace=True)
+        sol2 = ctx.solution()
+    finally:
+        ctx.close()
+    assert s1 == s2 == 0 and t1 == t2
+    for k in ("iters", "final_mu", "final_pobj", "final_dobj", "refine_passes", "factors"):
+        assert st1[k] == st2[k], k
+    for a, b in zip(sol1, sol2):
+        assert np.array_equal(a, b)

@@ -1,8 +1,9 @@
-"""The fused panel kernels against each other: k_diag + k_trsm (IPO_HIP_PANEL=0),
-k_panel (8 waves, =1) and k_panel_w (one wave, =2, the default) apply the
-same operations in the same order to every entry of the factor (the
-reference's l = a / d, a -= l (l_j d) form, kkt_dense.hip), so the refined
-solves and whole IPM traces they produce must be bitwise identical."""
+"""The fused panel kernels against the per-phase ones: k_diag + k_trsm +
+k_tail_syrk (IPO_HIP_PANEL=0, the dependent-pivot path) and the fused
+k_panel_s / k_panel_w / look-ahead tail (default) apply the same operations
+in the same order to every entry of the factor (the reference's l = a / d,
+a -= l (l_j d) form, kkt_dense.hip), so the refined solves and whole IPM
+traces they produce must be bitwise identical."""
 import os
 
 import numpy as np
@@ -13,7 +14,7 @@ from conftest import mps_path
 
 pytestmark = pytest.mark.gpu
 
-KINDS = ("0", "1", "2")
+KINDS = ("0", "1")
 
 
 def _with_panel(kind, fn):
@@ -54,7 +55,7 @@ def test_panel_kinds_solve_bitwise(name):
 def test_panel_kinds_hsd_trace_bitwise(name):
     """Whole HSD solves (dfl001: 117 iterations, dense tail of 44 block
     columns, dependent-pivot redos): identical printed traces."""
-    texts = [_with_panel(kind, lambda: ipo_amd.run_mps(mps_path(name), "hsd"))[1] for kind in ("1", "2")]
+    texts = [_with_panel(kind, lambda: ipo_amd.run_mps(mps_path(name), "hsd"))[1] for kind in KINDS]
     assert texts[0] == texts[1]
 
 
@@ -102,24 +103,9 @@ def _solve_env(var, val):
     return status, text, {k: st[k] for k in sorted(st) if k.startswith("final") or k == "iters"}
 
 
-def test_fused_split_k_bitwise():
-    """Split-K gather units combined by their last-arriving chunk inside
-    k_update (default) against the separate k_update_reduce launch
-    (IPO_HIP_SPLITK_FUSED=0): the same partial sums in chunk order, so the
-    dfl001 HSD solves agree to the last bit of the final iterate's values."""
-    assert _solve_env("IPO_HIP_SPLITK_FUSED", "0") == _solve_env("IPO_HIP_SPLITK_FUSED", "1")
-
-
 def test_hsd_overlap_bitwise():
     """mu, residuals and right-hand sides on a side stream beside the
     factorisation (default) against the sequential iteration
     (IPO_HIP_OVERLAP=0): the device mu / phi / psi / theta are the host's
     operations in the host's order, so the solves are identical."""
     assert _solve_env("IPO_HIP_OVERLAP", "0") == _solve_env("IPO_HIP_OVERLAP", "1")
-
-
-def test_frag_skip_bitwise():
-    """The gather's optional MFMA fragment skip (IPO_HIP_FRAG_SKIP=1: 16 x 16
-    fragments whose row or column group no slot of the k-step touches are not
-    issued) adds only exact zeros when on: identical dfl001 HSD solves."""
-    assert _solve_env("IPO_HIP_FRAG_SKIP", "0") == _solve_env("IPO_HIP_FRAG_SKIP", "1")

@@ -2,7 +2,9 @@
 
 The GPU box has one device and RCCL refuses two ranks on one GPU, so the
 two ranks here share it and exchange through the host-callback transport
-(exchange.h make_host_exchange) over gloo; RCCL is the same Exchange
+(exchange.h make_host_exchange) over host sockets (ipo_amd.hostcomm; no
+torch in a GPU process, whose bundled HIP runtime would sit beside the
+library's); RCCL is the same Exchange
 interface and carries bench.py's multi-GPU runs.  Checked, for hsd and
 intpt:
   * both ranks report the same status and iteration count;
@@ -44,15 +46,13 @@ def _free_port():
 def _rank_main(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path[:0] = [os.path.join(REPO, "linear-programming-vanderbei_amd"), os.path.join(REPO, "tests")]
-    import torch
-    import torch.distributed as dist
-
     import ipo_amd
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    ops = {0: dist.ReduceOp.SUM, 1: dist.ReduceOp.MAX, 2: dist.ReduceOp.MIN}
+    from ipo_amd.hostcomm import HostComm
+    comm = HostComm(rank, world)
+    ops = {0: "sum", 1: "max", 2: "min"}
 
     def allreduce(buf, op):
-        dist.all_reduce(torch.from_numpy(buf), op=ops[op])
+        comm.allreduce(buf, ops[op])
     try:
         p = ipo_amd.synth_block_angular(*DIMS)
         loc = ipo_amd.shard_block_angular(p, world, rank)
@@ -67,7 +67,7 @@ def _rank_main(rank, world, port, q):
         import traceback
         q.put((rank, None, None, traceback.format_exc()))
     finally:
-        dist.destroy_process_group()
+        comm.close()
 
 
 def _check(st, iters, pobj, dobj, ref):
@@ -88,7 +88,7 @@ def _references(p, method):
 @pytest.mark.gpu
 @pytest.mark.timeout(300)
 def test_two_shards_on_one_gpu_match_unsharded_and_oracle():
-    import torch.multiprocessing as mp
+    import multiprocessing as mp
     ipo_amd.require_gpu()
     world = 2
     ctx = mp.get_context("spawn")

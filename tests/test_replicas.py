@@ -1,4 +1,4 @@
-"""bench.py's multi-process path on CPU (gloo, world size 2).
+"""bench.py's multi-process path on CPU (world size 2, host sockets).
 
 dfl001 does not shard: N ranks run independent replicas,
 the timed region is bracketed by barriers and the reported time is the
@@ -27,7 +27,7 @@ def _rank_main(rank, world, port, q):
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, REPO)
     import bench
-    d = bench.Dist(backend="gloo")
+    d = bench.Dist()
     # uneven per-rank work: rank r "iterates" (r + 1) * 3 times, 20 ms each
     iters = (rank + 1) * 3
 
@@ -46,7 +46,7 @@ def _rank_main(rank, world, port, q):
 
 @pytest.mark.timeout(120)
 def test_replicas_max_time_and_sum_over_two_gloo_ranks():
-    import torch.multiprocessing as mp
+    import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -1,0 +1,28 @@
+#!/usr/bin/env python3
+"""GPU side of the dependent-pivot investigation (developer tool): run the
+ipo_hip driver on the given problems with IPO_HIP_DUMP_DIR (every
+factorisation's input and classification, kkt_device.hip dump_factor) and
+IPO_HIP_TRACE_FULL (full-precision iterate scalars on stderr).
+usage: tools/gpu_dump.py <outdir> name[:method] ...   (method: hsd, intpt, hsdls)"""
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+from conftest import mps_path  # noqa: E402
+
+EXE = os.path.join(REPO, "linear-programming-vanderbei_amd", "bin", "ipo_hip")
+out = sys.argv[1]
+for spec in sys.argv[2:]:
+    name, _, method = spec.partition(":")
+    method = method or "hsd"
+    d = os.path.join(out, f"{name}.{method}")
+    os.makedirs(d, exist_ok=True)
+    env = dict(os.environ, IPO_HIP_DUMP_DIR=d, IPO_HIP_TRACE_FULL="1")
+    r = subprocess.run([EXE, mps_path(name), method], capture_output=True, text=True, env=env, timeout=300)
+    with open(os.path.join(d, "trace.txt"), "w") as fh:
+        fh.write(r.stdout)
+    with open(os.path.join(d, "stderr.txt"), "w") as fh:
+        fh.write(r.stderr)
+    print(spec, r.returncode, r.stdout.strip().splitlines()[-1] if r.stdout.strip() else "", flush=True)
