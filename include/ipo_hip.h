@@ -124,6 +124,18 @@ ipo_hip_ctx *ipo_hip_ctx_create_shard(int m, int n, const int *kA, const int *iA
  * minus the .out file.  Returns the status (3 = free variable). */
 int ipo_hip_run_mps(const char *path, int method, FILE *out, int timing, ipo_hip_stats *stats);
 
+/* ipo_hip_run_mps with options.  flags: IPO_HIP_SPLIT_FREE -- the
+ * free-variable extension (not in the reference, which returns 3 "dual
+ * unbounded" at solve.c:79-87): free columns are split (x = x+ - x-) or
+ * reflected (x = u - x') before the normalisation (lp_io.h
+ * split_free_columns).  solfile != NULL: the reference's writesol report
+ * (iolp.c:976-1045, main.c:54-56 writes it to <NAME>.out) for the original
+ * problem, z as solver() returned it (the reference reads it after freeing
+ * it, hsd.c:290-291). */
+#define IPO_HIP_SPLIT_FREE 1
+int ipo_hip_run_mps_ex(const char *path, int method, int flags, const char *solfile, FILE *out, int timing,
+                       ipo_hip_stats *stats);
+
 /* Dimensions of an MPS file after normalisation (for tests/harnesses).
  * Returns 0, 3 (free variable) or the reader's error number. */
 int ipo_hip_mps_dims(const char *path, int *m0, int *n0, int *nz0, int *m, int *n, int *nz);
@@ -131,6 +143,16 @@ int ipo_hip_mps_dims(const char *path, int *m0, int *n0, int *nz0, int *m, int *
 /* Normalised problem export: caller passes NULL to query sizes first. */
 int ipo_hip_mps_load(const char *path, int *m, int *n, int *nz, int *kA, int *iA, double *A,
                      double *b, double *c, double *f);
+
+/* The writesol report (iolp.c:976-1045) of an MPS file from solver()-form
+ * vectors x (n + m), y (n + m), z (n) of its normalisation (host code, no
+ * device; ipo_hip_run_mps_ex calls the same writer).  0 on success. */
+int ipo_hip_write_sol(const char *path, int flags, const double *x, const double *y, const double *z,
+                      const char *solfile);
+
+/* ipo_hip_mps_load with the flags of ipo_hip_run_mps_ex. */
+int ipo_hip_mps_load_ex(const char *path, int flags, int *m, int *n, int *nz, int *kA, int *iA, double *A,
+                        double *b, double *c, double *f);
 
 /* KKT factor handle: symbolic + device numeric LDL' of K(E, D) for tests. */
 typedef struct ipo_hip_kkt ipo_hip_kkt;

@@ -259,6 +259,27 @@ ipo_hip_ctx* ipo_hip_ctx_create_shard(int m, int n, const int* kA, const int* iA
 }
 
 int ipo_hip_run_mps(const char* path, int method, FILE* out, int timing, ipo_hip_stats* stats) {
+    return ipo_hip_run_mps_ex(path, method, 0, nullptr, out, timing, stats);
+}
+
+namespace {
+// read + (optionally) split free columns + normalise; returns the
+// to_solver_form status (3: a free variable and no split requested)
+int load_form(const char* path, int flags, ipo::MpsProblem& p, ipo::MpsProblem& q, ipo::FreeMap& fm,
+              ipo::SolverForm& s, std::string& err, FILE* out) {
+    const int rc = ipo::read_mps(path, p, &err);
+    if (rc) return -rc;
+    if (out) std::fprintf(out, "m = %d,n = %d,nz = %d \n", p.m, p.n, p.kA.empty() ? 0 : p.kA[p.n]);
+    if (flags & IPO_HIP_SPLIT_FREE) {
+        ipo::split_free_columns(p, q, fm);
+        return ipo::to_solver_form(q, s);
+    }
+    return ipo::to_solver_form(p, s);
+}
+}  // namespace
+
+int ipo_hip_run_mps_ex(const char* path, int method, int flags, const char* solfile, FILE* out, int timing,
+                       ipo_hip_stats* stats) {
     if (out) {
         std::fprintf(out, "%s\n%s\n%s%5s%s\n%s\n%s\n", "\t+-------------------------------------------------+",
                      "\t                                                   ", "\t   ", "./ipo",
@@ -267,19 +288,19 @@ int ipo_hip_run_mps(const char* path, int method, FILE* out, int timing, ipo_hip
                      "\t+-------------------------------------------------+");
         std::fflush(out);
     }
-    ipo::MpsProblem p;
-    std::string err;
-    const int rc = ipo::read_mps(path, p, &err);
-    if (rc) {
-        set_err(err);
-        if (out) std::fprintf(out, "ERROR(%d): %s\n\n", rc, err.c_str());
-        return -rc;
-    }
-    if (out) std::fprintf(out, "m = %d,n = %d,nz = %d \n", p.m, p.n, p.kA.empty() ? 0 : p.kA[p.n]);
+    ipo::MpsProblem p, q;
+    ipo::FreeMap fm;
     ipo::SolverForm s;
-    int status = ipo::to_solver_form(p, s);
+    std::string err;
+    int status = load_form(path, flags, p, q, fm, s, err, out);
+    if (status < 0) {
+        set_err(err);
+        if (out) std::fprintf(out, "ERROR(%d): %s\n\n", -status, err.c_str());
+        return status;
+    }
     bool dev_err = false;
     if (stats) std::memset(stats, 0, sizeof(*stats));
+    std::vector<double> x(s.n + s.m, 0.0), y(s.n + s.m, 0.0), w(s.m > 0 ? s.m : 1, 0.0), z(s.n > 0 ? s.n : 1, 0.0);
     if (status == 0) {
         if (out && s.m < 7 && s.n < 7) {   // solve.c:210-222
             std::fprintf(out, "A: \n");
@@ -295,7 +316,6 @@ int ipo_hip_run_mps(const char* path, int method, FILE* out, int timing, ipo_hip
             for (int j = 0; j < s.n; j++) std::fprintf(out, "%10.5f \n", s.c[j]);
             std::fprintf(out, "\n");
         }
-        std::vector<double> x(s.n + s.m, 0.0), y(s.n + s.m, 0.0), w(s.m > 0 ? s.m : 1, 0.0), z(s.n > 0 ? s.n : 1, 0.0);
         status = solve_impl(method_from_int(method), s.m, s.n, s.nz, s.iA.data(),
                             s.kA.data(), s.A.data(), s.b.data(), s.c.data(), s.f, x.data(), y.data(), w.data(),
                             z.data(), out, 200, timing, stats, &dev_err);
@@ -305,6 +325,12 @@ int ipo_hip_run_mps(const char* path, int method, FILE* out, int timing, ipo_hip
         if (dev_err) std::fprintf(out, "device error: %s\n", g_err.c_str());
         else std::fprintf(out, "%s \n", kStatusText[status]);
         std::fflush(out);
+    }
+    if (solfile && !dev_err) {
+        const ipo::MpsProblem& src = (flags & IPO_HIP_SPLIT_FREE) ? q : p;
+        ipo::SolutionOut so = ipo::untransform(src, s, x.data(), y.data(), z.data());
+        if (flags & IPO_HIP_SPLIT_FREE) ipo::merge_split(p, fm, so);
+        if (ipo::write_sol(solfile, p, so, &err)) set_err(err);
     }
     return status;
 }
@@ -325,14 +351,34 @@ int ipo_hip_mps_dims(const char* path, int* m0, int* n0, int* nz0, int* m, int* 
     return st;
 }
 
+int ipo_hip_write_sol(const char* path, int flags, const double* x, const double* y, const double* z,
+                      const char* solfile) {
+    ipo::MpsProblem p, q;
+    ipo::FreeMap fm;
+    ipo::SolverForm s;
+    std::string err;
+    const int st = load_form(path, flags, p, q, fm, s, err, nullptr);
+    if (st < 0) { set_err(err); return -st; }
+    if (st) return st;
+    ipo::SolutionOut so = ipo::untransform((flags & IPO_HIP_SPLIT_FREE) ? q : p, s, x, y, z);
+    if (flags & IPO_HIP_SPLIT_FREE) ipo::merge_split(p, fm, so);
+    if (ipo::write_sol(solfile, p, so, &err)) { set_err(err); return 2; }
+    return 0;
+}
+
 int ipo_hip_mps_load(const char* path, int* m, int* n, int* nz, int* kA, int* iA, double* A, double* b, double* c,
                      double* f) {
-    ipo::MpsProblem p;
-    std::string err;
-    const int rc = ipo::read_mps(path, p, &err);
-    if (rc) { set_err(err); return rc; }
+    return ipo_hip_mps_load_ex(path, 0, m, n, nz, kA, iA, A, b, c, f);
+}
+
+int ipo_hip_mps_load_ex(const char* path, int flags, int* m, int* n, int* nz, int* kA, int* iA, double* A, double* b,
+                        double* c, double* f) {
+    ipo::MpsProblem p, q;
+    ipo::FreeMap fm;
     ipo::SolverForm s;
-    const int st = ipo::to_solver_form(p, s);
+    std::string err;
+    const int st = load_form(path, flags, p, q, fm, s, err, nullptr);
+    if (st < 0) { set_err(err); return -st; }
     if (st) return st;
     if (m) *m = s.m;
     if (n) *n = s.n;

@@ -80,6 +80,7 @@ int read_mps(const char* path, MpsProblem& P, std::string* err) {
             else if (!std::strcmp(word0, "RHS")) rhs_set = word1;
             else if (!std::strcmp(word0, "RANGES")) rng_set = word1;
             else if (!std::strcmp(word0, "BOUNDS")) bnd_set = word1;
+            else if (!std::strcmp(word0, "INFTOL")) P.inftol = std::atof(word1);
             break;
         case Section::Name:
             if (!std::strcmp(cd.buf, "ROW")) sec = Section::Rows;
@@ -104,6 +105,7 @@ int read_mps(const char* path, MpsProblem& P, std::string* err) {
             }
             row_id[lab] = static_cast<int>(row_kind.size());
             row_kind.push_back(kind);
+            P.rowlab.push_back(lab);
             P.r.push_back(rng);
             break;
         }
@@ -238,17 +240,169 @@ int read_mps(const char* path, MpsProblem& P, std::string* err) {
             renum[i] = mm;
             P.b[mm] = row_kind[i] == 1 ? -P.b[i] : P.b[i];
             P.r[mm] = P.r[i];
+            P.rowlab[mm] = P.rowlab[i];
             mm++;
         }
         for (int& i : P.iA) i = renum[i];
         P.b.resize(mm);
         P.r.resize(mm);
+        P.rowlab.resize(mm);
+        P.collab = col_name;
         P.m = mm;
         P.n = n;
     }
 finish:
     std::fclose(fp);
     return rc;
+}
+
+int split_free_columns(const MpsProblem& P, MpsProblem& Q, FreeMap& map) {
+    const int n = P.n, m = P.m;
+    Q = P;
+    map = FreeMap();
+    map.n = n;
+    map.shift.assign(n, 0.0);
+    std::vector<int> split;
+    for (int j = 0; j < n; j++)
+        if (P.l[j] == -HUGE_VAL) {
+            map.nfree++;
+            if (P.u[j] == HUGE_VAL) split.push_back(j);
+        }
+    const int n2 = n + static_cast<int>(split.size());
+    Q.n = n2;
+    Q.kA.assign(1, 0);
+    Q.iA.clear();
+    Q.A.clear();
+    Q.c.assign(n2, 0.0);
+    Q.l.assign(n2, 0.0);
+    Q.u.assign(n2, HUGE_VAL);
+    map.colmap.assign(n2, 0);
+    for (int j = 0; j < n; j++) {
+        const bool refl = P.l[j] == -HUGE_VAL && P.u[j] < HUGE_VAL;
+        const double sg = refl ? -1.0 : 1.0;
+        for (int k = P.kA[j]; k < P.kA[j + 1]; k++) {
+            Q.iA.push_back(P.iA[k]);
+            Q.A.push_back(sg * P.A[k]);
+            if (refl) Q.b[P.iA[k]] -= P.A[k] * P.u[j];
+        }
+        Q.kA.push_back(static_cast<int>(Q.iA.size()));
+        Q.c[j] = sg * P.c[j];
+        map.colmap[j] = refl ? -(j + 1) : (j + 1);
+        if (refl) {
+            Q.f += P.c[j] * P.u[j];
+            map.shift[j] = P.u[j];
+        } else {
+            Q.l[j] = P.l[j] == -HUGE_VAL ? 0.0 : P.l[j];
+            Q.u[j] = P.u[j];
+        }
+    }
+    int jn = n;
+    for (int j : split) {
+        for (int k = P.kA[j]; k < P.kA[j + 1]; k++) { Q.iA.push_back(P.iA[k]); Q.A.push_back(-P.A[k]); }
+        Q.kA.push_back(static_cast<int>(Q.iA.size()));
+        Q.c[jn] = -P.c[j];
+        map.colmap[jn] = -(j + 1);
+        jn++;
+    }
+    (void)m;
+    return map.nfree;
+}
+
+void FreeMap::recover(const double* xs, double* x) const {
+    for (int j = 0; j < n; j++) x[j] = shift[j];
+    for (size_t q = 0; q < colmap.size(); q++) {
+        const int c = colmap[q];
+        if (c > 0) x[c - 1] += xs[q];
+        else x[-c - 1] -= xs[q];
+    }
+}
+
+SolutionOut untransform(const MpsProblem& p, const SolverForm& s, const double* x, const double* y, const double* z) {
+    const int m = p.m, n = p.n;
+    SolutionOut o;
+    o.x.resize(n);
+    o.z.resize(n);
+    o.y.resize(m);
+    o.u = p.u;
+    o.b.resize(m);
+    for (int j = 0; j < n; j++) {
+        o.x[j] = x[j] + p.l[j];                         // solve.c:241
+        o.z[j] = z[j];
+        if (o.u[j] != HUGE_VAL) o.u[j] -= p.l[j];       // solve.c:103-104, in place in the reference's LP
+    }
+    // b - A l, negated (solve.c:105-109, :145); the y of the first m rows,
+    // negated for MIN (solve.c:247-250)
+    std::vector<double> al(m, 0.0);
+    for (int j = 0; j < n; j++)
+        for (int k = p.kA[j]; k < p.kA[j + 1]; k++) al[p.iA[k]] += p.A[k] * p.l[j];
+    for (int i = 0; i < m; i++) {
+        o.b[i] = -(p.b[i] - al[i]);
+        o.y[i] = s.sense == 1 ? -y[i] : y[i];
+    }
+    // rowact of writesol (iolp.c:1003-1007): the rebuilt A, whose first m rows
+    // are the negated originals (solve.c:142-146), times the shifted-back x
+    o.rowact.assign(m, 0.0);
+    for (int j = 0; j < n; j++)
+        for (int k = p.kA[j]; k < p.kA[j + 1]; k++) o.rowact[p.iA[k]] += o.x[j] * -p.A[k];
+    return o;
+}
+
+void merge_split(const MpsProblem& orig, const FreeMap& fm, SolutionOut& so) {
+    const int n = orig.n;
+    std::vector<double> x(n), z(n, 0.0);
+    fm.recover(so.x.data(), x.data());
+    for (int j = 0; j < n; j++) z[j] = fm.colmap[j] < 0 ? -so.z[j] : so.z[j];
+    // rows: the same rows, activity of the original columns
+    std::vector<double> ract(orig.m, 0.0);
+    for (int j = 0; j < n; j++)
+        for (int k = orig.kA[j]; k < orig.kA[j + 1]; k++) ract[orig.iA[k]] += x[j] * -orig.A[k];
+    std::vector<double> u(orig.u);
+    for (int j = 0; j < n; j++)
+        if (u[j] != HUGE_VAL && orig.l[j] != -HUGE_VAL) u[j] -= orig.l[j];
+    std::vector<double> al(orig.m, 0.0), b(orig.m);
+    for (int j = 0; j < n; j++)
+        if (orig.l[j] != -HUGE_VAL)
+            for (int k = orig.kA[j]; k < orig.kA[j + 1]; k++) al[orig.iA[k]] += orig.A[k] * orig.l[j];
+    for (int i = 0; i < orig.m; i++) b[i] = -(orig.b[i] - al[i]);
+    so.x.swap(x);
+    so.z.swap(z);
+    so.rowact.swap(ract);
+    so.u.swap(u);
+    so.b.swap(b);
+}
+
+int write_sol(const char* path, const MpsProblem& p, const SolutionOut& so, std::string* err) {
+    FILE* fp = std::fopen(path, "w");
+    if (!fp) { if (err) *err = std::string("cannot open file ") + path; return 2; }
+    const double eps = p.inftol * 1.2;
+    const std::vector<double>& l = p.l;
+    std::fprintf(fp, "COLUMNS SECTION\n");
+    std::fprintf(fp, "   index       label  primal_val reduced_cst");
+    std::fprintf(fp, "    lower_bd    upper_bd   OB_flag\n");
+    for (int j = 0; j < p.n; j++) {
+        const char* lab = p.collab[j].c_str();
+        const double x = so.x[j], z = so.z[j], u = so.u[j];
+        if (l[j] > -HUGE_VAL && u < HUGE_VAL) std::fprintf(fp, "%8d  %10s %11.4e %11.4e %11.4e %11.4e", j, lab, x, z, l[j], u);
+        else if (l[j] > -HUGE_VAL) std::fprintf(fp, "%8d  %10s %11.4e %11.4e %11.4e    Infinity", j, lab, x, z, l[j]);
+        else if (u < HUGE_VAL) std::fprintf(fp, "%8d  %10s %11.4e %11.4e   -Infinity %11.4e", j, lab, x, z, u);
+        else std::fprintf(fp, "%8d  %10s %11.4e %11.4e   -Infinity    Infinity", j, lab, x, z);
+        if (x < l[j] - eps || x > u + eps) std::fprintf(fp, "      OB\n");
+        else std::fprintf(fp, "\n");
+    }
+    std::fprintf(fp, "ROWS SECTION\n");
+    std::fprintf(fp, "   index       label    dual_val  row_actvty");
+    std::fprintf(fp, " rght_hnd_sd       range   OB_flag\n");
+    for (int i = 0; i < p.m; i++) {
+        const char* lab = p.rowlab[i].c_str();
+        const double r = p.r[i], b = so.b[i], ra = so.rowact[i];
+        if (r < HUGE_VAL) std::fprintf(fp, "%8d  %10s %11.4e %11.4e %11.4e %11.4e", i, lab, so.y[i], ra, b, r);
+        else std::fprintf(fp, "%8d  %10s %11.4e %11.4e %11.4e    Infinity", i, lab, so.y[i], ra, b);
+        if (ra < b - eps || ra > b + r + eps) std::fprintf(fp, "     OB\n");
+        else std::fprintf(fp, "\n");
+    }
+    std::fprintf(fp, "ENDOUT\n");
+    std::fclose(fp);
+    return 0;
 }
 
 void csc_transpose(int m, int n, const int* ka, const int* ia, const double* a,

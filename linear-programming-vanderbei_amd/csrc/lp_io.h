@@ -23,6 +23,8 @@ struct MpsProblem {
     std::vector<double> A, b, c, r, l, u;
     double f = 0.0;
     int sense = 1;                  // 1 = MIN, -1 = MAX
+    double inftol = 1.0e-5;         // INFTOL header keyword (iolp.c:98, :297)
+    std::vector<std::string> rowlab, collab;   // field text, trailing blanks kept (iolp.c:387, :422)
     std::vector<std::string> warnings;
 };
 
@@ -41,6 +43,45 @@ struct SolverForm {
 
 // Returns 0, or 3 ("dual unbounded") when a variable has no lower bound.
 int to_solver_form(const MpsProblem& p, SolverForm& s);
+
+// Free-variable extension (not in the reference, which aborts with status
+// 3, solve.c:79-87): an equivalent problem whose
+// every column has a finite lower bound.
+//   l = -inf, u = +inf : x = x+ - x-   column j keeps (a_j, c_j), l = 0; a
+//                        column (-a_j, -c_j), l = 0, is appended (appended
+//                        columns in order of j, after the original n);
+//   l = -inf, u finite : x = u - x'    column j becomes (-a_j, -c_j), l = 0,
+//                        u = inf; b -= a_j u, f += c_j u.
+// colmap[j'] = +(j+1) / -(j+1): x_j' enters x_j with that sign; shift[j] =
+// the u of a reflected column.  The same transform as the oracle's
+// orc_split_free (test infrastructure), so the two can be compared.
+struct FreeMap {
+    int n = 0, nfree = 0;
+    std::vector<int> colmap;        // [n'] signed 1-based original column
+    std::vector<double> shift;      // [n]
+    // x (n original columns) from the split problem's x' (n' columns, after
+    // the solver's lower-bound shift is undone)
+    void recover(const double* xs, double* x) const;
+};
+int split_free_columns(const MpsProblem& in, MpsProblem& out, FreeMap& map);
+
+// What writesol (iolp.c:976-1045) prints after solvelp has undone its
+// transform (solve.c:237-255): per original column x + l and z, per
+// original row the dual (negated for MIN) and the quantities writesol
+// reads from the LP as solvelp left it -- b (shifted by A l and negated,
+// solve.c:105-109, :145), u (shifted by l, :103-104) and the row activity
+// of the transformed, negated rows (rowact = -A x).  z is the solver's z:
+// the reference frees it in hsd.c:290-291 and writesol then reads freed
+// memory; here it is the value solver() returned.
+struct SolutionOut {
+    std::vector<double> x, z, y, rowact, b, u;
+};
+SolutionOut untransform(const MpsProblem& p, const SolverForm& s, const double* x, const double* y, const double* z);
+// A free-variable split problem's solution mapped back onto the original
+// columns (x_j = recovered, z_j = the dual slack of its first image).
+void merge_split(const MpsProblem& orig, const FreeMap& fm, SolutionOut& so);
+// writesol (iolp.c:976-1045): the COLUMNS / ROWS report to `path`.
+int write_sol(const char* path, const MpsProblem& p, const SolutionOut& so, std::string* err);
 
 // CSC transpose with the reference's stable order (linalg.c:75-103).
 void csc_transpose(int m, int n, const int* ka, const int* ia, const double* a,

@@ -68,7 +68,8 @@ PHASES = ["gather", "diag", "trsm", "tail_syrk", "forward", "backward"]
 
 EXPORTED = [
     "solver", "ldltfac", "forwardbackward", "inv_clo",
-    "ipo_hip_solve", "ipo_hip_run_mps", "ipo_hip_mps_dims", "ipo_hip_mps_load",
+    "ipo_hip_solve", "ipo_hip_run_mps", "ipo_hip_run_mps_ex", "ipo_hip_mps_dims", "ipo_hip_mps_load",
+    "ipo_hip_mps_load_ex", "ipo_hip_write_sol",
     "ipo_hip_kkt_create", "ipo_hip_kkt_destroy", "ipo_hip_kkt_factor", "ipo_hip_kkt_solve",
     "ipo_hip_kkt_info", "ipo_hip_kkt_perm", "ipo_hip_symbolic",
     "ipo_hip_device_count", "ipo_hip_device_synchronize", "ipo_hip_last_error", "ipo_hip_version",
@@ -107,6 +108,13 @@ def lib() -> C.CDLL:
     L.ipo_hip_solve.restype = _I
     L.ipo_hip_run_mps.argtypes = [C.c_char_p, _I, _P, _I, C.POINTER(Stats)]
     L.ipo_hip_run_mps.restype = _I
+    L.ipo_hip_run_mps_ex.argtypes = [C.c_char_p, _I, _I, C.c_char_p, _P, _I, C.POINTER(Stats)]
+    L.ipo_hip_run_mps_ex.restype = _I
+    L.ipo_hip_mps_load_ex.argtypes = [C.c_char_p, _I, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), _P, _P, _P, _P, _P,
+                                      C.POINTER(_D)]
+    L.ipo_hip_mps_load_ex.restype = _I
+    L.ipo_hip_write_sol.argtypes = [C.c_char_p, _I, _P, _P, _P, C.c_char_p]
+    L.ipo_hip_write_sol.restype = _I
     L.ipo_hip_mps_dims.argtypes = [C.c_char_p] + [C.POINTER(_I)] * 6
     L.ipo_hip_mps_dims.restype = _I
     L.ipo_hip_mps_load.argtypes = [C.c_char_p, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I), _P, _P, _P, _P, _P,
@@ -225,11 +233,18 @@ def mps_dims(path: str):
     return tuple(x.value for x in v) + (st,)
 
 
-def load_mps(path: str) -> SolverForm:
-    """Read + normalise an MPS file with the native front end (lp_io.cpp)."""
+SPLIT_FREE = 1      # include/ipo_hip.h IPO_HIP_SPLIT_FREE
+
+
+def load_mps(path: str, free: str = "abort") -> SolverForm:
+    """Read + normalise an MPS file with the native front end (lp_io.cpp).
+    free="split": the free-variable extension (split / reflected columns)
+    instead of the reference's abort (status 3)."""
     L = lib()
+    fl = SPLIT_FREE if free == "split" else 0
     m, n, nz = C.c_int(0), C.c_int(0), C.c_int(0)
-    st = L.ipo_hip_mps_load(path.encode(), C.byref(m), C.byref(n), C.byref(nz), None, None, None, None, None, None)
+    st = L.ipo_hip_mps_load_ex(path.encode(), fl, C.byref(m), C.byref(n), C.byref(nz), None, None, None, None, None,
+                               None)
     if st:
         raise IpoHipError(f"mps load {path}: status {st} {last_error()}")
     kA = np.zeros(n.value + 1, np.int32)
@@ -238,9 +253,20 @@ def load_mps(path: str) -> SolverForm:
     b = np.zeros(m.value, np.float64)
     c = np.zeros(n.value, np.float64)
     f = C.c_double(0.0)
-    L.ipo_hip_mps_load(path.encode(), C.byref(m), C.byref(n), C.byref(nz), _ptr(kA), _ptr(iA), _ptr(A), _ptr(b),
-                       _ptr(c), C.byref(f))
+    L.ipo_hip_mps_load_ex(path.encode(), fl, C.byref(m), C.byref(n), C.byref(nz), _ptr(kA), _ptr(iA), _ptr(A), _ptr(b),
+                          _ptr(c), C.byref(f))
     return SolverForm(m.value, n.value, kA, iA, A, b, c, f.value)
+
+
+def write_sol(path: str, x, y, z, solfile: str, free: str = "abort") -> None:
+    """writesol (iolp.c:976-1045) of MPS file `path` from solver()-form
+    vectors of its normalisation (host code)."""
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    z = np.ascontiguousarray(z, np.float64)
+    if lib().ipo_hip_write_sol(path.encode(), SPLIT_FREE if free == "split" else 0, _ptr(x), _ptr(y), _ptr(z),
+                               solfile.encode()):
+        raise IpoHipError("write_sol: " + last_error())
 
 
 def _capture(fn):
@@ -260,12 +286,15 @@ def _capture(fn):
     return r, text
 
 
-def run_mps(path: str, method: str = "hsd", timing: bool = False):
-    """Equivalent of `ipo path` (main.c) on the GPU.  Returns (status, stdout text, stats dict)."""
+def run_mps(path: str, method: str = "hsd", timing: bool = False, free: str = "abort", solfile: str = None):
+    """Equivalent of `ipo path` (main.c) on the GPU.  Returns (status, stdout text, stats dict).
+    free="split": the free-variable extension; solfile: write the writesol report there."""
     require_gpu()
     st = Stats()
-    status, text = _capture(lambda fp: lib().ipo_hip_run_mps(path.encode(), METHODS[method], fp, int(timing),
-                                                            C.byref(st)))
+    fl = SPLIT_FREE if free == "split" else 0
+    status, text = _capture(lambda fp: lib().ipo_hip_run_mps_ex(path.encode(), METHODS[method], fl,
+                                                               solfile.encode() if solfile else None, fp, int(timing),
+                                                               C.byref(st)))
     return status, text, st.as_dict()
 
 

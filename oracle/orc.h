@@ -47,6 +47,7 @@ typedef struct {
     double fixed;          /* f                                               */
     int sense;             /* 1 = MIN (default), -1 = MAX                     */
     char name[256];
+    char **rowlab, **collab; /* [m], [n] field text (iolp.c:387, :422)        */
 } orc_mps;
 
 /* ---------- problem as handed to solver(): max c'x, Ax<=b, x>=0 ---------- */
@@ -69,6 +70,11 @@ void orc_mps_free(orc_mps *p);
 /* solve.c:28-205.  Returns 0, or 3 when a free variable is present
  * ("dual unbounded", solve.c:79-87).  Prints "m = ..,n = ..,nz = .. " to log. */
 int  orc_stdform(const orc_mps *in, orc_std *out, FILE *log);
+/* Free-variable extension (not in the reference): an equivalent problem
+ * with finite lower bounds only (split / reflected columns); see
+ * orc_stdform.c.  Q shares the label / name fields of P. */
+int  orc_split_free(const orc_mps *P, orc_mps *Q, int **colmap, double **shift);
+void orc_split_free_release(orc_mps *Q, int *colmap, double *shift);
 void orc_std_free(orc_std *p);
 
 /* ---------- KKT LDL^T (ldlt.c) ----------
@@ -131,6 +137,14 @@ int orc_hsdls(int m, int n, int nz, const int *iA, const int *kA, const double *
 double orc_linesearch(double xj, double zj, double dxj, double dzj, double beta, double delta, double mu);
 /* method: 0 hsd, 1 intpt, 2 hsdls */
 int orc_ipo_run(const char *mps_path, int method, FILE *out, orc_run *run);
+
+/* writesol (iolp.c:976-1045) for the problem P as read, from solver()'s
+ * x, y, z of its normalisation S (solve.c:237-255 undone here).  z is the
+ * solver's (the reference frees it, hsd.c:290-291, then reads it). */
+int orc_writesol(const char *path, const orc_mps *P, const orc_std *S, const double *x, const double *y,
+                 const double *z);
+
+int orc_writesol_mps(const char *mps, const double *x, const double *y, const double *z, const char *solfile);
 
 /* linalg.c helpers */
 double orc_dot(const double *x, const double *y, int n);

@@ -411,6 +411,20 @@ static const char *status_text[] = {
     "suboptimal solution"
 };
 
+/* writesol of an MPS file from solver()-form x, y, z (tests) */
+int orc_writesol_mps(const char *mps, const double *x, const double *y, const double *z, const char *solfile)
+{
+    orc_mps P;
+    int rc = orc_mps_read(mps, &P, NULL);
+    if (rc) return rc;
+    orc_std S;
+    int st = orc_stdform(&P, &S, NULL);
+    if (st == 0) st = orc_writesol(solfile, &P, &S, x, y, z);
+    orc_std_free(&S);
+    orc_mps_free(&P);
+    return st;
+}
+
 int orc_ipo_run(const char *path, int method, FILE *out, orc_run *run)
 {
     orc_run local; memset(&local, 0, sizeof(local));
@@ -429,7 +443,14 @@ int orc_ipo_run(const char *path, int method, FILE *out, orc_run *run)
     int rc = orc_mps_read(path, &P, out);
     if (rc) return -rc;
     orc_std S;
-    int status = orc_stdform(&P, &S, out);
+    int status;
+    if (getenv("ORC_FREE")) {   /* free-variable extension (orc_split_free) */
+        orc_mps Q; int *cm; double *sh;
+        orc_split_free(&P, &Q, &cm, &sh);
+        status = orc_stdform(&Q, &S, out);
+        orc_split_free_release(&Q, cm, sh);
+    } else
+        status = orc_stdform(&P, &S, out);
     if (status == 0) {
         int m = S.m, n = S.n;
         double *x = calloc((size_t)(n + m), sizeof(double)), *y = calloc((size_t)(n + m), sizeof(double));
@@ -437,6 +458,7 @@ int orc_ipo_run(const char *path, int method, FILE *out, orc_run *run)
         if (method == 1)      status = orc_intpt(m, n, S.nz, S.rowind, S.colptr, S.val, S.b, S.c, S.f, x, y, w, z, run);
         else if (method == 2) status = orc_hsdls(m, n, S.nz, S.rowind, S.colptr, S.val, S.b, S.c, S.f, x, y, w, z, run);
         else                  status = orc_hsd(m, n, S.nz, S.rowind, S.colptr, S.val, S.b, S.c, S.f, x, y, w, z, run);
+        if (getenv("ORC_SOLFILE") && !getenv("ORC_FREE")) orc_writesol(getenv("ORC_SOLFILE"), &P, &S, x, y, z);
         free(x); free(y); free(w); free(z);
     }
     if (out) { fprintf(out, "%s \n", status_text[status]); fflush(out); }

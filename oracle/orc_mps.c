@@ -100,7 +100,7 @@ int orc_mps_read(const char *path, orc_mps *P, FILE *log)
     int *colstart = NULL; double *up = NULL;
     int *ia = NULL; double *av = NULL;
     double *b = NULL, *c = NULL, *lo = NULL;
-    char **collab = NULL;
+    char **collab = NULL, **rowlab = NULL;
 
     char line[240], w0[256] = "", w1[256] = "";
     line[79] = '\0';
@@ -138,6 +138,8 @@ int orc_mps_read(const char *path, orc_mps *P, FILE *log)
             }
             GROW(kind, mcap, m, int);
             rng = realloc(rng, (size_t)mcap * sizeof(double));
+            rowlab = realloc(rowlab, (size_t)mcap * sizeof(char *));
+            rowlab[m] = strdup(l0);
             {
                 char t = ty[0] == ' ' ? ty[1] : ty[0];
                 if (t == 'L')      { rng[m] = HUGE_VAL; kind[m] = 1; }
@@ -264,12 +266,16 @@ int orc_mps_read(const char *path, orc_mps *P, FILE *log)
         int *newrow = malloc((size_t)(m > 0 ? m : 1) * sizeof(int));
         int mnew = 0;
         for (int i = 0; i < m; i++) {
-            if (i == ic || kind[i] == 2) continue;
+            if (i == ic || kind[i] == 2) { free(rowlab[i]); rowlab[i] = NULL; continue; }
             newrow[i] = mnew;
             b[mnew] = kind[i] == 1 ? -b[i] : b[i];
             rng[mnew] = rng[i];
+            char *keep = rowlab[i];
+            rowlab[i] = NULL;
+            rowlab[mnew] = keep;   /* i >= mnew: slot i was read before it is reused */
             mnew++;
         }
+        for (int i = mnew; i < m; i++) { free(rowlab[i]); rowlab[i] = NULL; }
         for (int k = 0; k < nz; k++) ia[k] = newrow[ia[k]];
         free(newrow);
         m = mnew;
@@ -280,12 +286,15 @@ int orc_mps_read(const char *path, orc_mps *P, FILE *log)
     P->rhs = b; P->obj = c; P->range = rng; P->lo = lo; P->hi = up;
     P->fixed = 0.0; P->sense = sense;
     strncpy(P->name, nm, 255);
+    P->rowlab = rowlab; P->collab = collab;
     colstart = NULL; ia = NULL; av = NULL; b = c = rng = lo = up = NULL;
+    rowlab = collab = NULL;
 
 done:
     fclose(fp);
     lbl_free(&rows); lbl_free(&cols);
     if (collab) { for (int j = 0; j < n; j++) free(collab[j]); free(collab); }
+    if (rowlab) { for (int i = 0; i < m; i++) free(rowlab[i]); free(rowlab); }
     free(kind);
     if (rc) { free(rng); free(colstart); free(up); free(ia); free(av); free(b); free(c); free(lo); }
     return rc;
@@ -293,6 +302,8 @@ done:
 
 void orc_mps_free(orc_mps *p)
 {
+    if (p->rowlab) { for (int i = 0; i < p->m; i++) free(p->rowlab[i]); free(p->rowlab); }
+    if (p->collab) { for (int j = 0; j < p->n; j++) free(p->collab[j]); free(p->collab); }
     free(p->colptr); free(p->rowind); free(p->val); free(p->rhs); free(p->obj);
     free(p->range); free(p->lo); free(p->hi);
     memset(p, 0, sizeof(*p));

@@ -30,9 +30,27 @@ def cli_path():
     return exe
 
 
-def run_cli(mps: str, method: str = "hsd", timeout: float = 3600) -> str:
-    out = subprocess.run([cli_path(), mps, method], capture_output=True, text=True, timeout=timeout)
+def run_cli(mps: str, method: str = "hsd", timeout: float = 3600, free: str = "abort", solfile: str = None) -> str:
+    """The oracle's `ipo` stdout.  free="split": the free-variable extension
+    (orc_split_free); solfile: its writesol report there."""
+    env = dict(os.environ)
+    if free == "split":
+        env["ORC_FREE"] = "1"
+    if solfile:
+        env["ORC_SOLFILE"] = solfile
+    out = subprocess.run([cli_path(), mps, method], capture_output=True, text=True, timeout=timeout, env=env)
     return out.stdout
+
+
+def write_sol(mps: str, x, y, z, solfile: str) -> int:
+    """orc_writesol_mps: the oracle's writesol restatement from solver()-form vectors."""
+    L = lib()
+    L.orc_writesol_mps.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p]
+    L.orc_writesol_mps.restype = C.c_int
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    z = np.ascontiguousarray(z, np.float64)
+    return L.orc_writesol_mps(mps.encode(), x.ctypes.data, y.ctypes.data, z.ctypes.data, solfile.encode())
 
 
 def lib():

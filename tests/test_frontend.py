@@ -38,3 +38,29 @@ def test_solver_form_is_well_formed(name):
         col = p.iA[p.kA[j]:p.kA[j + 1]]
         assert np.all(np.diff(col) > 0)
     assert p.iA.min() >= 0 and p.iA.max() < p.m
+
+
+# writesol (iolp.c:976-1045): the product's report (lp_io.cpp write_sol)
+# against the oracle's restatement (orc_writesol) from the same solver()-form
+# vectors -- the oracle's own HSD solution -- byte for byte.  The reference
+# holds no .out file, so this pins the writer to the oracle only (parity
+# unpinned against the reference itself); z is the solver's z in both (the
+# reference frees it before writesol reads it, hsd.c:290-291).
+WRITESOL = ["afiro", "adlittle", "boeing1", "bore3d", "e226", "fit1d", "kb2", "sc50a", "scorpion", "stocfor1"]
+
+
+@pytest.mark.parametrize("name", WRITESOL)
+def test_writesol_matches_oracle(name, tmp_path):
+    import oracle_lib
+    path = mps_path(name)
+    p = ipo_amd.load_mps(path)
+    r = oracle_lib.solve_arrays(p, "hsd")
+    a, b = str(tmp_path / "prod.out"), str(tmp_path / "orc.out")
+    ipo_amd.write_sol(path, r["x"], r["y"], r["z"], a)
+    assert oracle_lib.write_sol(path, r["x"], r["y"], r["z"], b) == 0
+    ta, tb = open(a).read(), open(b).read()
+    assert ta == tb
+    lines = ta.splitlines()
+    assert lines[0] == "COLUMNS SECTION" and lines[-1] == "ENDOUT"
+    m0, n0 = ipo_amd.mps_dims(path)[:2]
+    assert len(lines) == n0 + m0 + 5

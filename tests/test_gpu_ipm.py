@@ -275,3 +275,47 @@ def test_back_to_back_solves_on_one_context_identical():
         assert st1[k] == st2[k], k
     for a, b in zip(sol1, sol2):
         assert np.array_equal(a, b)
+
+
+FREE_FAST = ["capri", "modszk1", "stair", "tuff", "vtp.base"]
+
+
+@pytest.mark.parametrize("name", FREE_FAST)
+def test_split_free_hsd(name):
+    """The free-variable extension on the GPU (tests/test_free_vars.py): the
+    oracle's status on the same split problem and the netlib optimum within
+    the extension's bar."""
+    from test_free_vars import HSD_BAR, OPT, rows_status
+    path = mps_path(name)
+    status, text, st = ipo_amd.run_mps(path, "hsd", free="split")
+    rows, stat = rows_status(text)
+    ref = oracle_lib.run_cli(path, "hsd", free="split")
+    rrows, rstat = rows_status(ref)
+    assert text.splitlines()[:12] == ref.splitlines()[:12]       # banner, both dims lines, header, iteration 0
+    assert stat == rstat == "optimal solution"
+    o = OPT[name]
+    target = -o["sense"] * o["optimum"]
+    assert abs(float(rows[-1][1]) - target) <= HSD_BAR[name] * max(1.0, abs(target))
+
+
+@pytest.mark.parametrize("name", ["afiro", "boeing1", "e226"])
+def test_writesol_after_gpu_solve(name, tmp_path):
+    """ipo's <NAME>.out (main.c:54-56, iolp.c:976-1045) from the GPU solve
+    against the oracle's from its own solve: same layout, labels and flags;
+    numbers (printed %11.4e) within 1e-4 relative or 1e-7 absolute (both
+    solves stop at mu < 1e-12 from different summation orders)."""
+    path = mps_path(name)
+    a, b = str(tmp_path / "gpu.out"), str(tmp_path / "orc.out")
+    status, _, _ = ipo_amd.run_mps(path, "hsd", solfile=a)
+    oracle_lib.run_cli(path, "hsd", solfile=b)
+    la, lb = open(a).read().splitlines(), open(b).read().splitlines()
+    assert status == 0 and len(la) == len(lb)
+    num = re.compile(r"^-?\d\.\d{4}e[+-]\d\d$")
+    for x, y in zip(la, lb):
+        fx, fy = x.split(), y.split()
+        assert len(fx) == len(fy)
+        for u, v in zip(fx, fy):
+            if num.match(u) and num.match(v):
+                assert abs(float(u) - float(v)) <= max(1e-7, 1e-4 * abs(float(v))), (x, y)
+            else:
+                assert u == v, (x, y)

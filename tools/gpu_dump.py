@@ -20,7 +20,7 @@ for spec in sys.argv[2:]:
     d = os.path.join(out, f"{name}.{method}")
     os.makedirs(d, exist_ok=True)
     env = dict(os.environ, IPO_HIP_DUMP_DIR=d, IPO_HIP_TRACE_FULL="1")
-    r = subprocess.run([EXE, mps_path(name), method], capture_output=True, text=True, env=env, timeout=300)
+    r = subprocess.run([EXE, mps_path(name), method, "--no-out"], capture_output=True, text=True, env=env, timeout=300)
     with open(os.path.join(d, "trace.txt"), "w") as fh:
         fh.write(r.stdout)
     with open(os.path.join(d, "stderr.txt"), "w") as fh:

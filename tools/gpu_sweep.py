@@ -26,7 +26,7 @@ for name in available_problems():
         continue
     t0 = time.time()
     try:
-        out = subprocess.run([EXE, mps_path(name)], capture_output=True, text=True, timeout=int(os.environ.get("SWEEP_TIMEOUT", "120")))
+        out = subprocess.run([EXE, mps_path(name), "--no-out"], capture_output=True, text=True, timeout=int(os.environ.get("SWEEP_TIMEOUT", "120")))
         text, err = out.stdout, out.stderr
     except subprocess.TimeoutExpired:
         print(json.dumps({"name": name, "timeout": True}), flush=True)
