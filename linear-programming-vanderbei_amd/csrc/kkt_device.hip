@@ -1790,7 +1790,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     std::vector<int> kat, iat;
     std::vector<double> at;
     csc_transpose(m, n, kA, iA, A, kat, iat, at);
-    plan_ = build_kkt_plan(m, n, kA, iA, kat.data(), iat.data(), nforced);
+    double tail_density = 1.0;
+    if (const char* e = std::getenv("IPO_HIP_TAIL_DENSITY")) tail_density = std::atof(e);
+    plan_ = build_kkt_plan(m, n, kA, iA, kat.data(), iat.data(), nforced, tail_density);
     if (nforced > 0) dLinkAx_.alloc(2 * static_cast<size_t>(nforced));
     const int nz = kA[n];
     hipStream_t s = stream_;

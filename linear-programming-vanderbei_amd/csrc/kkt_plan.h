@@ -153,7 +153,10 @@ struct KktPlan {
     double bytes_update = 0.0;      // algorithmic bytes of k_update per factorisation
 };
 
+// tail_density < 1: the dense tail starts at the longest suffix of columns
+// whose lower triangle is at least that full (1: only the full triangle,
+// the reference's dense window)
 KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
-                       int nforced = 0);
+                       int nforced = 0, double tail_density = 1.0);
 
 }  // namespace ipo

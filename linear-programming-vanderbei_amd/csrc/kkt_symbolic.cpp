@@ -316,7 +316,8 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
     return o;
 }
 
-KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced) {
+KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced,
+                       double tail_density) {
     KktOrdering o = order_tiered_min_degree(m, n, kA, iA, kAt, iAt, nforced);
     KktPlan P;
     P.m = m; P.n = n; P.T = o.T;
@@ -337,6 +338,22 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
         tc = T - nforced;               // the tail is exactly the forced rows
     } else {
         while (tc > 0 && cnt[tc - 1] == T - tc) tc--;
+        // optionally widen the dense tail to the longest suffix whose lower
+        // triangle is still at least `rho` full (structural zeros stay exact
+        // zeros in the dense factor): the narrow, tall supernodes just below
+        // the reference's dense window then become 64-column MFMA blocks
+        // instead of one elimination level each
+        if (tail_density < 1.0 && tc < T) {
+            double nnz = 0.5 * double(T - tc) * double(T - tc - 1);
+            int best = tc;
+            for (int j = tc - 1; j >= 0; j--) {
+                nnz += cnt[j];
+                const double nt = T - j;
+                if (nnz >= tail_density * 0.5 * nt * (nt - 1)) best = j;
+                else if (nnz < 0.5 * tail_density * 0.5 * nt * (nt - 1)) break;
+            }
+            tc = best;
+        }
         if (T - tc < kTailMin) tc = T;
     }
     P.tail_c0 = tc;

@@ -70,6 +70,7 @@ void orc_mps_free(orc_mps *p);
 /* solve.c:28-205.  Returns 0, or 3 when a free variable is present
  * ("dual unbounded", solve.c:79-87).  Prints "m = ..,n = ..,nz = .. " to log. */
 int  orc_stdform(const orc_mps *in, orc_std *out, FILE *log);
+int  orc_stdform_quiet(const orc_mps *in, orc_std *out, FILE *log);   /* without the dims line */
 /* Free-variable extension (not in the reference): an equivalent problem
  * with finite lower bounds only (split / reflected columns); see
  * orc_stdform.c.  Q shares the label / name fields of P. */

@@ -447,7 +447,8 @@ int orc_ipo_run(const char *path, int method, FILE *out, orc_run *run)
     if (getenv("ORC_FREE")) {   /* free-variable extension (orc_split_free) */
         orc_mps Q; int *cm; double *sh;
         orc_split_free(&P, &Q, &cm, &sh);
-        status = orc_stdform(&Q, &S, out);
+        if (out) fprintf(out, "m = %d,n = %d,nz = %d \n", P.m, P.n, P.nz);   /* the problem as read */
+        status = orc_stdform_quiet(&Q, &S, out);
         orc_split_free_release(&Q, cm, sh);
     } else
         status = orc_stdform(&P, &S, out);

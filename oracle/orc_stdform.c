@@ -19,9 +19,17 @@
 
 int orc_stdform(const orc_mps *P, orc_std *S, FILE *log)
 {
+    if (log) fprintf(log, "m = %d,n = %d,nz = %d \n", P->m, P->n, P->nz);
+    return orc_stdform_quiet(P, S, log);
+}
+
+/* orc_stdform without the solve.c:62 dimension line (the free-variable
+ * extension prints the dimensions of the problem as read, then normalises
+ * its split form) */
+int orc_stdform_quiet(const orc_mps *P, orc_std *S, FILE *log)
+{
     memset(S, 0, sizeof(*S));
     int m = P->m, n = P->n, nz = P->nz;
-    if (log) fprintf(log, "m = %d,n = %d,nz = %d \n", m, n, nz);
 
     S->m0 = m; S->n0 = n; S->sense = P->sense;
     for (int j = 0; j < n; j++)

@@ -13,6 +13,8 @@ from conftest import available_problems, golden_trace, mps_path  # noqa: E402
 
 EXE = os.path.join(REPO, "linear-programming-vanderbei_amd", "bin", "ipo_hip")
 SKIP = set(os.environ.get("SWEEP_SKIP", "").split(","))
+SAVE = os.environ.get("SWEEP_SAVE")          # directory for the full traces (name.method.txt)
+METHOD = os.environ.get("SWEEP_METHOD", "hsd")
 
 
 def iters_and_last(text):
@@ -26,8 +28,13 @@ for name in available_problems():
         continue
     t0 = time.time()
     try:
-        out = subprocess.run([EXE, mps_path(name), "--no-out"], capture_output=True, text=True, timeout=int(os.environ.get("SWEEP_TIMEOUT", "120")))
+        out = subprocess.run([EXE, mps_path(name), METHOD, "--no-out"], capture_output=True, text=True,
+                             timeout=int(os.environ.get("SWEEP_TIMEOUT", "120")))
         text, err = out.stdout, out.stderr
+        if SAVE:
+            os.makedirs(SAVE, exist_ok=True)
+            with open(os.path.join(SAVE, f"{name}.{METHOD}.txt"), "w") as fh:
+                fh.write(text)
     except subprocess.TimeoutExpired:
         print(json.dumps({"name": name, "timeout": True}), flush=True)
         continue
