@@ -318,7 +318,7 @@ int ipo_hip_run_mps_ex(const char* path, int method, int flags, const char* solf
         }
         status = solve_impl(method_from_int(method), s.m, s.n, s.nz, s.iA.data(),
                             s.kA.data(), s.A.data(), s.b.data(), s.c.data(), s.f, x.data(), y.data(), w.data(),
-                            z.data(), out, 200, timing, stats, &dev_err);
+                            z.data(), out, 0, timing, stats, &dev_err);   // 0: the method's MAX_ITER
     }
     // a device / host exception is not a numerical outcome: no status text for it
     if (out) {

@@ -1790,7 +1790,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     std::vector<int> kat, iat;
     std::vector<double> at;
     csc_transpose(m, n, kA, iA, A, kat, iat, at);
-    double tail_density = 1.0;
+    // the dense tail reaches down to the longest suffix at least 70 % full
+    // (IPO_HIP_TAIL_DENSITY=1: only the reference's full dense window)
+    double tail_density = kTailDensity;
     if (const char* e = std::getenv("IPO_HIP_TAIL_DENSITY")) tail_density = std::atof(e);
     plan_ = build_kkt_plan(m, n, kA, iA, kat.data(), iat.data(), nforced, tail_density);
     if (nforced > 0) dLinkAx_.alloc(2 * static_cast<size_t>(nforced));

@@ -27,6 +27,8 @@ constexpr int kPanelCols = 64;     // max columns per supernode panel
 constexpr int kTileRows = 64;      // rows per factor work unit
 constexpr int kSlab = 16;         // k-columns staged per MFMA gather step
 constexpr int kTailMin = 128;      // smallest dense tail handled as a dense block
+constexpr int kTailMaxWiden = 8192;   // a widened dense tail stays within 8192 columns (512 MB)
+constexpr double kTailDensity = 0.7;  // default suffix density of the widened tail (measured)
 
 struct KktOrdering {
     int m = 0, n = 0, T = 0;

@@ -346,7 +346,7 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
         if (tail_density < 1.0 && tc < T) {
             double nnz = 0.5 * double(T - tc) * double(T - tc - 1);
             int best = tc;
-            for (int j = tc - 1; j >= 0; j--) {
+            for (int j = tc - 1; j >= 0 && T - j <= kTailMaxWiden; j--) {
                 nnz += cnt[j];
                 const double nt = T - j;
                 if (nnz >= tail_density * 0.5 * nt * (nt - 1)) best = j;

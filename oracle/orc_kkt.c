@@ -301,27 +301,64 @@ static void numeric_ldlt(orc_kkt *K)
     for (int v = 0; v < T; v++) if (dabs(d[v]) > dmaxabs) dmaxabs = dabs(d[v]);
     K->ndep = 0;
 
+    /* Stability probe (test infrastructure, tools/rounding_stability.py):
+     * ORC_PERTURB=reverse / sorted applies the contributions of the columns
+     * j to column col in the reverse of the reference's linked-list order /
+     * in increasing j -- the same algorithm and operations, another
+     * summation order (like any other implementation's).  The list itself
+     * is maintained exactly as lltnum does. */
+    static int perturb = -1;
+    if (perturb < 0) {
+        const char *e = getenv("ORC_PERTURB");
+        perturb = !e ? 0 : !strcmp(e, "reverse") ? 1 : !strcmp(e, "sorted") ? 2 : 0;
+    }
+    int *js = perturb ? malloc(sizeof(int) * (size_t)(T ? T : 1)) : NULL;
+    int *ks = perturb ? malloc(sizeof(int) * (size_t)(T ? T : 1)) : NULL;
+
     for (int col = 0; col < T; col++) {
         double piv = d[col];
         int sgn = K->perm[col] < m ? -1 : 1;
+        int nj = 0;
         for (int j = link[col], nxt; j != -1; j = nxt) {
             nxt = link[j];
             int k = first[j];
+            if (perturb) { js[nj] = j; ks[nj] = k; nj++; }
+            else {
             double lij = Lx[k];
             double lijdj = lij * d[j];
             piv -= lij * lijdj;
+            }
             int kb = k + 1, ke = Lp[j + 1];
             if (kb < ke) {
                 first[j] = kb;
                 int r = Li[kb];
                 link[j] = link[r];
                 link[r] = j;
+                if (perturb) continue;
+                double lijdj = Lx[k] * d[j];
                 if (j < K->denwin) {
                     for (int kk = kb; kk < ke; kk++) acc[Li[kk]] += lijdj * Lx[kk];
                 } else {
                     double *p = &acc[r];
                     for (int kk = kb; kk < ke; kk++) { *p += lijdj * Lx[kk]; p++; }
                 }
+            }
+        }
+        if (perturb && nj > 0) {
+            if (perturb == 2) {     /* increasing j (insertion sort on the pairs) */
+                for (int a = 1; a < nj; a++) {
+                    int jj = js[a], kk0 = ks[a], b = a - 1;
+                    while (b >= 0 && js[b] > jj) { js[b + 1] = js[b]; ks[b + 1] = ks[b]; b--; }
+                    js[b + 1] = jj; ks[b + 1] = kk0;
+                }
+            }
+            for (int q = 0; q < nj; q++) {
+                int idx = perturb == 1 ? nj - 1 - q : q;
+                int j = js[idx], k = ks[idx];
+                double lij = Lx[k];
+                double lijdj = lij * d[j];
+                piv -= lij * lijdj;
+                for (int kk = k + 1; kk < Lp[j + 1]; kk++) acc[Li[kk]] += lijdj * Lx[kk];
             }
         }
         int kb = Lp[col], ke = Lp[col + 1];
@@ -346,6 +383,8 @@ static void numeric_ldlt(orc_kkt *K)
             }
         }
     }
+    free(js);
+    free(ks);
 }
 
 void orc_kkt_factor(orc_kkt *K, const double *E, const double *D)

@@ -63,6 +63,23 @@ def _check_header_and_start(text, gold, rows, grows):
     assert rows[0][1:3] == grows[0][1:3]
 
 
+def _check_trajectory(rows, grows, mu_floor):
+    """Every printed iteration, not only the last: while the reference's mu
+    is at least mu_floor (1e-8; 1e-6 where the reference runs into its
+    iteration limit along a slow tail), the GPU's line of the same iteration
+    carries the same primal and dual objective to 1e-5 relative and the same
+    printed mu to 10 % (two printed digits).  Measured over the 58
+    rounding-stable problems with traces (round 3): objectives agree to
+    <= 1e-6 (pilot87 and greenbea, whose reference hits MAX_ITER, to 2e-6
+    above mu 1e-6), mu to the printed digit but for one 1.3e-8 vs 1.4e-8."""
+    for r, g in zip(rows, grows):
+        if g[5] < mu_floor:
+            break
+        assert r[0] == g[0]
+        assert rel(r[1], g[1]) <= 1e-5 and rel(r[3], g[3]) <= 1e-5, (r, g)
+        assert abs(r[5] - g[5]) <= 0.1 * g[5], (r, g)
+
+
 def _params(names):
     return [pytest.param(n, marks=pytest.mark.xfail(reason=f"known divergence {KNOWN_DIVERGENT[n]}", strict=False))
             if n in KNOWN_DIVERGENT else n for n in names]
@@ -79,6 +96,7 @@ def test_hsd_trace_matches_golden(name):
         # the reference ran out of iterations (MAX_ITER=200) on a problem it
         # was still converging on; finishing earlier is not a regression
         _check_header_and_start(text, gold, rows, grows)
+        _check_trajectory(rows, grows, 1e-6)
         assert rows[-1][5] < 1e-10
         return
     assert stat == gstat
@@ -86,6 +104,7 @@ def test_hsd_trace_matches_golden(name):
         assert not rows
         return
     _check_header_and_start(text, gold, rows, grows)
+    _check_trajectory(rows, grows, 1e-8 if gstat == "optimal solution" else 1e-6)
     assert abs(len(rows) - len(grows)) <= 1
     if stat == "optimal solution":
         tol = 1e-6 if grows[-1][2] < 1e-3 else 1e-4
