@@ -137,7 +137,14 @@ def block_angular_leg(d, args, sync):
     finally:
         ctx.close()
     iters = st["iters"]
-    return {"workload": BA_WORKLOAD, "value": iters / el, "unit": "iterations/s", "scaling": "strong",
+    # SURVEY.md 8(d)'s per-iteration work of every shard's own factor and
+    # solves (the replicated linking-row tail counted on each), summed over
+    # the ranks, against N x the per-GPU peak
+    fl, by = survey_work(st, loc.m, loc.n, loc.nz)
+    fl, by = d.sum(fl), d.sum(by)
+    roof = roofline_of(fl / d.world, by / d.world, el / max(iters, 1))
+    roof["per"] = "IPM iteration, per GPU (SURVEY.md 8(d) algorithmic work summed over the shards / N)"
+    return {"workload": BA_WORKLOAD, "value": iters / el, "roofline": roof, "unit": "iterations/s", "scaling": "strong",
             "n_gpus": d.world, "parallelism": f"shard{d.world}" if d.world > 1 else "one process",
             "exchange": "RCCL allreduce over xGMI" if d.world > 1 else "none (linking rows in the dense tail)",
             "ms_per_iteration": 1e3 * el / max(iters, 1), "iterations": iters,
@@ -148,6 +155,63 @@ def block_angular_leg(d, args, sync):
 
 
 WATCHDOG_EXIT = 3
+
+BANDED_WORKLOAD = ("synthetic random sparse LP, BASELINE configs[3] banded variant (SURVEY.md 8(d)): m=200,000, "
+                   "n=1,000,000, 4 nnz/column in a window of 256 rows around j m / n, seed 20251121, hsd")
+
+
+def survey_work(st, m, n, nz, solves=2):
+    """SURVEY.md 8(d)'s algorithmic work of one IPM iteration (the unit of the
+    roofline fraction): flops = narth + s (4 nnz(L) + N) + 2 nz (2 + 2 s),
+    bytes = 12 nnz(L) (2 + 2 s) + 12 nz (2 + 2 s) + 8 (m + n) 40, with s the
+    solves per iteration (2 for hsd) and N = m + n (the KKT dimension)."""
+    N, L = m + n, st["lnz"]
+    flops = st["narth"] + solves * (4.0 * L + N) + 2.0 * nz * (2 + 2 * solves)
+    byts = 12.0 * L * (2 + 2 * solves) + 12.0 * nz * (2 + 2 * solves) + 8.0 * N * 40
+    return flops, byts
+
+
+def roofline_of(flops, byts, seconds):
+    """The binding roofline of a (flops, bytes) workload done in `seconds`."""
+    if flops / (FP64_PEAK_TFLOPS * 1e12) >= byts / (HBM_PEAK_GBS * 1e9):
+        a = flops / seconds / 1e12
+        return {"bound": "mfma", "achieved": a, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": a / FP64_PEAK_TFLOPS,
+                "traffic": None, "algorithmic_flops": flops, "algorithmic_bytes": byts}
+    a = byts / seconds / 1e9
+    return {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS,
+            "traffic": None, "algorithmic_flops": flops, "algorithmic_bytes": byts}
+
+
+def banded_leg(args):
+    """BASELINE configs[3], banded variant: the whole HSD solve (factor +
+    refined solves every iteration) on one GPU; it/s and the roofline
+    fraction of SURVEY.md 8(d)'s per-iteration work.  A second, short run
+    (5 iterations, HIP events) splits the time by phase."""
+    import ipo_amd
+    t0 = time.perf_counter()
+    p = ipo_amd.synth_random(200000, 1000000, 4, 256)
+    t_gen = time.perf_counter() - t0
+    ctx = ipo_amd.Context(p)
+    try:
+        t0 = time.perf_counter()
+        status, st, _ = ctx.run("hsd")
+        el = time.perf_counter() - t0
+        _, stt, _ = ctx.run("hsd", max_iter=5, timing=True)
+    finally:
+        ctx.close()
+    it = st["iters"]
+    flops, byts = survey_work(st, p.m, p.n, p.nz)
+    roof = roofline_of(flops, byts, el / max(it, 1))
+    roof["per"] = "IPM iteration (SURVEY.md 8(d) algorithmic work)"
+    ph = {name: {"ms_per_iteration": stt["phase_ms"][i] / 5, "launches_per_iteration": stt["phase_launches"][i] / 5}
+          for i, name in enumerate(ipo_amd.PHASES) if stt["phase_launches"][i]}
+    return {"workload": BANDED_WORKLOAD, "value": it / el, "unit": "iterations/s", "n_gpus": 1,
+            "ms_per_iteration": 1e3 * el / max(it, 1), "iterations": it, "status": ipo_amd.STATUS_TEXT.get(status, status),
+            "final_mu": st["final_mu"], "final_pobj": st["final_pobj"], "final_dobj": st["final_dobj"],
+            "m": p.m, "n": p.n, "nz": p.nz, "lnz": st["lnz"], "nsup": st["nsup"], "levels": st["nlevels"],
+            "refine_passes": st["refine_passes"], "setup_s": ctx.setup_seconds, "generate_s": t_gen,
+            "roofline": roof, "phases_first_5_iterations": ph,
+            "round1_reference_value": 1.8}
 
 
 HBM_WORKLOAD = ("synthetic random sparse LP, BASELINE configs[3] uniform variant: m=200,000, n=1,000,000, "
@@ -207,6 +271,22 @@ def pmc_traffic(phase):
     return ph["hbm_bytes_per_launch"], os.path.basename(files[-1])
 
 
+def pmc_mfma():
+    """f64 MFMA utilisation per phase from the newest committed counter
+    summary (profiles/<round>_pmc_mfma.json, tools/profile_summary.py from a
+    rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_VALU_MFMA_MOPS_F64 /
+    GRBM_GUI_ACTIVE pass), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_mfma.json")))
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        d = json.load(fh)
+    return {"source": os.path.basename(files[-1]),
+            "phases": {k: {"mfma_util": v["mfma_util"], "f64_mfma_flops_per_launch": v["f64_mfma_flops_per_launch"]}
+                       for k, v in d.get("phases", {}).items()}}
+
+
 def cpu_baseline(mps, iters):
     """Oracle (single-threaded C restatement of ipo) on `iters` HSD iterations of dfl001."""
     import oracle_lib
@@ -260,6 +340,8 @@ def main():
     ap.add_argument("--ba-steps", type=int, default=200, help="MAX_ITER of the block-angular solve")
     ap.add_argument("--ba-warmup", type=int, default=2, help="untimed IPM iterations before the block-angular solve")
     ap.add_argument("--ba-timeout", type=float, default=300.0, help="watchdog for the block-angular leg (s)")
+    ap.add_argument("--banded", choices=["on", "off"], default="on",
+                    help="also solve BASELINE configs[3] banded (factor + solve throughput, reported under banded)")
     ap.add_argument("--hbm", choices=["on", "off"], default="on",
                     help="also time the HBM-bound vector kernels on BASELINE configs[3] (reported under hbm_roofline)")
     args = ap.parse_args()
@@ -328,6 +410,10 @@ def main():
         tr = pmc_traffic(top)
         if tr is not None:
             roof["traffic"], roof["traffic_source"] = tr
+        mf = pmc_mfma()
+        if mf is not None and top in mf["phases"]:
+            roof["mfma_util"] = mf["phases"][top]["mfma_util"]
+            roof["mfma_source"] = mf["source"]
         roof.update({"phase": top, "kernels": ph["kernels"], "avg_launch_us": ph["avg_launch_us"],
                      "launches": ph["launches"], "algorithmic_flops_per_launch": flops_l,
                      "algorithmic_bytes_per_launch": bytes_l, "share_of_timed_region": ph["share_of_timed_region"]})
@@ -351,6 +437,7 @@ def main():
                    "phase_timing": "second identical solve with HIP events" if not args.no_timing else None},
         "roofline": roof,
         "phases": phases,
+        "mfma_counters": pmc_mfma(),
         "cpu_baseline": None,
     }
     if d.rank == 0 and d.world == 1 and args.cpu_iters > 0:
@@ -366,6 +453,11 @@ def main():
             out["end_to_end"] = end_to_end(p, golden, sync)
         except Exception as e:  # noqa: BLE001 -- the headline number stands on its own
             out["end_to_end"] = {"error": repr(e)}
+    if args.banded == "on" and d.world == 1:
+        try:
+            out["banded"] = banded_leg(args)
+        except Exception as e:  # noqa: BLE001 -- the headline number stands on its own
+            out["banded"] = {"workload": BANDED_WORKLOAD, "error": repr(e)}
     if args.hbm == "on" and d.rank == 0:
         try:
             out["hbm_roofline"] = hbm_roofline_leg(20)

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <stdexcept>
 
 #include "dev_common.h"
 #include "hip_util.h"
@@ -1132,8 +1133,11 @@ void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, 
 
 void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,
                   int kb, hipStream_t s) {
-    if (fu_sup) {
+    // kb < 0: fused units of a sparse level (whose list pointer is null when
+    // the problem has none, so the pointer cannot tell the modes apart)
+    if (kb < 0) {
         if (count <= 0) return;
+        if (!fu_sup || !fu_j) throw std::runtime_error("launch_panel: sparse units without a unit list");
         hipLaunchKernelGGL(k_panel_w, dim3(count), dim3(PNT), 0, s, pv, fu_sup, fu_j, f0, tv, -1);
     } else {
         const int h = tv.nt - kb * PC;

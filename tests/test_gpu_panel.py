@@ -29,7 +29,7 @@ def _with_panel(kind, fn):
             os.environ["IPO_HIP_PANEL"] = old
 
 
-@pytest.mark.parametrize("name", ["afiro", "25fv47", "pds-02", "dfl001"])
+@pytest.mark.parametrize("name", ["afiro", "25fv47", "pds-02", "d6cube", "dfl001"])
 def test_panel_kinds_solve_bitwise(name):
     p = ipo_amd.load_mps(mps_path(name))
     rng = np.random.default_rng(7)

@@ -1,14 +1,17 @@
 #!/bin/bash
 # Round profile on the GPU box (developer tool):
-#   1. bench.py, default flags                 -> gpurun_out/<tag>_bench.log
-#   2. rocprofv3 --kernel-trace --stats, same  -> gpurun_out/<tag>_trace/
-#   3. two PMC passes (FETCH_SIZE, WRITE_SIZE) on one complete solve
-tag=${1:-r01}
+#   1. bench.py, default flags                           -> gpurun_out/<tag>_bench.log
+#   2. rocprofv3 --kernel-trace --stats, dfl001 solves   -> gpurun_out/<tag>_trace/
+#   3. PMC passes, one counter group each (rocprofv3 does not split passes):
+#      FETCH_SIZE, WRITE_SIZE, and the f64 MFMA counters
+# Every step must exit 0 (no tolerance for a non-zero profiler exit).
+tag=${1:-r03}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
+B="python3 bench.py --steps 2 --warmup 0 --cpu-iters 0 --block-angular off --hbm off --banded off"
 timeout -k 10 300 python3 bench.py > gpurun_out/${tag}_bench.log 2>&1 || exit 1
-# rocprofv3 has been seen to fault in its own finalisation after writing the
-# database (cooperative launches in the trace): go on when the database exists
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_trace -o run -- python3 bench.py --steps 2 --warmup 0 --block-angular off --hbm off > gpurun_out/${tag}_trace.log 2>&1 || test -s gpurun_out/${tag}_trace/run_results.db || exit 1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${tag}_pmc_fetch -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-iters 0 --no-timing --block-angular off --hbm off > gpurun_out/${tag}_pmc_fetch.log 2>&1 || test -s gpurun_out/${tag}_pmc_fetch/run_results.db || exit 1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${tag}_pmc_write -o run -- python3 bench.py --steps 1 --warmup 0 --cpu-iters 0 --no-timing --block-angular off --hbm off > gpurun_out/${tag}_pmc_write.log 2>&1 || test -s gpurun_out/${tag}_pmc_write/run_results.db || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_trace -o run -- $B > gpurun_out/${tag}_trace.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${tag}_pmc_fetch -o run -- $B --no-timing --steps 1 > gpurun_out/${tag}_pmc_fetch.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${tag}_pmc_write -o run -- $B --no-timing --steps 1 > gpurun_out/${tag}_pmc_write.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/${tag}_pmc_mfma -o run -- $B --no-timing --steps 1 > gpurun_out/${tag}_pmc_mfma.log 2>&1 || exit 1
+echo profile_round $tag done

@@ -80,6 +80,44 @@ with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:
     json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, bench.py --steps 1 --warmup 0 --no-timing "
                          "(dfl001 hsd, first 10 iterations); FETCH_SIZE doubled (gfx950)",
                "phases": phases, "kernels": kern}, fh, indent=1)
+# f64 MFMA utilisation per kernel / phase: SQ_VALU_MFMA_BUSY_CYCLES (MFMA-busy
+# cycles summed over the SIMDs) over GRBM_GUI_ACTIVE x SIMDs (1,024 on
+# MI355X: 256 CUs x 4); f64 MFMA flops from SQ_INSTS_VALU_MFMA_MOPS_F64
+# (units of 512 flops) over the kernel's trace duration
+mdb = os.path.join(src, f"{tag}_pmc_mfma", "run_results.db")
+if os.path.exists(mdb):
+    SIMDS = 1024
+    busy = per_kernel(mdb, "SQ_VALU_MFMA_BUSY_CYCLES")
+    mops = per_kernel(mdb, "SQ_INSTS_VALU_MFMA_MOPS_F64")
+    gui = per_kernel(mdb, "GRBM_GUI_ACTIVE")
+    sqb = per_kernel(mdb, "SQ_BUSY_CYCLES")
+    dur = {short(n): avg for n, _, _, avg, _ in rows}     # ns per launch, kernel-trace run
+    mk = {}
+    for k in busy:
+        b, n = busy[k]
+        g = gui.get(k, (0.0, 1))[0]
+        mo = mops.get(k, (0.0, 1))[0]
+        mk[k] = {"launches": n, "mfma_busy_cycles": b / n, "gui_active_cycles": g / n,
+                 "mfma_util": b / (g * SIMDS) if g else None, "f64_mfma_flops_per_launch": 512.0 * mo / n,
+                 "sq_busy_cycles": sqb.get(k, (0.0, 1))[0] / n}
+        if k in dur and dur[k]:
+            mk[k]["f64_mfma_tflops"] = mk[k]["f64_mfma_flops_per_launch"] / (dur[k] * 1e-9) / 1e12
+    mph = {}
+    for ph, names in PHASE_KERNELS.items():
+        want = set(re.split(r"[|+]", names))
+        ks = [k for k in mk if base(k) in want]
+        b = sum(mk[k]["mfma_busy_cycles"] * mk[k]["launches"] for k in ks)
+        g = sum(mk[k]["gui_active_cycles"] * mk[k]["launches"] for k in ks)
+        f = sum(mk[k]["f64_mfma_flops_per_launch"] * mk[k]["launches"] for k in ks)
+        nl = sum(mk[k]["launches"] for k in ks)
+        if nl:
+            mph[ph] = {"kernels": ks, "launches": nl, "mfma_util": b / (g * SIMDS) if g else None,
+                       "f64_mfma_flops_per_launch": f / nl}
+    with open(os.path.join(dst, f"{tag}_pmc_mfma.json"), "w") as fh:
+        json.dump({"source": "rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES "
+                             "GRBM_GUI_ACTIVE, bench.py --steps 1 --warmup 0 --no-timing (dfl001 hsd); util = "
+                             "MFMA-busy cycles / (GRBM_GUI_ACTIVE x 1024 SIMDs); MOPS_F64 in units of 512 flops",
+                   "phases": mph, "kernels": mk}, fh, indent=1)
 line = [ln for ln in open(os.path.join(src, f"{tag}_bench.log")) if ln.startswith("{")][-1]
 with open(os.path.join(dst, f"{tag}_bench.json"), "w") as fh:
     fh.write(line)
