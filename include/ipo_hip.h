@@ -163,6 +163,9 @@ int    ipo_hip_kkt_solve(ipo_hip_kkt *k, const double *E, const double *D, doubl
 int    ipo_hip_kkt_info(const ipo_hip_kkt *k, long *lnz, double *narth, int *nsup, int *nlevels, int *denwin,
                         int *pdf, double *epsdiag, int *ndep, int *passes);
 int    ipo_hip_kkt_perm(const ipo_hip_kkt *k, int *perm);
+/* the last factor's pivots D (diag of ldlt.c's lltnum, new order) and live
+ * marks (0 = dependent pivot, ldlt.c:600-614), T = m + n entries each */
+int    ipo_hip_kkt_pivots(const ipo_hip_kkt *k, double *d, int *live);
 /* start from a captured state: the reference's eps_diag floor (ldlt.c:31,301-305) */
 void   ipo_hip_kkt_set_epsdiag(ipo_hip_kkt *k, double epsdiag);
 

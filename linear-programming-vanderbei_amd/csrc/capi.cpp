@@ -525,6 +525,16 @@ int ipo_hip_kkt_perm(const ipo_hip_kkt* k, int* perm) {
 
 void ipo_hip_kkt_set_epsdiag(ipo_hip_kkt* k, double e) { k->kkt->set_epsdiag(e); }
 
+int ipo_hip_kkt_pivots(const ipo_hip_kkt* k, double* d, int* live) {
+    try {
+        k->kkt->download_factor(nullptr, d, live);
+        return 0;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "ipo_hip_kkt_pivots: %s\n", e.what());
+        return -1;
+    }
+}
+
 int ipo_hip_symbolic(int m, int n, const int* kA, const int* iA, int* perm, long* lnz, double* narth, int* denwin,
                      int* pdf, int* nsup, int* nlevels) {
     try {

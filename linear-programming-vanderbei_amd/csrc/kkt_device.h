@@ -110,7 +110,7 @@ class KktDevice {
     void reset_timers() { tm_ = KktTimers(); }
 
     // Diagnostics: copy numeric factor to host (panels + D), for tests.
-    void download_factor(double* lx, double* d) const;
+    void download_factor(double* lx, double* d, int* live = nullptr) const;
     double* device_lx() const { return dLx_.get(); }
     double* device_diag() const { return dDg_.get(); }
 

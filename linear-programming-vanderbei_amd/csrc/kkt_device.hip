@@ -2838,9 +2838,10 @@ int KktDevice::solve2(const double* dE, const double* dD, double* dfy1, double* 
     return ok[0] && ok[1];
 }
 
-void KktDevice::download_factor(double* lx, double* d) const {
+void KktDevice::download_factor(double* lx, double* d, int* live) const {
     if (lx) dLx_.download(lx, plan_.lx_size, stream_);
     if (d) dDg_.download(d, T_, stream_);
+    if (live) dLive_.download(live, T_, stream_);
     IPO_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 

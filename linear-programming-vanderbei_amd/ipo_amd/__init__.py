@@ -71,7 +71,7 @@ EXPORTED = [
     "ipo_hip_solve", "ipo_hip_run_mps", "ipo_hip_run_mps_ex", "ipo_hip_mps_dims", "ipo_hip_mps_load",
     "ipo_hip_mps_load_ex", "ipo_hip_write_sol",
     "ipo_hip_kkt_create", "ipo_hip_kkt_destroy", "ipo_hip_kkt_factor", "ipo_hip_kkt_solve",
-    "ipo_hip_kkt_info", "ipo_hip_kkt_perm", "ipo_hip_symbolic",
+    "ipo_hip_kkt_info", "ipo_hip_kkt_perm", "ipo_hip_kkt_pivots", "ipo_hip_symbolic",
     "ipo_hip_device_count", "ipo_hip_device_synchronize", "ipo_hip_last_error", "ipo_hip_version",
     "ipo_hip_ctx_create", "ipo_hip_ctx_run", "ipo_hip_ctx_download", "ipo_hip_ctx_destroy",
     "ipo_hip_ctx_setup_seconds", "ipo_hip_kkt_set_epsdiag",
@@ -133,6 +133,8 @@ def lib() -> C.CDLL:
     L.ipo_hip_kkt_info.restype = _I
     L.ipo_hip_kkt_perm.argtypes = [_P, _P]
     L.ipo_hip_kkt_perm.restype = _I
+    L.ipo_hip_kkt_pivots.argtypes = [_P, _P, _P]
+    L.ipo_hip_kkt_pivots.restype = _I
     L.ipo_hip_kkt_set_epsdiag.argtypes = [_P, _D]
     L.ipo_hip_kkt_set_epsdiag.restype = None
     L.ipo_hip_symbolic.argtypes = [_I, _I, _P, _P, _P, C.POINTER(C.c_long), C.POINTER(_D), C.POINTER(_I),
@@ -367,6 +369,14 @@ class KktFactor:
         p = np.zeros(self.m + self.n, np.int32)
         lib().ipo_hip_kkt_perm(self.h, _ptr(p))
         return p
+
+    def pivots(self):
+        """(D, live) of the last factorisation, new order."""
+        d = np.zeros(self.m + self.n)
+        live = np.zeros(self.m + self.n, np.int32)
+        if lib().ipo_hip_kkt_pivots(self.h, _ptr(d), _ptr(live)) != 0:
+            raise RuntimeError("ipo_hip_kkt_pivots failed")
+        return d, live
 
     def close(self):
         if self.h:

@@ -28,6 +28,11 @@
 #include <stdio.h>
 #include "orc.h"
 
+/* summation-order probe of numeric_ldlt (ORC_PERTURB, below); -1 = read the
+ * environment on first use; orc_set_perturb: 0 plain, 1 reverse, 2 sorted */
+static int g_perturb = -1;
+void orc_set_perturb(int p) { g_perturb = p; }
+
 #define EPS_PIVOT   1.0e-8   /* ldlt.c:27  */
 #define EPS_SOLVE   1.0e-6   /* ldlt.c:28  */
 #define EPS_NUM     0.0      /* ldlt.c:29  */
@@ -307,11 +312,11 @@ static void numeric_ldlt(orc_kkt *K)
      * in increasing j -- the same algorithm and operations, another
      * summation order (like any other implementation's).  The list itself
      * is maintained exactly as lltnum does. */
-    static int perturb = -1;
-    if (perturb < 0) {
+    if (g_perturb < 0) {
         const char *e = getenv("ORC_PERTURB");
-        perturb = !e ? 0 : !strcmp(e, "reverse") ? 1 : !strcmp(e, "sorted") ? 2 : 0;
+        g_perturb = !e ? 0 : !strcmp(e, "reverse") ? 1 : !strcmp(e, "sorted") ? 2 : 0;
     }
+    const int perturb = g_perturb;
     int *js = perturb ? malloc(sizeof(int) * (size_t)(T ? T : 1)) : NULL;
     int *ks = perturb ? malloc(sizeof(int) * (size_t)(T ? T : 1)) : NULL;
 

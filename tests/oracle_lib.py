@@ -79,6 +79,8 @@ def lib():
         L.orc_kkt_perm.argtypes = [P, P]
         L.orc_kkt_diag.argtypes = [P, P]
         L.orc_kkt_live.argtypes = [P, P]
+        L.orc_set_perturb.argtypes = [I]
+        L.orc_set_perturb.restype = None
         L.orc_kkt_set_epsdiag.argtypes = [P, D]
         _lib = L
     return _lib
