@@ -53,7 +53,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 METRIC = "IPM iterations/sec (ADA^T factor+solve) on netlib dfl001; duality gap ≤1e-8"
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, AMD spec (the guide has no fp64 row)
 PHASE_KERNELS = {"gather": "k_update",
-                 "diag": "k_panel_w|k_panel_s|k_tail_pr|k_diag|k_tail_diag_coop", "trsm": "k_trsm",
+                 "diag": "k_panel_w|k_panel_s|k_tail_pr|k_diag", "trsm": "k_trsm",
                  "tail_syrk": "k_tail_syrk",
                  "forward": "k_forward|k_fwd_diag|k_fwd_gemv|k_fwd_sf|k_tail_gather|k_tail_fwd|k_tail_fwd_chain",
                  "backward": "k_backward|k_bwd_partial|k_bwd_finish|k_bwd_sf|k_tail_dscale|k_tail_bwd|k_tail_bwd_chain"}

@@ -329,136 +329,6 @@ k_trsm(PlanView p, int u0, TailView tv, int kb) {
     solve_rows(DiagCtx{p.dscale, p.dg, p.live, p.flags, p.sign, p.tau}, panel, ld, nc, c0, rlo, rhi, wbuf, ldw, wrow0);
 }
 
-// ----------------------------------------- dense tail, dependent pivots
-// The redo path's diagonal block + rows below of one dense-tail block column
-// in one cooperative launch (every workgroup resident): workgroup g
-// factors the diagonal block redundantly in LDS exactly as factor_diag_block
-// does and keeps its own 64-row tile (rows nc + 64 g ..) solved column by
-// column as solve_rows does (l = a / d_k on live columns, a -= l (L11 d)),
-// so at a pivot that fails the zero test every tile already holds column k
-// after the updates of columns < k -- the values the reference's rule needs
-// (ldlt.c:600-614).  Each workgroup publishes the largest magnitude of its
-// tile's column k (and of the block's own rows), one grid barrier later
-// all reduce the same values in the same order and take the same decision.
-// Same operations per entry as k_diag + k_trsm (bitwise the same factor);
-// the tile rows cost one parallel pass instead of a partial substitution
-// per row per dependent pivot inside a single workgroup.
-__device__ __forceinline__ void grid_barrier(int* ctr, int nblocks, int gen) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < gen * nblocks)
-            __builtin_amdgcn_s_sleep(1);
-    }
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(NT)
-k_tail_diag_coop(PlanView p, TailView tv, int kb, double* __restrict__ gmax, int* __restrict__ gctr) {
-    __shared__ double B[PC][PC + 1];
-    __shared__ double dv[PC];
-    __shared__ int lv[PC];
-    __shared__ double dsc[PC];
-    __shared__ double red[4];
-    __shared__ double lk[PC];
-    __shared__ int ndep_sh;
-    const int k0 = kb * PC, nt = tv.nt, ld = nt;
-    const int nc = min(PC, nt - k0), h = nt - k0, c0 = tv.tc + k0;
-    double* panel = tv.S + k0 + (size_t)k0 * nt;
-    const int G = gridDim.x, g = blockIdx.x;
-    const int tid = threadIdx.x, tr = tid & 63, tp = tid >> 6, np = NT >> 6;
-    const int row = nc + g * TR + tr;
-    const bool rok = row < h;
-    for (int c = tp; c < nc; c += np) B[tr][c] = (tr < nc && tr >= c) ? panel[tr + (size_t)c * ld] : 0.0;
-    for (int k = tid; k < nc; k += NT) dsc[k] = p.dscale[c0 + k];
-    double a[16];
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-        const int c = 4 * q + tp;
-        const bool ok = rok && c < nc;
-        const double t = panel[ok ? row + (size_t)c * ld : 0];
-        a[q] = ok ? t : 0.0;
-    }
-    if (tid == 0) ndep_sh = 0;
-    int gen = 0;
-    __syncthreads();
-#pragma unroll
-    for (int qk = 0; qk < 16; qk++) {
-        for (int pk = 0; pk < 4; pk++) {
-            const int k = 4 * qk + pk;
-            if (k >= nc) break;
-            double dk = B[k][k];
-            int alive = 1;
-            if (fabs(dk) <= p.tau * dsc[k]) {           // wave-uniform (LDS values)
-                double mx = 0.0;
-                for (int r = k + 1 + tid; r < nc; r += NT) mx = ref_max(mx, ref_abs(B[r][k]));
-                if (tp == pk && rok) mx = ref_max(mx, ref_abs(a[qk]));
-                mx = wave_max(mx);
-                if (tr == 0) red[tp] = mx;
-                __syncthreads();
-                if (tid == 0) {
-                    double m2 = red[0];
-                    for (int q = 1; q < np; q++) m2 = ref_max(m2, red[q]);
-                    __hip_atomic_store(gmax + g, m2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                grid_barrier(gctr, G, ++gen);
-                if (tid == 0) {
-                    double m2 = __hip_atomic_load(gmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    for (int q = 1; q < G; q++)
-                        m2 = ref_max(m2, __hip_atomic_load(gmax + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    red[0] = m2;
-                }
-                grid_barrier(gctr, G, ++gen);                // every workgroup has read gmax
-                mx = red[0];
-                if (mx < 1.0e+6 * 1.0e-8) alive = 0;
-                else dk = (p.sign[c0 + k] < 0 ? -1.0 : 1.0) * 1.0e-8;
-                if (tid == 0) ndep_sh++;
-            }
-            if (tid == 0) { dv[k] = dk; lv[k] = alive; }
-            for (int r = k + 1 + tid; r < nc; r += NT) B[r][k] = alive ? B[r][k] / dk : 0.0;
-            if (tp == pk) {
-                const double l = alive ? a[qk] / dk : 0.0;
-                a[qk] = l;
-                lk[tr] = l;
-            }
-            __syncthreads();
-            if (alive && tr > k && tr < nc) {
-                const double lr = B[tr][k];
-                for (int c = k + 1 + tp; c <= tr; c += np) {
-                    const double tk = lr * (B[c][k] * dk);
-                    B[tr][c] -= tk;
-                    if (tr == c) dsc[c] += fabs(tk);
-                }
-            }
-            {
-                const double l = lk[tr];
-#pragma unroll
-                for (int q = 0; q < 16; q++) {
-                    const int c = 4 * q + tp;
-                    const double bk = (k < c && c < nc) ? B[c][k] * dk : 0.0;
-                    a[q] = c > k ? a[q] - l * bk : a[q];
-                }
-            }
-            __syncthreads();
-        }
-    }
-    if (rok) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) {
-            const int c = 4 * q + tp;
-            if (c < nc) {
-                panel[row + (size_t)c * ld] = a[q];
-                tv.W[(row) + (size_t)c * nt] = a[q] * dv[c];
-            }
-        }
-    }
-    if (g != 0) return;
-    for (int r = tp; r < nc; r += np)
-        if (tr < r) panel[tr + (size_t)r * ld] = B[r][tr];
-    for (int k = tid; k < nc; k += NT) { p.dg[c0 + k] = dv[k]; p.live[c0 + k] = lv[k]; }
-    if (tid == 0 && ndep_sh) atomicAdd(&p.flags[0], ndep_sh);
-}
-
 // ------------------------------------------------------------ fused panel
 // Diagonal block and the rows below it in one launch: the fast path of
 // k_diag + k_trsm (k_panel_w below).  A pivot that fails the zero test stops
@@ -1106,25 +976,6 @@ void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const doubl
 
 void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s) {
     if (tv.ntb - t - 1 > 0) hipLaunchKernelGGL(k_tail_col, dim3(tv.ntb - t - 1), dim3(PNT), 0, s, pv, tv, t, W);
-}
-
-bool launch_tail_diag_coop(const PlanView& pv, const TailView& tv, int kb, double* gmax, int* gctr, hipStream_t s) {
-    const int below = tv.nt - kb * PC - std::min(PC, tv.nt - kb * PC);
-    const int g = std::max(1, (below + TR - 1) / TR);
-    IPO_HIP_CHECK(hipMemsetAsync(gctr, 0, sizeof(int), s));
-    PlanView p = pv;
-    TailView t = tv;
-    void* args[] = {&p, &t, &kb, &gmax, &gctr};
-    // a cooperative launch is refused (not queued) when its workgroups cannot
-    // all be resident, e.g. beside another tenant: the caller then takes the
-    // two-kernel path, so the grid barrier can never wait on an absent peer
-    const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_tail_diag_coop), dim3(g), dim3(NT),
-                                                    args, 0, s);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return true;
 }
 
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s) {

@@ -215,9 +215,6 @@ class KktDevice {
     DevBuf<int> dtail_task_ptr_, dkslot_, dkslot_ptr_, dtail_kslot_, dtail_kslot_ptr_;
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;
-    bool coop_tail_ = false;       // redo path: k_tail_diag_coop instead of k_diag + k_trsm on the tail
-    DevBuf<double> dCoopMax_;      // its per-tile maxima
-    DevBuf<int> dCoopCtr_;         // its grid-barrier counter
     // numeric
     DevBuf<double> dLx_, dDg_;
     DevBuf<int> dLive_;

@@ -2039,16 +2039,6 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         static_assert(sizeof(TailTask) == 32, "TailTask layout");
         dtail_tasks_.upload(reinterpret_cast<const uint64_t*>(plan_.tail_tasks.data()), plan_.tail_tasks.size() * 4, s);
         dW_.alloc(2 * static_cast<size_t>(plan_.nt) * kPanelCols);   // two block columns (look-ahead tail)
-        {   // cooperative redo kernel for the tail: all tiles of a block column resident at once
-            int dev = 0, ncu = 0, coop = 0;
-            IPO_HIP_CHECK(hipGetDevice(&dev));
-            IPO_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-            IPO_HIP_CHECK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
-            coop_tail_ = coop != 0 && plan_.ntb <= ncu;
-            if (const char* e = std::getenv("IPO_HIP_COOP_TAIL")) coop_tail_ = coop_tail_ && std::atoi(e) != 0;
-            dCoopMax_.alloc(std::max(1, plan_.ntb));
-            dCoopCtr_.alloc(1);
-        }
         dChainFlags_.alloc(plan_.ntb);
         IPO_HIP_CHECK(hipMemsetAsync(dChainFlags_.get(), 0, plan_.ntb * sizeof(int), s));
         if (plan_.ntb <= kChainMaxBlocks) {
@@ -2389,8 +2379,6 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
             if (fused) {
                 launch_panel(pv, nullptr, nullptr, 0, 0, tv, kb, s);
                 ph_end(kPhDiag, 1, s);
-            } else if (coop_tail_ && launch_tail_diag_coop(pv, tv, kb, dCoopMax_.get(), dCoopCtr_.get(), s)) {
-                ph_end(kPhDiag, 1, s);     // dependent-pivot rule over all rows of the block column, one launch
             } else {
                 launch_diag(pv, nullptr, 0, 1, tv, kb, s);
                 ph_end(kPhDiag, 1, s);
@@ -2473,10 +2461,8 @@ void KktDevice::repair_tail() {
         tv.W = wbuf(tb);
         const int k0 = tb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0), below = plan_.nt - k0 - nc;
         ph_begin(s);
-        if (!(coop_tail_ && launch_tail_diag_coop(pv, tv, tb, dCoopMax_.get(), dCoopCtr_.get(), s))) {
-            launch_diag(pv, nullptr, 0, 1, tv, tb, s);
-            if (below > 0) launch_trsm(pv, 0, -1, tv, tb, s);
-        }
+        launch_diag(pv, nullptr, 0, 1, tv, tb, s);
+        if (below > 0) launch_trsm(pv, 0, -1, tv, tb, s);
         ph_end(kPhDiag, 1, s);
         for (int t = tb + 1; t < plan_.ntb; t++) {
             ph_begin(s);

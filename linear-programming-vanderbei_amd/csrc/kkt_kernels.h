@@ -68,11 +68,6 @@ void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const doubl
                       hipStream_t s);
 // Block t's update of block column t + 1 alone (W = block t's L21 D).
 void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s);
-// Redo path: diagonal block + rows below of dense-tail block column kb with
-// the dependent-pivot rule, one cooperative launch (k_tail_diag_coop);
-// gmax: one double per 64-row tile, gctr: grid-barrier counter (cleared here).
-// Returns false (nothing launched) when the runtime refuses the cooperative launch.
-bool launch_tail_diag_coop(const PlanView& pv, const TailView& tv, int kb, double* gmax, int* gctr, hipStream_t s);
 // Fused panel of supernodes sups[q0 .. q0+count) that have at most 16
 // columns and 64 rows (one wave each, k_panel_s); same bail-out contract.
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s);

@@ -71,15 +71,6 @@ def _with_env(var, val, fn):
             os.environ[var] = old
 
 
-def test_coop_tail_redo_bitwise():
-    """The redo path's dense tail with dependent pivots: the cooperative
-    k_tail_diag_coop against k_diag + k_trsm (partial substitution per row)
-    on the dfl001 HSD solve, whose redone factorisations hit dependent pivots
-    in the tail -- identical traces."""
-    texts = [_with_env("IPO_HIP_COOP_TAIL", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1] for v in ("0", "1")]
-    assert texts[0] == texts[1]
-
-
 def test_sync_free_sweeps_bitwise():
     """The sync-free top-level sweeps (k_fwd_sf / k_bwd_sf) against the
     per-level launches (IPO_HIP_SF=0): the same arithmetic per supernode, so

@@ -11,8 +11,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out, name, rho = sys.argv[1], sys.argv[2], sys.argv[3]
-variants = {"default": {}, "panel0": {"IPO_HIP_PANEL": "0"}, "repair0": {"IPO_HIP_TAIL_REPAIR": "0"},
-            "coop0": {"IPO_HIP_COOP_TAIL": "0"}}
+variants = {"default": {}, "panel0": {"IPO_HIP_PANEL": "0"}, "repair0": {"IPO_HIP_TAIL_REPAIR": "0"}}
 code = f"""
 import sys, numpy as np
 sys.path[:0] = {[os.path.join(REPO, 'tests'), os.path.join(REPO, 'linear-programming-vanderbei_amd')]!r}
