@@ -329,6 +329,158 @@ k_trsm(PlanView p, int u0, TailView tv, int kb) {
     solve_rows(DiagCtx{p.dscale, p.dg, p.live, p.flags, p.sign, p.tau}, panel, ld, nc, c0, rlo, rhi, wbuf, ldw, wrow0);
 }
 
+// ----------------------------------------- dense tail, dependent pivots
+// Block column kb of the dense tail when the look-ahead panel bailed on a
+// pivot that fails the zero test (the repair path): diagonal block + every
+// row below with the reference's rule (ldlt.c:600-614), in rounds of one
+// launch each.  Workgroup g factors the diagonal block redundantly in LDS
+// (factor_diag_block's operations) and keeps its own 64-row tile of the rows
+// below solved column by column (solve_rows': l = a / d_k on live columns,
+// a -= l (L11 d)), so at a failing pivot k every tile holds column k after
+// the updates of columns < k -- the values the rule's largest off-diagonal
+// magnitude is taken over.  A round runs until such a column whose decision
+// is not known yet: each workgroup publishes its tile's largest magnitude
+// (the diagonal block's rows included) and its rows' state in place,
+// workgroup 0 the block's state, and the round ends; the next round (the
+// kernel boundary orders everything) reloads the state, reduces the
+// published maxima in workgroup order -- every workgroup the same values,
+// the same decision: drop, or +-1e-8 by node class -- and goes on.  No grid
+// barrier, no co-residency assumption: one launch per dependent pivot.
+// State: st = B (PC x PC) | dv | lv | dsc | gmax[G]; sti = k0, 1 + pending
+// column (0: none), done, ndep.
+constexpr int kDepState = PC * PC + 3 * PC;
+
+__global__ void __launch_bounds__(NT)
+k_tail_dep(PlanView p, TailView tv, int kb, double* __restrict__ st, int* __restrict__ sti) {
+    __shared__ double B[PC][PC + 1];
+    __shared__ double dv[PC];
+    __shared__ int lv[PC];
+    __shared__ double dsc[PC];
+    __shared__ double red[4];
+    __shared__ double lk[PC];
+    __shared__ int ndep_sh;
+    const int k0b = kb * PC, nt = tv.nt, ld = nt;
+    const int nc = min(PC, nt - k0b), h = nt - k0b, c0 = tv.tc + k0b;
+    double* panel = tv.S + k0b + (size_t)k0b * nt;
+    const int G = gridDim.x, g = blockIdx.x;
+    const int tid = threadIdx.x, tr = tid & 63, tp = tid >> 6, np = NT >> 6;
+    const int row = nc + g * TR + tr;
+    const bool rok = row < h;
+    const int kstart = sti[0], pending = sti[1] - 1;
+    double* gmax = st + kDepState;
+    if (kstart == 0) {
+        for (int c = tp; c < nc; c += np) B[tr][c] = (tr < nc && tr >= c) ? panel[tr + (size_t)c * ld] : 0.0;
+        for (int k = tid; k < nc; k += NT) { dsc[k] = p.dscale[c0 + k]; dv[k] = 0.0; lv[k] = 1; }
+    } else {
+        for (int c = tp; c < nc; c += np) B[tr][c] = st[tr * PC + c];
+        for (int k = tid; k < nc; k += NT) {
+            dv[k] = st[PC * PC + k];
+            lv[k] = static_cast<int>(st[PC * PC + PC + k]);
+            dsc[k] = st[PC * PC + 2 * PC + k];
+        }
+    }
+    double a[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int c = 4 * q + tp;
+        const bool ok = rok && c < nc;
+        const double t = panel[ok ? row + (size_t)c * ld : 0];
+        a[q] = ok ? t : 0.0;
+    }
+    if (tid == 0) ndep_sh = kstart == 0 ? 0 : sti[3];
+    __syncthreads();
+#pragma unroll
+    for (int qk = 0; qk < 16; qk++) {
+        for (int pk = 0; pk < 4; pk++) {
+            const int k = 4 * qk + pk;
+            if (k >= nc) break;
+            if (k < kstart) continue;
+            double dk = B[k][k];
+            int alive = 1;
+            if (fabs(dk) <= p.tau * dsc[k]) {           // wave-uniform (LDS values)
+                if (pending != k) {
+                    // publish this tile's largest magnitude of column k and the
+                    // state, end the round
+                    double mx = 0.0;
+                    for (int r = k + 1 + tid; r < nc; r += NT) mx = ref_max(mx, ref_abs(B[r][k]));
+                    if (tp == pk && rok) mx = ref_max(mx, ref_abs(a[qk]));
+                    mx = wave_max(mx);
+                    if (tr == 0) red[tp] = mx;
+                    __syncthreads();
+                    if (tid == 0) {
+                        double m2 = red[0];
+                        for (int q = 1; q < np; q++) m2 = ref_max(m2, red[q]);
+                        gmax[g] = m2;
+                    }
+                    if (rok) {
+#pragma unroll
+                        for (int q = 0; q < 16; q++) {
+                            const int c = 4 * q + tp;
+                            if (c < nc) panel[row + (size_t)c * ld] = a[q];
+                        }
+                    }
+                    if (g == 0) {
+                        for (int c = tp; c < nc; c += np) st[tr * PC + c] = B[tr][c];
+                        for (int kk = tid; kk < nc; kk += NT) {
+                            st[PC * PC + kk] = dv[kk];
+                            st[PC * PC + PC + kk] = lv[kk];
+                            st[PC * PC + 2 * PC + kk] = dsc[kk];
+                        }
+                        if (tid == 0) { sti[0] = k; sti[1] = k + 1; sti[3] = ndep_sh; }
+                    }
+                    return;
+                }
+                double mx = gmax[0];
+                for (int q = 1; q < G; q++) mx = ref_max(mx, gmax[q]);
+                if (mx < 1.0e+6 * 1.0e-8) alive = 0;
+                else dk = (p.sign[c0 + k] < 0 ? -1.0 : 1.0) * 1.0e-8;
+                if (tid == 0) ndep_sh++;
+            }
+            if (tid == 0) { dv[k] = dk; lv[k] = alive; }
+            for (int r = k + 1 + tid; r < nc; r += NT) B[r][k] = alive ? B[r][k] / dk : 0.0;
+            if (tp == pk) {
+                const double l = alive ? a[qk] / dk : 0.0;
+                a[qk] = l;
+                lk[tr] = l;
+            }
+            __syncthreads();
+            if (alive && tr > k && tr < nc) {
+                const double lr = B[tr][k];
+                for (int c = k + 1 + tp; c <= tr; c += np) {
+                    const double tk = lr * (B[c][k] * dk);
+                    B[tr][c] -= tk;
+                    if (tr == c) dsc[c] += fabs(tk);
+                }
+            }
+            {
+                const double l = lk[tr];
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    const int c = 4 * q + tp;
+                    const double bk = (k < c && c < nc) ? B[c][k] * dk : 0.0;
+                    a[q] = c > k ? a[q] - l * bk : a[q];
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (rok) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int c = 4 * q + tp;
+            if (c < nc) panel[row + (size_t)c * ld] = a[q];
+        }
+    }
+    if (g != 0) return;
+    for (int r = tp; r < nc; r += np)
+        if (tr < r) panel[tr + (size_t)r * ld] = B[r][tr];
+    for (int k = tid; k < nc; k += NT) { p.dg[c0 + k] = dv[k]; p.live[c0 + k] = lv[k]; }
+    if (tid == 0) {
+        if (ndep_sh) atomicAdd(&p.flags[0], ndep_sh);
+        sti[2] = 1;
+    }
+}
+
 // ------------------------------------------------------------ fused panel
 // Diagonal block and the rows below it in one launch: the fast path of
 // k_diag + k_trsm (k_panel_w below).  A pivot that fails the zero test stops
@@ -546,7 +698,7 @@ struct PanelLds {
 // goes to wtail.
 __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __restrict__ fu_sup,
                                              const int* __restrict__ fu_j, int f0, const TailView& tv, int kb, int bid,
-                                             PanelLds& S, double* wtail, const double* __restrict__ wpre = nullptr) {
+                                             PanelLds& S, double* wtail, bool pre = false) {
     double (*Ct)[CTS] = S.Ct;
     double (*Lr)[PC] = S.Lr;
     double (*Lb)[PC] = S.Lb;
@@ -595,7 +747,7 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
     double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
     double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
-    if (wpre) {
+    if (pre) {
         // dense tail, block column kb > 0: block kb - 1's update of this
         // workgroup's rows, k_tail_syrk's MFMA fragments and order; the
         // entries get old - acc and the pivots' |terms| old + sum_k |l w|,
@@ -614,10 +766,12 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
                 const int k = (tid + u * PNT) / TR;
                 const double x = Lcol[okd ? rd + (size_t)k * nt : 0];
                 const double y = Lcol[okj ? rj + (size_t)k * nt : 0];
-                const double z = wpre[okd ? (rd - kp) + (size_t)k * nt : 0];
+                // W = L21 D of block t - 1 formed here, the product its panel
+                // would have stored (l * d, the same operands: bitwise)
+                const double dk = p.dg[tv.tc + kp + k];
                 vd[u] = okd ? x : 0.0;
                 vj[u] = okj ? y : 0.0;
-                vw[u] = okd ? z : 0.0;
+                vw[u] = okd ? x * dk : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < NU; u++) {
@@ -757,7 +911,7 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
                 if (c < nc) panel[row + (size_t)c * ld] = a[q];
             }
         }
-        if (wpre && j == 0 && !h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc_pre;
+        if (pre && j == 0 && !h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc_pre;
     }
     if (j != 0) return;
     // workgroup 0: L11' into the upper slot through an LDS transpose (Ct is
@@ -793,7 +947,7 @@ struct SyrkLds {
 };
 
 __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& tv, int kb, int bi, int bj,
-                                             const double* __restrict__ W, SyrkLds& L) {
+                                             SyrkLds& L) {
     const int nt = tv.nt, k0 = kb * PC, nc = min(PC, nt - k0), tid = threadIdx.x;
     const double* Lcol = tv.S + (size_t)k0 * nt;
     {
@@ -804,9 +958,10 @@ __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& 
             const int ra = bi * TR + rr, rb = bj * TR + rr;
             const bool oka = k < nc && ra < nt, okb = k < nc && rb < nt;
             const double x = Lcol[oka ? ra + (size_t)k * nt : 0];
-            const double y = W[okb ? (rb - k0) + (size_t)k * nt : 0];
+            const double y = Lcol[okb ? rb + (size_t)k * nt : 0];    // W = L21 D formed here (bitwise its store)
+            const double d = p.dg[tv.tc + k0 + (k < nc ? k : 0)];
             va[u] = oka ? x : 0.0;
-            vb[u] = okb ? y : 0.0;
+            vb[u] = okb ? y * d : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < TR * PC / PNT; u++) {
@@ -860,47 +1015,136 @@ __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& 
     }
 }
 
+constexpr int kVisitBlocks = 4;      // blocks per deferred trailing update of a tile
+
+// Deferred trailing update of the dense tail ("visit"): tile (bi, bj) of S
+// receives the updates of blocks b0 .. b1 - 1 (at most kVisitBlocks) in one
+// pass, S(bi, bj) -= sum_b L(bi, b) W(bj, b)', W = L D formed on the load
+// (no W array: bitwise the product the panel would store), the products summed
+// in the MFMA accumulators (k ascending inside a block, blocks ascending),
+// one read-modify-write of the tile for all of them.  Block b + 1's operands
+// are loaded into registers while block b's are multiplied from LDS.  On a
+// diagonal tile the |terms| of every block go to dscale (one add).
+__device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView& tv, int bi, int bj, int b0, int b1,
+                                              SyrkLds& L) {
+    const int nt = tv.nt, tid = threadIdx.x;
+    constexpr int NU = TR * PC / PNT;
+    double va[NU], vb[NU];
+    auto load = [&](int b) {
+        const int k0 = b * PC, nc = min(PC, nt - k0);
+        const double* __restrict__ Lcol = tv.S + (size_t)k0 * nt;
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int idx = tid + u * PNT, rr = idx % TR, k = idx / TR;
+            const int ra = bi * TR + rr, rb = bj * TR + rr;
+            const bool oka = k < nc && ra < nt, okb = k < nc && rb < nt;
+            const double x = Lcol[oka ? ra + (size_t)k * nt : 0];
+            const double y = Lcol[okb ? rb + (size_t)k * nt : 0];
+            const double d = p.dg[tv.tc + k0 + (k < nc ? k : 0)];
+            va[u] = oka ? x : 0.0;
+            vb[u] = okb ? y * d : 0.0;      // W = L21 D of block b, formed as its panel forms it (bitwise)
+        }
+    };
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int wr = (wv & 1) * 32, wc = (wv >> 1) * 16;
+    const int li = lane & 15, lk = lane >> 4;
+    const bool diag_tile = bi == bj;
+    double4_t acc[2];
+#pragma unroll
+    for (int a = 0; a < 2; a++) acc[a] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    double as = 0.0;
+    load(b0);
+    for (int b = b0; b < b1; b++) {
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int idx = tid + u * PNT;
+            L.As[idx % TR][idx / TR] = va[u];
+            L.Bs[idx % TR][idx / TR] = vb[u];
+        }
+        __syncthreads();
+        if (b + 1 < b1) load(b + 1);
+#pragma unroll
+        for (int kk = 0; kk < PC; kk += 4) {
+            double av[2];
+#pragma unroll
+            for (int a = 0; a < 2; a++) av[a] = L.As[wr + a * 16 + li][kk + lk];
+            const double bv = L.Bs[wc + li][kk + lk];
+#pragma unroll
+            for (int a = 0; a < 2; a++) acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv, acc[a], 0, 0, 0);
+        }
+        if (diag_tile && tid < TR) {
+            const int nc = min(PC, nt - b * PC);
+            for (int k = 0; k < nc; k++) as += fabs(L.As[tid][k] * L.Bs[tid][k]);
+        }
+        __syncthreads();
+    }
+    double old[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int rr = wr + a * 16 + (lane >> 4) + 4 * i, cc = wc + (lane & 15);
+            const int rg = bi * TR + rr, cg = bj * TR + cc;
+            const bool ok = rg < nt && cg < nt && !(diag_tile && cc > rr);
+            old[a][i] = ok ? tv.S[rg + (size_t)cg * nt] : 0.0;
+        }
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int rr = wr + a * 16 + (lane >> 4) + 4 * i, cc = wc + (lane & 15);
+            const int rg = bi * TR + rr, cg = bj * TR + cc;
+            if (rg < nt && cg < nt && !(diag_tile && cc > rr)) tv.S[rg + (size_t)cg * nt] = old[a][i] - acc[a][i];
+        }
+    if (diag_tile && tid < TR && bi * TR + tid < nt) p.dscale[tv.tc + bi * TR + tid] += as;
+}
+
 constexpr size_t kTailStepLds0 = sizeof(PanelLds) > sizeof(SyrkLds) ? sizeof(PanelLds) : sizeof(SyrkLds);
 constexpr size_t kTailStepLds = kTailStepLds0 > sizeof(PreLds) ? kTailStepLds0 : sizeof(PreLds);
 
+// Visits of launch t (tail_visit_cols): block column c receives the updates
+// of blocks 0 .. c - 2 in chunks of kVisitBlocks, the latest chunk in launch
+// c - 1, the one before in launch c - 2, ...: launch c - 1 - k applies blocks
+// [c - 1 - 4 (k + 1), c - 1 - 4 k) (clipped at 0) -- every block available
+// (b < t) and every column done before its panel, block c - 1 being the
+// panel's own pre-update.  Each entry still receives blocks 0, 1, ... in
+// order; the work is spread over the launches (late-as-possible, so the
+// early steps, once 3x the panel's time under the right-looking update, are
+// panel-bound) and a tile is read and written once per chunk, not per block.
+__host__ __device__ __forceinline__ int visit_hi(int t, int c) { return c - 1 - kVisitBlocks * (c - 1 - t); }
+
 // Step t of the look-ahead dense-tail factorisation, one launch:
-//   workgroups [0, gp):  panel of block column t (k_panel_w's body), its
-//                        W = L21 D into Wcur;
-//   the rest:            R(t - 1), the update of block column t - 1 on the
-//                        columns right of t: tiles (bi, bj), bj >= t + 1.
-// Block column t holds every update from blocks <= t - 2 (earlier R
-// launches); the panel workgroups apply block t - 1's to their own rows
-// first (panel_w_body's pre-update, k_tail_syrk's fragments and order) -- so
-// one launch per block column, the big trailing update beside the panel,
-// and every entry still receives the updates of blocks 0, 1, ... in order
-// (bitwise the factor of panel + k_tail_syrk).  W is double-buffered by
-// parity: the pre-update and R read block t - 1's while the panel writes
-// block t's.
+//   workgroups [0, gp):  panel of block column t (k_panel_w's body);
+//   the rest:            the visits of launch t, one tile each, columns
+//                        t + 1, t + 2, ... (visit_hi above).
+// Block column t holds every update from blocks <= t - 2 (earlier visits);
+// the panel workgroups apply block t - 1's to their own rows first
+// (panel_w_body's pre-update, k_tail_syrk's fragments and order).
 __global__ void __launch_bounds__(PNT)
-k_tail_pr(PlanView p, TailView tv, int t, int gp, const double* __restrict__ Wprev, double* __restrict__ Wcur) {
+k_tail_pr(PlanView p, TailView tv, int t, int gp) {
     __shared__ __attribute__((aligned(16))) char lds[kTailStepLds];
     // a panel of an earlier step bailed (flags[2] = 1 + its block column;
-    // not this launch's own, whose trailing tiles must complete): the host
+    // not this launch's own, whose visits must complete): the host
     // resumes the look-ahead from there
     const int bailed = p.flags[2];
     if (bailed && bailed - 1 < t) return;
     if ((int)blockIdx.x < gp) {
-        panel_w_body(p, nullptr, nullptr, 0, tv, t, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), Wcur,
-                     t > 0 ? Wprev : nullptr);
+        panel_w_body(p, nullptr, nullptr, 0, tv, t, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), nullptr, t > 0);
         return;
     }
-    int tile = blockIdx.x - gp, bj = t + 1;
-    while (tile >= tv.ntb - bj) { tile -= tv.ntb - bj; bj++; }
-    syrk_tile512(p, tv, t - 1, bj + tile, bj, Wprev, *reinterpret_cast<SyrkLds*>(lds));
+    int tile = blockIdx.x - gp, c = t + 1;
+    while (tile >= tv.ntb - c) { tile -= tv.ntb - c; c++; }
+    const int b1 = visit_hi(t, c);
+    visit_tile512(p, tv, c + tile, c, max(0, b1 - kVisitBlocks), b1, *reinterpret_cast<SyrkLds*>(lds));
 }
 
 // Block t's update of block column t + 1 only (tiles (bi, t + 1), bi > t):
 // what the look-ahead panel of step t + 1 applies to its own rows, for the
 // repair path that resumes the look-ahead after a dependent pivot.
 __global__ void __launch_bounds__(PNT)
-k_tail_col(PlanView p, TailView tv, int t, const double* __restrict__ W) {
+k_tail_col(PlanView p, TailView tv, int t) {
     __shared__ __attribute__((aligned(16))) char lds[sizeof(SyrkLds)];
-    syrk_tile512(p, tv, t, t + 1 + blockIdx.x, t + 1, W, *reinterpret_cast<SyrkLds*>(lds));
+    syrk_tile512(p, tv, t, t + 1 + blockIdx.x, t + 1, *reinterpret_cast<SyrkLds*>(lds));
 }
 
 // ------------------------------------------------------- small panels
@@ -966,16 +1210,32 @@ k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count) {
 
 }  // namespace
 
-void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const double* Wprev, double* Wcur,
-                      hipStream_t s) {
-    const int h = tv.nt - t * PC;
-    const int gp = std::max(1, (h + TR - 1) / TR - 1);
-    const int nr = t > 0 ? (tv.ntb - t - 1) * (tv.ntb - t) / 2 : 0;
-    hipLaunchKernelGGL(k_tail_pr, dim3(gp + nr), dim3(PNT), 0, s, pv, tv, t, gp, Wprev, Wcur);
+int tail_visit_tiles(int ntb, int t) {
+    int n = 0;
+    for (int c = t + 1; c < ntb && visit_hi(t, c) > 0; c++) n += ntb - c;
+    return t > 0 ? n : 0;
 }
 
-void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s) {
-    if (tv.ntb - t - 1 > 0) hipLaunchKernelGGL(k_tail_col, dim3(tv.ntb - t - 1), dim3(PNT), 0, s, pv, tv, t, W);
+void launch_tail_step(const PlanView& pv, const TailView& tv, int t, hipStream_t s) {
+    const int h = tv.nt - t * PC;
+    const int gp = std::max(1, (h + TR - 1) / TR - 1);
+    const int nr = tail_visit_tiles(tv.ntb, t);
+    hipLaunchKernelGGL(k_tail_pr, dim3(gp + nr), dim3(PNT), 0, s, pv, tv, t, gp);
+}
+
+void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, hipStream_t s) {
+    if (tv.ntb - t - 1 > 0) hipLaunchKernelGGL(k_tail_col, dim3(tv.ntb - t - 1), dim3(PNT), 0, s, pv, tv, t);
+}
+
+int tail_dep_tiles(const TailView& tv, int kb) {
+    const int below = tv.nt - kb * PC - std::min(PC, tv.nt - kb * PC);
+    return std::max(1, (below + TR - 1) / TR);
+}
+
+size_t tail_dep_state_doubles(int ntb) { return kDepState + static_cast<size_t>(std::max(1, ntb)); }
+
+void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, double* st, int* sti, hipStream_t s) {
+    hipLaunchKernelGGL(k_tail_dep, dim3(tail_dep_tiles(tv, kb)), dim3(NT), 0, s, pv, tv, kb, st, sti);
 }
 
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s) {

@@ -44,6 +44,7 @@ struct KktTimers {
     long panel_redos = 0;     // factorisations redone without the fused panel kernels
     long redo_where[4] = {0, 0, 0, 0};   // ... by the kernel that bailed (k_panel, k_panel_w sparse / tail, k_panel_s)
     long tail_repairs = 0;    // dense-tail block columns redone in place (look-ahead resumed after them)
+    long tail_dep_rounds = 0; // k_tail_dep launches of those repairs
 };
 
 class KktDevice {
@@ -195,7 +196,7 @@ class KktDevice {
     std::vector<int> small_ptr_;          // per level: small panels [small_ptr_[l], small_ptr_[l+1]) (k_panel_s)
     DevBuf<int> dsmall_sups_;
     bool use_panel_ = true;               // fused diagonal-block + panel kernels (IPO_HIP_PANEL=0: off)
-    bool factor_pass(const double* dE, const double* dD, bool fused);
+    bool factor_pass(const double* dE, const double* dD, bool fused, bool tail_fused);
     bool finish_pass(bool fused);
     void repair_tail();
     std::vector<int> chunk_ptr_;          // per level: solve chunks [chunk_ptr_[l], chunk_ptr_[l+1])
@@ -210,11 +211,13 @@ class KktDevice {
     DevBuf<double> dPartialTile_;
     DevBuf<TaskSrc> dusrc_, dtsrc_;   // per gather task: source panel descriptor
     DevBuf<SlotRec> dslot_rec_, dtail_slot_rec_;   // per gather k-slot record (sparse units, dense tail)
-    DevBuf<int> dChainFlags_;    // dense-tail sweep chains: per block, epoch of the last completed sweep
-    int chain_epoch_ = 0;      // forward-sweep update values, one per row of every R_s
+    DevBuf<unsigned long long> dChainGran_;   // dense-tail sweep chains: z of every block as epoch-tagged granules
+    int chain_epoch_ = 0;      // the chains' launch epoch (one per launch, never reused)
     DevBuf<int> dtail_task_ptr_, dkslot_, dkslot_ptr_, dtail_kslot_, dtail_kslot_ptr_;
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;
+    DevBuf<double> dDepSt_;        // k_tail_dep's block state and per-tile maxima
+    DevBuf<int> dDepI_;            // its round counters
     // numeric
     DevBuf<double> dLx_, dDg_;
     DevBuf<int> dLive_;

@@ -1136,15 +1136,14 @@ k_tail_bwd(PlanView p, TailView tv, int kb, double* __restrict__ z, const double
 
 // ------------------------------------------- dense-tail sweeps, one launch
 // Sync-free block-row chains: workgroup i owns 64-row block i of the tail
-// and waits, block by block, for the blocks it depends on (flags[j] ==
-// epoch).  Hand-off per MI355X_MICROARCH.md (inter-workgroup visibility,
-// table row 1): the producer stores its block with sc1 stores (relaxed
-// agent-scope atomics), waits vmcnt(0), joins a barrier, and one lane
-// stores the flag sc1; the consumer polls the flag with sc1 loads from one
-// lane, joins a barrier and reads the block with sc1 loads.  One
-// workgroup per CU is enforced with dynamic LDS.  Every workgroup only
-// waits on blocks of lower rank in its own launch order, so the grid
-// drains as long as it is resident (ntb <= kChainMaxBlocks).
+// and waits, block by block, for the blocks it depends on.  Each block's z
+// is handed on as epoch-tagged granules (gran_put / gran_wait above,
+// MI355X_MICROARCH.md hand-off table row R2: the data is the flag -- one
+// store round trip on the producer, one load round trip on the consumer;
+// round 2's sc1 payload + drained flag took two of each).  One workgroup
+// per CU is enforced with dynamic LDS.  Every workgroup only waits on blocks
+// of lower rank in its own launch order, so the grid drains as long as it
+// is resident (ntb <= kChainMaxBlocks).
 constexpr int kChainMaxBlocks = 200;
 constexpr size_t kChainLds = 96 * 1024;
 static_assert(2 * PC * (PC + 1) * sizeof(double) <= kChainLds, "k_tail_bwd_chain scratch");
@@ -1164,11 +1163,50 @@ __device__ __forceinline__ void chain_publish(int* flags, int i, int epoch) {
     if (threadIdx.x == 0) __hip_atomic_store(flags + i, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Data-tagged hand-off of a block's z (MI355X_MICROARCH.md hand-off table,
+// row R2): every double travels as two naturally aligned 8-byte granules
+// {tag = epoch, 32-bit half}, each written by ONE relaxed agent-scope
+// (sc1) store -- no flag, no drain, no barrier on the producer; the consumer
+// re-reads its granules until every tag is the launch's epoch and has the
+// data with the match.  Epochs grow by one per launch and are never reused
+// (the buffer starts zeroed, the first epoch is 1), so no reset per launch.
+// Block j, right-hand side r, row q: granules ((j R + r) 64 + q) 2 + {0, 1}.
+typedef unsigned long long gran_t;
+__device__ __forceinline__ void gran_put(gran_t* g, unsigned epoch, double v) {
+    const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(v));
+    const unsigned long long e = static_cast<unsigned long long>(epoch) << 32;
+    __hip_atomic_store(g, e | (b & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + 1, e | (b >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one wave: lane q < nr waits for row q of block j's R values
+template <int R>
+__device__ __forceinline__ void gran_wait(const gran_t* g, unsigned epoch, int lane, int nr, double (&v)[R]) {
+    for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (lane < nr) {
+                const gran_t* q = g + ((size_t)r * 64 + lane) * 2;
+                const unsigned long long lo = __hip_atomic_load(const_cast<gran_t*>(q), __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long hi = __hip_atomic_load(const_cast<gran_t*>(q + 1), __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT);
+                ok &= (lo >> 32) == epoch && (hi >> 32) == epoch;
+                v[r] = __longlong_as_double(static_cast<long long>(((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull)));
+            } else {
+                v[r] = 0.0;
+            }
+        }
+        if (__all(ok)) return;
+        __builtin_amdgcn_s_sleep(IPO_POLL_SLEEP);
+    }
+}
+
 // forward: z_i -= sum_{j<i} L(i, j) z_j, then the unit-lower L11 solve of block i
 template <int R>
 __global__ void __launch_bounds__(NT)
-k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, int* __restrict__ flags,
-                 int epoch) {
+k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, gran_t* __restrict__ gran,
+                 unsigned epoch) {
     extern __shared__ double lds_pad[];
     __shared__ double Ls[PC][PC + 1];
     __shared__ int lv[PC];
@@ -1194,10 +1232,11 @@ k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
         double t[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) t[q] = col[(size_t)q * nt];
-        chain_wait(flags, j, epoch);
-        if (tid < PC) {
+        if (wv == 0) {
+            double zj[R];
+            gran_wait<R>(gran + (size_t)j * R * 128, epoch, lane, PC, zj);
 #pragma unroll
-            for (int r = 0; r < R; r++) zb[r][tid] = sc1_load(V.z + r * V.zs + tc + j * PC + tid);
+            for (int r = 0; r < R; r++) zb[r][lane] = zj[r];
         }
         __syncthreads();
 #pragma unroll
@@ -1220,11 +1259,13 @@ k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
         tri_lower<R>(zr, Ls, lv, nc, eps, bad);
         if (lane < nc) {
 #pragma unroll
-            for (int r = 0; r < R; r++) sc1_store(V.z + r * V.zs + tc + k0 + lane, zr[r]);
+            for (int r = 0; r < R; r++) {
+                gran_put(gran + (((size_t)i * R + r) * 64 + lane) * 2, epoch, zr[r]);
+                V.z[r * V.zs + tc + k0 + lane] = zr[r];
+            }
         }
         flag_bad<R>(p, bad);
     }
-    chain_publish(flags, i, epoch);
 }
 
 // backward (launch order = blocks from the last): z_i = D^{-1} z_i
@@ -1232,8 +1273,8 @@ k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
 // block i, lanes stride the rows of block j (coalesced column reads).
 template <int R>
 __global__ void __launch_bounds__(NT)
-k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, int* __restrict__ flags,
-                 int epoch) {
+k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, gran_t* __restrict__ gran,
+                 unsigned epoch) {
     extern __shared__ double lds_pad[];
     __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L(j, r)
     __shared__ int lv[PC];
@@ -1266,10 +1307,11 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
         double t[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, max(nq, 1) - 1) * nt];
-        chain_wait(flags, j, epoch);
-        if (tid < PC) {
+        if (wv == 0) {
+            double zj[R];
+            gran_wait<R>(gran + (size_t)j * R * 128, epoch, lane, nr, zj);
 #pragma unroll
-            for (int r = 0; r < R; r++) zb[r][tid] = tid < nr ? sc1_load(V.z + r * V.zs + tc + r0 + tid) : 0.0;
+            for (int r = 0; r < R; r++) zb[r][lane] = zj[r];
         }
         __syncthreads();
 #pragma unroll
@@ -1292,11 +1334,13 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
         tri_upper<R>(zr, Ls, lv, nc, eps, bad);
         if (lane < nc) {
 #pragma unroll
-            for (int r = 0; r < R; r++) sc1_store(V.z + r * V.zs + tc + k0 + lane, zr[r]);
+            for (int r = 0; r < R; r++) {
+                gran_put(gran + (((size_t)i * R + r) * 64 + lane) * 2, epoch, zr[r]);
+                V.z[r * V.zs + tc + k0 + lane] = zr[r];
+            }
         }
         flag_bad<R>(p, bad);
     }
-    chain_publish(flags, i, epoch);
 }
 
 // ------------------------------------------- sync-free sweeps, top levels
@@ -2038,9 +2082,11 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dtail_kslot_ptr_.upload(plan_.tail_kslot_ptr, s);
         static_assert(sizeof(TailTask) == 32, "TailTask layout");
         dtail_tasks_.upload(reinterpret_cast<const uint64_t*>(plan_.tail_tasks.data()), plan_.tail_tasks.size() * 4, s);
-        dW_.alloc(2 * static_cast<size_t>(plan_.nt) * kPanelCols);   // two block columns (look-ahead tail)
-        dChainFlags_.alloc(plan_.ntb);
-        IPO_HIP_CHECK(hipMemsetAsync(dChainFlags_.get(), 0, plan_.ntb * sizeof(int), s));
+        dW_.alloc(static_cast<size_t>(plan_.nt) * kPanelCols);   // W = L21 D of one block column (per-phase path)
+        dDepSt_.alloc(tail_dep_state_doubles(plan_.ntb));
+        dDepI_.alloc(4);
+        dChainGran_.alloc(static_cast<size_t>(plan_.ntb) * 2 * 128);     // R <= 2 right-hand sides
+        IPO_HIP_CHECK(hipMemsetAsync(dChainGran_.get(), 0, dChainGran_.bytes(), s));
         if (plan_.ntb <= kChainMaxBlocks) {
             for (const void* f : {reinterpret_cast<const void*>(&k_tail_fwd_chain<1>),
                                   reinterpret_cast<const void*>(&k_tail_fwd_chain<2>),
@@ -2208,8 +2254,9 @@ KktDevice::~KktDevice() {
 #endif
     if (std::getenv("IPO_HIP_DEBUG_REDO"))
         std::fprintf(stderr, "kkt: %ld factorisations, %ld redone; bails (unused) %ld, k_panel_w sparse %ld, tail %ld, "
-                             "k_panel_s %ld; tail block columns repaired %ld\n", tm_.factors, tm_.panel_redos,
-                     tm_.redo_where[0], tm_.redo_where[1], tm_.redo_where[2], tm_.redo_where[3], tm_.tail_repairs);
+                             "k_panel_s %ld; tail block columns repaired %ld in %ld rounds\n", tm_.factors,
+                     tm_.panel_redos, tm_.redo_where[0], tm_.redo_where[1], tm_.redo_where[2], tm_.redo_where[3],
+                     tm_.tail_repairs, tm_.tail_dep_rounds);
     if (hScal_) (void)hipHostFree(hScal_);
     if (hFlags_) (void)hipHostFree(hFlags_);
     if (ev0_) (void)hipEventDestroy(ev0_);
@@ -2303,26 +2350,31 @@ void KktDevice::factor(const double* dE, const double* dD) {
 
 void KktDevice::factor_core(const double* dE, const double* dD) {
     // fast path: fused diagonal-block + panel kernels; a pivot that fails
-    // the zero test makes them stop unwritten, and the factorisation is
-    // redone with the per-phase kernels, which own the dependent-pivot rule
-    if (!factor_pass(dE, dD, use_panel_)) {
+    // the zero test makes them stop unwritten.  A bail in the dense tail
+    // only: the look-ahead resumes from the bailed block column (repair);
+    // in the sparse levels: the factorisation is redone with the per-phase
+    // kernels there, which own the dependent-pivot rule, and the tail again
+    // by the look-ahead (its own bails repaired the same way) -- a per-phase
+    // tail costs a single-workgroup partial substitution per block column
+    const char* rp = std::getenv("IPO_HIP_TAIL_REPAIR");
+    const bool repair = use_panel_ && !xch_ && (!rp || std::atoi(rp) != 0);
+    if (!factor_pass(dE, dD, use_panel_, use_panel_)) {
         tm_.panel_redos++;
         for (int b = 0; b < 4; b++) tm_.redo_where[b] += (hFlags_[1] >> b) & 1;
-        // only a look-ahead dense-tail panel bailed: everything before its
-        // block column stands, resume from there; else redo it all
-        const char* rp = std::getenv("IPO_HIP_TAIL_REPAIR");
-        const bool repair = !rp || std::atoi(rp) != 0;
-        if (repair && !xch_ && hFlags_[1] == 4 && hFlags_[4] > 0) repair_tail();
-        else factor_pass(dE, dD, false);
+        const bool tail_only = hFlags_[1] == 4 && hFlags_[4] > 0;
+        if (repair && tail_only) repair_tail();
+        else if (!factor_pass(dE, dD, false, repair) && repair && hFlags_[1] == 4 && hFlags_[4] > 0) repair_tail();
     }
     tm_.factors++;
     ndep_ = xch_ ? static_cast<int>(hScal_[1]) : hFlags_[0];
     if (-hScal_[0] < 1.0e-14) epsdiag_ *= 10;
 }
 
-// One numeric factorisation; returns false when fused kernels bailed out
-// (nothing of the result may then be used).
-bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
+// One numeric factorisation, the sparse levels by the fused kernels (fused)
+// or the per-phase ones, the dense tail by the look-ahead (tail_fused) or
+// the per-phase kernels; returns false when fused kernels bailed out
+// (flags[1] says where; nothing of a bailed part may then be used).
+bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool tail_fused) {
     hipStream_t s = stream_;
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev0_, s));
     const PlanView pv = IPO_VIEW();
@@ -2363,12 +2415,10 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
         // shards: S = sum of every shard's assembled + gathered tail (exchange.h)
         xsum(tv.S, static_cast<size_t>(plan_.nt) * plan_.nt, RedOp::Sum);
         xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
-        if (fused) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
-            const size_t wst = static_cast<size_t>(plan_.nt) * kPanelCols;
+        if (tail_fused) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
             for (int t = 0; t < plan_.ntb; t++) {
-                double* wc = dW_.get() + (t & 1) * wst;
                 ph_begin(s);
-                launch_tail_step(pv, tv, t, dW_.get() + ((t + 1) & 1) * wst, wc, s);
+                launch_tail_step(pv, tv, t, s);
                 ph_end(kPhDiag, 1, s);
             }
         } else
@@ -2376,10 +2426,7 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
             const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
             const int below = plan_.nt - k0 - nc;
             ph_begin(s);
-            if (fused) {
-                launch_panel(pv, nullptr, nullptr, 0, 0, tv, kb, s);
-                ph_end(kPhDiag, 1, s);
-            } else {
+            {
                 launch_diag(pv, nullptr, 0, 1, tv, kb, s);
                 ph_end(kPhDiag, 1, s);
                 if (below > 0) {
@@ -2396,7 +2443,7 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused) {
             }
         }
     }
-    return finish_pass(fused);
+    return finish_pass(fused || tail_fused);
 }
 
 // min |d| over the factor (ldlt.c:293-306), the dependent-pivot count and
@@ -2435,20 +2482,17 @@ bool KktDevice::finish_pass(bool fused) {
 }
 
 // The look-ahead dense tail bailed at block column tb (a pivot failed the
-// zero test; steps after it did nothing): the sparse factor and block
+// zero test; launches after it did nothing): the sparse factor and block
 // columns < tb stand, column tb holds the updates of blocks <= tb - 2 (its
-// panel stores S only once it holds) and the columns right of it those of
-// blocks <= tb - 1.  Apply block tb - 1 to column tb, factor column tb with
-// the dependent-pivot kernels (its W into the look-ahead's buffer of that
-// parity), and resume the look-ahead at tb + 1 -- per entry the operations
-// of the full redo, which would take the same path (no pivot before tb
-// fails the test), so bitwise its factor.  Repeats while a later column
-// bails.
+// panel stores S only once it holds) and every column right of it what its
+// visits up to launch tb gave it.  Apply block tb - 1 to column tb, factor
+// column tb with the dependent-pivot rounds (k_tail_dep), and resume
+// the look-ahead at tb + 1 with the same visit schedule: the fast path's
+// operations with block column tb's panel replaced by k_diag + k_trsm.
+// Repeats while a later column bails.
 void KktDevice::repair_tail() {
     hipStream_t s = stream_;
     const PlanView pv = IPO_VIEW();
-    const size_t wst = static_cast<size_t>(plan_.nt) * kPanelCols;
-    auto wbuf = [&](int t) { return dW_.get() + (t & 1) * wst; };
     for (;;) {
         const int tb = hFlags_[4] - 1;
         tm_.tail_repairs++;
@@ -2456,17 +2500,23 @@ void KktDevice::repair_tail() {
         IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get() + 1, 0, 2 * sizeof(int), s));
         TailView tv = tail_view();
         ph_begin(s);
-        if (tb > 0) launch_tail_colupdate(pv, tv, tb - 1, wbuf(tb - 1), s);
+        if (tb > 0) launch_tail_colupdate(pv, tv, tb - 1, s);
         ph_end(kPhSyrk, tb > 0, s);
-        tv.W = wbuf(tb);
-        const int k0 = tb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0), below = plan_.nt - k0 - nc;
-        ph_begin(s);
-        launch_diag(pv, nullptr, 0, 1, tv, tb, s);
-        if (below > 0) launch_trsm(pv, 0, -1, tv, tb, s);
-        ph_end(kPhDiag, 1, s);
+        // block column tb with the dependent-pivot rule, one round per dependent pivot
+        IPO_HIP_CHECK(hipMemsetAsync(dDepI_.get(), 0, 4 * sizeof(int), s));
+        for (int r = 0;; r++) {
+            if (r > kPanelCols + 1) throw std::runtime_error("kkt: dense-tail dependent-pivot rounds did not finish");
+            ph_begin(s);
+            launch_tail_dep_round(pv, tv, tb, dDepSt_.get(), dDepI_.get(), s);
+            ph_end(kPhDiag, 1, s);
+            IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 6, dDepI_.get() + 2, sizeof(int), hipMemcpyDeviceToHost, s));
+            IPO_HIP_CHECK(hipStreamSynchronize(s));
+            tm_.tail_dep_rounds++;
+            if (hFlags_[6]) break;
+        }
         for (int t = tb + 1; t < plan_.ntb; t++) {
             ph_begin(s);
-            launch_tail_step(pv, tail_view(), t, wbuf(t + 1), wbuf(t), s);
+            launch_tail_step(pv, tail_view(), t, s);
             ph_end(kPhDiag, 1, s);
         }
         if (finish_pass(true)) break;
@@ -2556,14 +2606,14 @@ void KktDevice::sweep(double* dz, const double* epsp) {
                            dyrow_idx_.get(), V);
         tail_rhs_end(dz, R);
         hipLaunchKernelGGL(k_tail_fwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
-                           dChainFlags_.get(), ++chain_epoch_);
+                           dChainGran_.get(), ++chain_epoch_);
     }
     ph_end(kPhForward, fwd_launches_, s);
     ph_begin(s);
     if (plan_.nt > 0) {
         const TailView tv = tail_view();
         hipLaunchKernelGGL(k_tail_bwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
-                           dChainFlags_.get(), ++chain_epoch_);
+                           dChainGran_.get(), ++chain_epoch_);
     }
     if (sf_level_ < plan_.nlevels) {
         const SfView sf{dsf_items_b_.get(), nsf_b_, dsf_bcnt_.get(), dsf_bflag_.get(), dsf_need_.get(), dsf_par_.get(),

@@ -62,12 +62,19 @@ void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0
                   int kb, hipStream_t s);
 // Look-ahead dense tail (fused path with k_panel_w): step t = panel of block
 // column t (which first applies block t - 1's update to its own rows) beside
-// the trailing update of block t - 1 on columns > t -- one launch per block
-// column, W of block t into Wcur, block t - 1's read from Wprev.
-void launch_tail_step(const PlanView& pv, const TailView& tv, int t, const double* Wprev, double* Wcur,
-                      hipStream_t s);
-// Block t's update of block column t + 1 alone (W = block t's L21 D).
-void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, const double* W, hipStream_t s);
+// the deferred trailing updates ("visits") scheduled for launch t -- one
+// launch per block column.  W = L21 D is formed from L and D where used.
+void launch_tail_step(const PlanView& pv, const TailView& tv, int t, hipStream_t s);
+// visit tiles of launch t (tail of ntb block columns)
+int tail_visit_tiles(int ntb, int t);
+// Repair path, block column kb of the dense tail with the dependent-pivot
+// rule: one round (k_tail_dep); sti = {k0, 1 + pending column, done, ndep},
+// zeroed before the first round; rounds until sti[2] (one per dependent
+// pivot).  st: tail_dep_state_doubles(ntb).
+void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, double* st, int* sti, hipStream_t s);
+size_t tail_dep_state_doubles(int ntb);
+// Block t's update of block column t + 1 alone.
+void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, hipStream_t s);
 // Fused panel of supernodes sups[q0 .. q0+count) that have at most 16
 // columns and 64 rows (one wave each, k_panel_s); same bail-out contract.
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s);

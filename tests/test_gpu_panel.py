@@ -1,9 +1,12 @@
 """The fused panel kernels against the per-phase ones: k_diag + k_trsm +
 k_tail_syrk (IPO_HIP_PANEL=0, the dependent-pivot path) and the fused
 k_panel_s / k_panel_w / look-ahead tail (default) apply the same operations
-in the same order to every entry of the factor (the reference's l = a / d,
-a -= l (l_j d) form, kkt_dense.hip), so the refined solves and whole IPM
-traces they produce must be bitwise identical."""
+to every entry of the sparse factor in the same order (the reference's
+l = a / d, a -= l (l_j d) form, kkt_dense.hip).  On the dense tail the fused
+path defers the trailing update and sums up to four blocks' products in one
+accumulator before subtracting them (visits, kkt_dense.hip), so there the two
+agree to rounding: refined solves to 1e-10 relative, whole IPM solves to the
+HSD parity bar (tests/test_gpu_ipm.py)."""
 import os
 
 import numpy as np
@@ -30,7 +33,7 @@ def _with_panel(kind, fn):
 
 
 @pytest.mark.parametrize("name", ["afiro", "25fv47", "pds-02", "d6cube", "dfl001"])
-def test_panel_kinds_solve_bitwise(name):
+def test_panel_kinds_solve(name):
     p = ipo_amd.load_mps(mps_path(name))
     rng = np.random.default_rng(7)
     E = rng.uniform(0.1, 10.0, p.m)
@@ -48,15 +51,17 @@ def test_panel_kinds_solve_bitwise(name):
     outs = [_with_panel(kind, run) for kind in KINDS]
     for gy, gx, ok in outs[1:]:
         assert ok == outs[0][2]
-        assert np.array_equal(gy, outs[0][0]) and np.array_equal(gx, outs[0][1])
+        scale = 1.0 + max(np.abs(outs[0][0]).max(), np.abs(outs[0][1]).max())
+        assert np.abs(gy - outs[0][0]).max() <= 1e-10 * scale and np.abs(gx - outs[0][1]).max() <= 1e-10 * scale
 
 
 @pytest.mark.parametrize("name", ["dfl001"])
-def test_panel_kinds_hsd_trace_bitwise(name):
-    """Whole HSD solves (dfl001: 117 iterations, dense tail of 44 block
-    columns, dependent-pivot redos): identical printed traces."""
-    texts = [_with_panel(kind, lambda: ipo_amd.run_mps(mps_path(name), "hsd"))[1] for kind in KINDS]
-    assert texts[0] == texts[1]
+def test_panel_kinds_hsd_trace(name):
+    """Whole HSD solves (dfl001: 117 iterations, dense tail of 70 block
+    columns, dependent-pivot redos) on either path: the golden parity bar."""
+    from test_gpu_ipm import check_hsd
+    for kind in KINDS:
+        check_hsd(name, _with_panel(kind, lambda: ipo_amd.run_mps(mps_path(name), "hsd"))[1])
 
 
 def _with_env(var, val, fn):
@@ -79,14 +84,15 @@ def test_sync_free_sweeps_bitwise():
     assert texts[0] == texts[1]
 
 
-def test_tail_repair_bitwise():
+def test_tail_repair():
     """A dependent pivot in the look-ahead dense tail: resuming the look-ahead
-    after redoing only the bailed block column (default) against redoing the
+    after redoing only the bailed block column (default) and redoing the
     whole factorisation with the per-phase kernels (IPO_HIP_TAIL_REPAIR=0) --
-    the dfl001 HSD solve meets such pivots in three factorisations; identical
-    traces."""
-    texts = [_with_env("IPO_HIP_TAIL_REPAIR", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1] for v in ("0", "1")]
-    assert texts[0] == texts[1]
+    the dfl001 HSD solve meets such pivots in a few factorisations; both
+    solves meet the golden parity bar."""
+    from test_gpu_ipm import check_hsd
+    for v in ("0", "1"):
+        check_hsd("dfl001", _with_env("IPO_HIP_TAIL_REPAIR", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1])
 
 
 def _solve_env(var, val):
