@@ -1216,6 +1216,23 @@ int tail_visit_tiles(int ntb, int t) {
     return t > 0 ? n : 0;
 }
 
+void tail_visit_work(int ntb, int nt, double& flops, double& bytes) {
+    flops = bytes = 0.0;
+    for (int t = 1; t < ntb; t++)
+        for (int c = t + 1; c < ntb && visit_hi(t, c) > 0; c++) {
+            const int b1 = visit_hi(t, c), b0 = std::max(0, b1 - kVisitBlocks);
+            for (int bi = c; bi < ntb; bi++) {
+                const double rows = std::min(TR, nt - bi * TR), cols = std::min(TR, nt - c * TR);
+                for (int b = b0; b < b1; b++) {
+                    const double k = std::min(PC, nt - b * PC);
+                    flops += 2.0 * rows * cols * k;
+                    bytes += 8.0 * k * (rows + cols);          // L rows of bi and of c (W = L D formed on load)
+                }
+                bytes += 16.0 * rows * cols;                   // one read-modify-write of the tile
+            }
+        }
+}
+
 void launch_tail_step(const PlanView& pv, const TailView& tv, int t, hipStream_t s) {
     const int h = tv.nt - t * PC;
     const int gp = std::max(1, (h + TR - 1) / TR - 1);

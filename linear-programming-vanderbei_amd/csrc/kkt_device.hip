@@ -2015,7 +2015,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             df += 2.0 * nc * nc * nc / 3.0;
             db += 8.0 * 1.5 * nc * nc;
             tf += below * nc * nc;
-            tb += 24.0 * below * nc;                                // L21 read + write, W write
+            tb += 16.0 * below * nc;                                // L21 read + write
             const double nb = P.ntb - kb - 1;
             sf += 2.0 * nc * (nb * (nb + 1) / 2) * kTileRows * kTileRows;
             sb += (nb * (nb + 1) / 2) * (16.0 * kTileRows * kTileRows + 16.0 * kTileRows * nc);
@@ -2024,11 +2024,15 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         work_flops[kPhGather] = gf; work_bytes[kPhGather] = gb;
         work_flops[kPhDiag] = df; work_bytes[kPhDiag] = db;
         work_flops[kPhTrsm] = tf; work_bytes[kPhTrsm] = tb;
-        if (use_panel_) {   // k_panel_w does both: the diag phase carries the trsm work
-            work_flops[kPhDiag] += tf; work_bytes[kPhDiag] += tb;
-            work_flops[kPhTrsm] = work_bytes[kPhTrsm] = 0;
-        }
         work_flops[kPhSyrk] = sf; work_bytes[kPhSyrk] = sb;
+        if (use_panel_) {   // k_panel_w does both: the diag phase carries the trsm work,
+            // and k_tail_pr the tail's trailing update (its visits)
+            double vf = 0, vb = 0;
+            if (P.ntb > 0) tail_visit_work(P.ntb, P.nt, vf, vb);
+            work_flops[kPhDiag] += tf + vf; work_bytes[kPhDiag] += tb + vb;
+            work_flops[kPhTrsm] = work_bytes[kPhTrsm] = 0;
+            work_flops[kPhSyrk] = work_bytes[kPhSyrk] = 0;
+        }
         // a sweep reads every factor entry once (sparse panels + the tail's
         // lower triangle) and the vector / update values it touches
         const double tail_tri = 0.5 * P.nt * (P.nt + 1.0);

@@ -67,6 +67,8 @@ void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0
 void launch_tail_step(const PlanView& pv, const TailView& tv, int t, hipStream_t s);
 // visit tiles of launch t (tail of ntb block columns)
 int tail_visit_tiles(int ntb, int t);
+// algorithmic flops / bytes of every visit of one factorisation
+void tail_visit_work(int ntb, int nt, double& flops, double& bytes);
 // Repair path, block column kb of the dense tail with the dependent-pivot
 // rule: one round (k_tail_dep); sti = {k0, 1 + pending column, done, ndep},
 // zeroed before the first round; rounds until sti[2] (one per dependent

@@ -90,27 +90,31 @@ with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:
                          "(dfl001 hsd, first 10 iterations); FETCH_SIZE doubled (gfx950)",
                "phases": phases, "kernels": kern}, fh, indent=1)
 # f64 MFMA utilisation per kernel / phase: SQ_VALU_MFMA_BUSY_CYCLES (MFMA-busy
-# cycles summed over the SIMDs) over GRBM_GUI_ACTIVE x SIMDs (1,024 on
-# MI355X: 256 CUs x 4); f64 MFMA flops from SQ_INSTS_VALU_MFMA_MOPS_F64
-# (units of 512 flops) over the kernel's trace duration
+# cycles summed over the SIMDs: 64 per v_mfma_f64_16x16x4f64, calibrated on
+# k_tail_pr whose instruction count is known) over the kernel's active
+# cycles x SIMDs (1,024 on MI355X: 256 CUs x 4), the active cycles being
+# GRBM_GUI_ACTIVE / 8 -- the counter sums the 8 XCDs (GRBM_GUI_ACTIVE / 8 at
+# ~2.4-2.8 GHz is the kernel's trace duration); f64 MFMA flops from
+# SQ_INSTS_VALU_MFMA_MOPS_F64 (units of 512 flops: 431 MFLOP per k_tail_pr
+# launch = the algorithmic count) over the kernel's trace duration (us)
 mdb = os.path.join(src, f"{tag}_pmc_mfma", "run_results.db")
 if os.path.exists(mdb):
-    SIMDS = 1024
+    SIMDS, XCDS = 1024, 8
     busy = per_kernel(mdb, "SQ_VALU_MFMA_BUSY_CYCLES")
     mops = per_kernel(mdb, "SQ_INSTS_VALU_MFMA_MOPS_F64")
     gui = per_kernel(mdb, "GRBM_GUI_ACTIVE")
     sqb = per_kernel(mdb, "SQ_BUSY_CYCLES")
-    dur = {short(n): avg for n, _, _, avg, _ in rows}     # ns per launch, kernel-trace run
+    dur = {short(n): avg for n, _, _, avg, _ in rows}     # us per launch, kernel-trace run
     mk = {}
     for k in busy:
         b, n = busy[k]
         g = gui.get(k, (0.0, 1))[0]
         mo = mops.get(k, (0.0, 1))[0]
         mk[k] = {"launches": n, "mfma_busy_cycles": b / n, "gui_active_cycles": g / n,
-                 "mfma_util": b / (g * SIMDS) if g else None, "f64_mfma_flops_per_launch": 512.0 * mo / n,
+                 "mfma_util": b / (g / XCDS * SIMDS) if g else None, "f64_mfma_flops_per_launch": 512.0 * mo / n,
                  "sq_busy_cycles": sqb.get(k, (0.0, 1))[0] / n}
         if k in dur and dur[k]:
-            mk[k]["f64_mfma_tflops"] = mk[k]["f64_mfma_flops_per_launch"] / (dur[k] * 1e-9) / 1e12
+            mk[k]["f64_mfma_tflops"] = mk[k]["f64_mfma_flops_per_launch"] / (dur[k] * 1e-6) / 1e12
     mph = {}
     for ph, names in PHASE_KERNELS.items():
         want = set(re.split(r"[|+]", names))
@@ -120,12 +124,13 @@ if os.path.exists(mdb):
         f = sum(mk[k]["f64_mfma_flops_per_launch"] * mk[k]["launches"] for k in ks)
         nl = sum(mk[k]["launches"] for k in ks)
         if nl:
-            mph[ph] = {"kernels": ks, "launches": nl, "mfma_util": b / (g * SIMDS) if g else None,
+            mph[ph] = {"kernels": ks, "launches": nl, "mfma_util": b / (g / XCDS * SIMDS) if g else None,
                        "f64_mfma_flops_per_launch": f / nl}
     with open(os.path.join(dst, f"{tag}_pmc_mfma.json"), "w") as fh:
         json.dump({"source": "rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES "
                              "GRBM_GUI_ACTIVE, bench.py --steps 1 --warmup 0 --no-timing (dfl001 hsd); util = "
-                             "MFMA-busy cycles / (GRBM_GUI_ACTIVE x 1024 SIMDs); MOPS_F64 in units of 512 flops",
+                             "MFMA-busy cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); MOPS_F64 in units of 512 "
+                             "flops; tflops over the kernel-trace average duration",
                    "phases": mph, "kernels": mk}, fh, indent=1)
 line = [ln for ln in open(os.path.join(src, f"{tag}_bench.log")) if ln.startswith("{")][-1]
 with open(os.path.join(dst, f"{tag}_bench.json"), "w") as fh:
