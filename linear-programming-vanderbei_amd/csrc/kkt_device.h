@@ -203,6 +203,7 @@ class KktDevice {
     DevBuf<int> dchunk_sup_, dchunk_r0_, dsup_chunk0_;
     DevBuf<double> dPartial_;    // backward partial sums, one 64-vector per chunk
     // split-K gather chunks per group (sparse level l, group nlevels = tail)
+    std::vector<bool> ck_wide_;      // per gather group: k_update<4> (few chunks, units split >= 4 ways)
     std::vector<int> ck_ptr_, sp_ptr_;
     DevBuf<int> dck_u_, dck_b_, dck_e_, dck_part_, dsp_u_, dsp_p0_, dsp_n_;
     DevBuf<int> dck_q_;          // split-unit index of each chunk (-1: unsplit)

@@ -273,6 +273,7 @@ __device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], 
 // Sum the np partial tiles of a split unit (slots p0.., thread-fragment
 // order) in chunk order: acc = ((0 + P_0) + P_1) + ...  The partials were
 // handed off inside this launch (sc1 loads, bypassing the CU's L1).
+template <int SG>
 __device__ __forceinline__ void split_sum(const double* __restrict__ partial, int p0, int np, double4_t (&acc)[2][2],
                                           double& dabs) {
     const int tid = threadIdx.x;
@@ -281,19 +282,28 @@ __device__ __forceinline__ void split_sum(const double* __restrict__ partial, in
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
     dabs = 0.0;
-    for (int j = 0; j < np; j++) {
-        const double* src = partial + (size_t)(p0 + j) * (TR * TR + 4 * TR);
-        double v[17];
+    // SG partials' loads in flight at once (each a dependent round trip
+    // otherwise: 12 partials took 12 of them), added in chunk order
+    for (int j0 = 0; j0 < np; j0 += SG) {
+        double v[SG][17];
 #pragma unroll
-        for (int e = 0; e < 16; e++) v[e] = sc1_load(src + e * NT + tid);
-        v[16] = sc1_load(src + TR * TR + tid);
+        for (int g = 0; g < SG; g++) {
+            const double* src = partial + (size_t)(p0 + min(j0 + g, np - 1)) * (TR * TR + 4 * TR);
 #pragma unroll
-        for (int a = 0; a < 2; a++)
+            for (int e = 0; e < 16; e++) v[g][e] = sc1_load(src + e * NT + tid);
+            v[g][16] = sc1_load(src + TR * TR + tid);
+        }
 #pragma unroll
-            for (int b = 0; b < 2; b++)
+        for (int g = 0; g < SG; g++) {
+            if (j0 + g >= np) break;
 #pragma unroll
-                for (int i = 0; i < 4; i++) acc[a][b][i] += v[(a * 2 + b) * 4 + i];
-        dabs += v[16];
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) acc[a][b][i] += v[g][(a * 2 + b) * 4 + i];
+            dabs += v[g][16];
+        }
     }
 }
 
@@ -306,6 +316,7 @@ __device__ __forceinline__ void split_sum(const double* __restrict__ partial, in
 // (MI355X_MICROARCH.md hand-off table row 1: last arriver told by its own
 // add's return value).  It resets the counter for the next factorisation.
 // tail >= 0: units are dense-tail tiles.
+template <int SG>
 __global__ void __launch_bounds__(NT)
 k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
          const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
@@ -346,7 +357,7 @@ k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
     }
     __syncthreads();
     if (!last) return;
-    split_sum(partial, sp_p0[q], np, acc, dabs);
+    split_sum<SG>(partial, sp_p0[q], np, acc, dabs);
     gather_store(g, acc, dabs, has_diag, dcol);
 }
 
@@ -1932,8 +1943,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         ck_ptr_.assign(plan_.nlevels + 2, 0);
         sp_ptr_.assign(plan_.nlevels + 2, 0);
         size_t max_part = 0;
-        const int wg_target = 512, min_chunk = 64;
+        const int wg_target = 512, min_chunk = 64;     // 64: measured best of 16-256 on configs[3] and dfl001
         auto group = [&](int u0, int u1, const std::vector<int>& kptr) {
+            const long nck0 = static_cast<long>(cu.size());
             long sumk = 0;
             for (int u = u0; u < u1; u++) sumk += kptr[u + 1] - kptr[u];
             // aim at >= wg_target workgroups per launch, chunks of min_chunk..512 slots
@@ -1954,13 +1966,25 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
                 }
             }
             max_part = std::max<size_t>(max_part, np);
+            // a group of few chunks (about one per CU: occupancy does not
+            // matter) whose units are split many ways waits on its partial
+            // sums: sum them several at a time
+            int mx = 0;
+            for (int u = u0; u < u1; u++) {
+                const long k = kptr[u + 1] - kptr[u];
+                mx = std::max<int>(mx, static_cast<int>((k + kmax - 1) / kmax));
+            }
+            ck_wide_.push_back(mx >= 4 && static_cast<long>(cu.size()) - nck0 <= 512);
         };
+        ck_wide_.clear();
         for (int l = 0; l < plan_.nlevels; l++) {
             if (l > 0) group(plan_.unit_level_ptr[l], plan_.unit_level_ptr[l + 1], plan_.kslot_ptr);
+            else ck_wide_.push_back(false);
             ck_ptr_[l + 1] = static_cast<int>(cu.size());
             sp_ptr_[l + 1] = static_cast<int>(su.size());
         }
         if (plan_.nt > 0) group(0, plan_.ntb * (plan_.ntb + 1) / 2, plan_.tail_kslot_ptr);
+        else ck_wide_.push_back(false);
         ck_ptr_[plan_.nlevels + 1] = static_cast<int>(cu.size());
         sp_ptr_[plan_.nlevels + 1] = static_cast<int>(su.size());
         dck_u_.upload(cu, s);
@@ -2535,7 +2559,15 @@ int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, i
     const int c0 = ck_ptr_[group], c1 = ck_ptr_[group + 1];
     if (c1 <= c0) return 0;
     const SlotRec* recs = tail < 0 ? dslot_rec_.get() : dtail_slot_rec_.get();
-    hipLaunchKernelGGL(k_update, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
+    // groups whose split units have many chunks sum their partials four
+    // at a time (more registers: three waves per SIMD drop to two, which
+    // the gathers of the other groups would pay for)
+    if (ck_wide_[group])
+    hipLaunchKernelGGL(k_update<4>, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
+                       dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(), dsp_n_.get(),
+                       dSplitCnt_.get());
+    else
+    hipLaunchKernelGGL(k_update<1>, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
                        dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(), dsp_n_.get(),
                        dSplitCnt_.get());
     return 1;
