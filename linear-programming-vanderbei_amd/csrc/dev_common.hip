@@ -73,6 +73,35 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
         if (tid == 0) out[j] = acc;
         return;
     }
+    if (len >= kOrderedMaxLen) {
+        // very long vectors (synthetic LPs of 10^6 columns; no netlib problem
+        // comes near): one sequential chain of len adds took 4.3 ms.  Fixed
+        // strided order instead: thread t sums i = t, t + 256, ... in index
+        // order (eight loads in flight), the 256 partials are added in thread
+        // order -- deterministic, not the reference's rounding
+        __shared__ double part[kOrdThreads];
+        double acc = 0.0;
+        for (int i0 = 0; i0 < len; i0 += 8 * kOrdThreads) {
+            double pa[8], pb[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int i = i0 + u * kOrdThreads + tid;
+                pa[u] = i < len ? a[i] : 0.0;
+                pb[u] = i < len ? b[i] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (i0 + u * kOrdThreads + tid < len) acc += pa[u] * pb[u];
+        }
+        part[tid] = acc;
+        __syncthreads();
+        if (tid == 0) {
+            double s = 0.0;
+            for (int t = 0; t < kOrdThreads; t++) s += part[t];
+            out[j] = s;
+        }
+        return;
+    }
     constexpr int CH = 8192;
     __shared__ __attribute__((aligned(16))) double prod[CH + 16];   // + one batch of read-ahead
     double s = 0.0e0;

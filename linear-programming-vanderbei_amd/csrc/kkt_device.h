@@ -200,10 +200,13 @@ class KktDevice {
     bool finish_pass(bool fused);
     void repair_tail();
     std::vector<int> chunk_ptr_;          // per level: solve chunks [chunk_ptr_[l], chunk_ptr_[l+1])
+    std::vector<int> leaf_cnt_;           // per level: leading single-column supernodes of dsweep_sups_
+    DevBuf<int> dsweep_sups_;             // level_sups in sweep order (leaves first on unchunked levels)
     DevBuf<int> dchunk_sup_, dchunk_r0_, dsup_chunk0_;
     DevBuf<double> dPartial_;    // backward partial sums, one 64-vector per chunk
     // split-K gather chunks per group (sparse level l, group nlevels = tail)
-    std::vector<bool> ck_wide_;      // per gather group: k_update<4> (few chunks, units split >= 4 ways)
+    bool visits_ = false;        // deep trees: early gather slots as visits in lower levels' launches
+    std::vector<bool> ck_wide_, ck_flat_;   // ck_flat_: k_update_flat (latency-bound launches of deep trees)      // per gather group: k_update<4> (few chunks, units split >= 4 ways)
     std::vector<int> ck_ptr_, sp_ptr_;
     DevBuf<int> dck_u_, dck_b_, dck_e_, dck_part_, dsp_u_, dsp_p0_, dsp_n_;
     DevBuf<int> dck_q_;          // split-unit index of each chunk (-1: unsplit)
@@ -214,7 +217,7 @@ class KktDevice {
     DevBuf<SlotRec> dslot_rec_, dtail_slot_rec_;   // per gather k-slot record (sparse units, dense tail)
     DevBuf<unsigned long long> dChainGran_;   // dense-tail sweep chains: z of every block as epoch-tagged granules
     int chain_epoch_ = 0;      // the chains' launch epoch (one per launch, never reused)
-    DevBuf<int> dtail_task_ptr_, dkslot_, dkslot_ptr_, dtail_kslot_, dtail_kslot_ptr_;
+    DevBuf<int> dtail_task_ptr_, dtail_kslot_, dtail_kslot_ptr_;
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;
     DevBuf<double> dDepSt_;        // k_tail_dep's block state and per-tile maxima

@@ -232,15 +232,12 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
     }
 }
 
-// out -= acc on the tile's lower part; dscale += the four waves' dabs in order
-__device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], double dabs, bool has_diag,
-                             int dcol) {
-    __shared__ double dred[4][TR];
+// The tile's current values (read before the first store: the compiler
+// cannot tell that the 16 entries are distinct and would otherwise
+// serialise 16 round trips)
+__device__ __forceinline__ void gather_old(const GatherTile& g, double (&old)[2][2][4]) {
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
-    // every load before the first store: the compiler cannot tell that the
-    // 16 entries are distinct and would otherwise serialise 16 round trips
-    double old[2][2][4];
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -252,6 +249,14 @@ __device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], 
                 const bool ok = rr < g.nrow && cc < g.ncol && g.row0 + rr >= g.col0 + cc;
                 old[a][b][i] = ok ? g.out[rr + (size_t)cc * g.ld] : 0.0;
             }
+}
+
+// out = old - acc on the tile's lower part; dscale += the four waves' dabs in order
+__device__ void gather_put(const GatherTile& g, const double (&old)[2][2][4], const double4_t (&acc)[2][2], double dabs,
+                           bool has_diag, int dcol) {
+    __shared__ double dred[4][TR];
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -268,6 +273,13 @@ __device__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], 
         __syncthreads();
         if (wv == 0 && has_diag) g.dscale_col[dcol] += ((dred[0][lane] + dred[1][lane]) + dred[2][lane]) + dred[3][lane];
     }
+}
+
+__device__ __forceinline__ void gather_store(const GatherTile& g, const double4_t (&acc)[2][2], double dabs, bool has_diag,
+                                             int dcol) {
+    double old[2][2][4];
+    gather_old(g, old);
+    gather_put(g, old, acc, dabs, has_diag, dcol);
 }
 
 // Sum the np partial tiles of a split unit (slots p0.., thread-fragment
@@ -336,6 +348,127 @@ k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
         gather_store(g, acc, dabs, has_diag, dcol);
         return;
     }
+    double* dst = partial + (size_t)pi * (TR * TR + 4 * TR);
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) sc1_store(dst + ((a * 2 + b) * 4 + i) * NT + tid, acc[a][b][i]);
+    sc1_store(dst + TR * TR + tid, dabs);
+    __shared__ int last;
+    const int q = ck_q[c];
+    const int np = sp_n[q];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const int prev = __hip_atomic_fetch_add(split_cnt + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == np - 1;
+        if (prev == np - 1) __hip_atomic_store(split_cnt + q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    split_sum<SG>(partial, sp_p0[q], np, acc, dabs);
+    gather_store(g, acc, dabs, has_diag, dcol);
+}
+
+// Flat gather for latency-bound launches (the level chain of deep trees,
+// where a launch holds one small gather per unit and nothing hides the
+// pipelined form's memory round trip per 16-slot slab -- 2.5 us each,
+// measured): up to 64 slots per round, their records staged in LDS by one
+// coalesced load, then every value of the round issued at once (32 loads
+// in flight per lane), one barrier, the MFMA steps.  Slot k of a round is
+// staged by the wave gather_acc gives it (k mod 16 in [4 wv, 4 wv + 4)) and
+// the MFMA steps and |terms| run in gather_acc's order: bitwise the same.
+constexpr int FK = 64;
+__device__ void gather_acc_flat(const PlanView& p, const SlotRec* __restrict__ recs, int kb, int ke, int dcol,
+                                bool has_diag, double4_t (&acc)[2][2], double& dabs) {
+    __shared__ double As[TR][FK + 1];
+    __shared__ double Bs[TR][FK + 1];
+    __shared__ SlotRec rl[FK];
+    const int tid = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
+    const int li = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    dabs = 0.0;
+    for (int k0 = kb; k0 < ke; k0 += FK) {
+        const int nk = min(FK, ke - k0), nsl = nk / KS;
+        if (tid < nk * 4)
+            reinterpret_cast<uint64_t*>(rl)[tid] = reinterpret_cast<const uint64_t*>(recs + k0)[tid];
+        __syncthreads();
+        double ra[FK / 16 * 4], rb[FK / 16 * 4];
+#pragma unroll
+        for (int sb = 0; sb < FK / KS; sb++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                ra[sb * 4 + j] = 0.0;
+                rb[sb * 4 + j] = 0.0;
+                if (sb < nsl) slot_vals(rl[sb * KS + wv * 4 + j], p.Lx, p.dg, lane, ra[sb * 4 + j], rb[sb * 4 + j]);
+            }
+#pragma unroll
+        for (int sb = 0; sb < FK / KS; sb++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (sb < nsl) {
+                    As[lane][sb * KS + wv * 4 + j] = ra[sb * 4 + j];
+                    Bs[lane][sb * KS + wv * 4 + j] = rb[sb * 4 + j];
+                }
+        __syncthreads();
+        for (int kk = 0; kk < nk; kk += 4) {
+            double av[2], bv[2];
+#pragma unroll
+            for (int a = 0; a < 2; a++) av[a] = As[wr + a * 16 + li][kk + lk];
+#pragma unroll
+            for (int b = 0; b < 2; b++) bv[b] = Bs[wc + b * 16 + li][kk + lk];
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 2; b++)
+                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+        }
+        if (has_diag) {
+            for (int sb = 0; sb < nsl; sb++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int k = sb * KS + wv * 4 + j;
+                    dabs += fabs(As[lane][k] * Bs[dcol][k]);
+                }
+        }
+        __syncthreads();
+    }
+}
+
+// k_update with the flat gather; an unsplit chunk reads its tile's old
+// values before the gather (no workgroup writes a tile its launch reads:
+// one chunk per unsplit unit, split units stored by their last chunk only)
+template <int SG>
+__global__ void __launch_bounds__(NT)
+k_update_flat(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
+              const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
+              const int* __restrict__ ck_part, int c0, double* __restrict__ partial,
+              const int* __restrict__ ck_q, const int* __restrict__ sp_p0, const int* __restrict__ sp_n,
+              int* __restrict__ split_cnt) {
+    const int c = c0 + blockIdx.x;
+    const int u = ck_u[c], kb = ck_b[c], ke = ck_e[c], pi = ck_part[c];
+    const GatherTile g = unit_tile(p, tv, u, tail);
+    const int lane = threadIdx.x & 63;
+    const int dcol = g.row0 + lane - g.col0;
+    const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
+    double4_t acc[2][2];
+    double dabs;
+    if (pi < 0) {
+        double old[2][2][4];
+        gather_old(g, old);
+        gather_acc_flat(p, recs, kb, ke, dcol, has_diag, acc, dabs);
+        gather_put(g, old, acc, dabs, has_diag, dcol);
+        return;
+    }
+    gather_acc_flat(p, recs, kb, ke, dcol, has_diag, acc, dabs);
     double* dst = partial + (size_t)pi * (TR * TR + 4 * TR);
     const int tid = threadIdx.x;
 #pragma unroll
@@ -818,6 +951,99 @@ k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __r
 #pragma unroll
         for (int r = 0; r < R; r++) V.y[r * V.ys + p.ybase[s] + i] = acc[r];
     }
+}
+
+// Single-column supernodes with at most 64 rows below (the bulk of the
+// bottom level: one per x-node of a large LP, 10^6 on configs[3]), one wave
+// each, four per workgroup -- k_forward / k_backward spend a 256-thread
+// workgroup, an L11 staging and two barriers on each.  The same operations
+// in the same order as those kernels' nc = 1 case (the update list summed
+// by 64 parts, part q taking entries q, q + 64, ... in list order, the
+// parts combined by the xor butterfly; the backward products summed by
+// wave_sum), so bitwise the same sweep.
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_fwd_leaf(PlanView p, const int* __restrict__ sups, int q0, int cnt, const int* __restrict__ yrow_ptr,
+           const int* __restrict__ yrow_idx, SweepVecs V, const double* __restrict__ epsp) {
+    const int w = blockIdx.x * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w >= cnt) return;
+    const int s = sups[q0 + w];
+    const int c0 = p.col0[s], hb = p.rowptr[s + 1] - p.rowptr[s];
+    double pr[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) pr[r] = 0.0;
+    for (int e = yrow_ptr[c0] + lane; e < yrow_ptr[c0 + 1]; e += 64) {
+        const int ix = yrow_idx[e];
+#pragma unroll
+        for (int r = 0; r < R; r++) pr[r] += V.y[r * V.ys + ix];
+    }
+    double z[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        for (int o = 1; o < 64; o <<= 1) {
+            const double ot = __shfl_xor(pr[r], o, 64);
+            pr[r] = (lane & o) ? ot + pr[r] : pr[r] + ot;
+        }
+        z[r] = __shfl(V.z[r * V.zs + c0] - pr[r], 0, 64);
+    }
+    if (!p.live[c0]) {          // dropped column (ldlt.c:446-470)
+        double eps[R];
+        load_eps<R>(epsp, eps);
+        int bad[R] = {};
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (fabs(z[r]) > eps[r]) bad[r] = 1;
+            else z[r] = 0.0;
+        }
+        if (lane == 0) flag_bad<R>(p, bad);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int r = 0; r < R; r++) V.z[r * V.zs + c0] = z[r];
+    }
+    if (lane < hb) {
+        const double l = p.Lx[p.off[s] + 1 + lane];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            double acc = 0.0;
+            acc += l * z[r];
+            V.y[r * V.ys + p.ybase[s] + lane] = acc;
+        }
+    }
+}
+
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_bwd_leaf(PlanView p, const int* __restrict__ sups, int q0, int cnt, SweepVecs V, const double* __restrict__ epsp) {
+    const int w = blockIdx.x * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w >= cnt) return;
+    const int s = sups[q0 + w];
+    const int c0 = p.col0[s], hb = p.rowptr[s + 1] - p.rowptr[s];
+    double acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = 0.0;
+    if (lane < hb) {
+        const int ri = p.rows[p.rowptr[s] + lane];
+        const double t = p.Lx[p.off[s] + 1 + lane];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] += t * V.z[r * V.zs + ri];
+    }
+    double eps[R];
+    load_eps<R>(epsp, eps);
+    int bad[R] = {};
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const double xs = wave_sum(acc[r]);
+        if (lane == 0) {
+            double zr = dscale_rule(p, c0, V.z[r * V.zs + c0], eps[r], bad[r]) - xs;
+            if (!p.live[c0]) {
+                if (fabs(zr) > eps[r]) bad[r] = 1;
+                else zr = 0.0;
+            }
+            V.z[r * V.zs + c0] = zr;
+        }
+    }
+    if (lane == 0) flag_bad<R>(p, bad);
 }
 
 // Forward for levels with large panels, part 1: diagonal parts only.
@@ -1934,28 +2160,113 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         IPO_HIP_CHECK(hipStreamSynchronize(s));   // csup / cr0 / chunk0 are stack vectors
         h_chunk0_ = chunk0;
     }
+    {   // sweep order of each level: on levels without solve chunks the
+        // single-column supernodes with <= 64 rows below come first (one wave
+        // each, k_fwd_leaf / k_bwd_leaf), the rest after them
+        std::vector<int> ss(plan_.level_sups);
+        leaf_cnt_.assign(plan_.nlevels, 0);
+        for (int l = 0; l < plan_.nlevels; l++) {
+            if (chunk_ptr_[l + 1] > chunk_ptr_[l]) continue;
+            const auto b = ss.begin() + plan_.level_ptr[l], e = ss.begin() + plan_.level_ptr[l + 1];
+            const auto mid = std::stable_partition(b, e, [&](int sp) {
+                return plan_.col0[sp + 1] - plan_.col0[sp] == 1 && plan_.rowptr[sp + 1] - plan_.rowptr[sp] <= 64;
+            });
+            leaf_cnt_[l] = static_cast<int>(mid - b);
+        }
+        dsweep_sups_.upload(ss, s);
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+    }
     dyrow_ptr_.upload(plan_.yrow_ptr, s);
     build_sync_free_plan();
-    dkslot_.upload(plan_.kslot, s);
-    dkslot_ptr_.upload(plan_.kslot_ptr, s);
+    // Deep elimination trees (at least kVisitLevels levels, e.g. the banded
+    // BASELINE configs[3]: 2,785 levels, most of them one or two 64-column
+    // supernodes): a level's gather would wait on every descendant's update,
+    // although 93 % of its k-slots come from supernodes finished several
+    // levels earlier.  There each unit's slots are ordered by the level of
+    // their source (stable), and only the slabs that hold a source of the
+    // level just below ("late") stay in the unit's own level's gather; the
+    // earlier slabs become visits of at most kVisitSlots slots, scheduled as
+    // late as their sources allow into the gather launches of the levels
+    // below (one visit per unit per launch, each a read-modify-write of the
+    // unit's tile in slot order).  The level chain then waits per level on
+    // one small gather and the panel, the visits ride in the same launches
+    // beside them.  IPO_HIP_VISITS=1/0 forces the schedule on / off.
+    std::vector<int> kslot_v;
     {   // gather chunks (split K): groups = sparse levels, then the dense tail
+        const int nu = static_cast<int>(plan_.unit_sup.size());
+        const char* ve = std::getenv("IPO_HIP_VISITS");
+        visits_ = ve ? std::atoi(ve) != 0 : plan_.nlevels >= kVisitLevels;
+        // flat gathers (k_update_flat) for the latency-bound launches of
+        // deep trees: IPO_HIP_GATHER_FLAT=0 never, 1 (default) deep trees,
+        // 2 every launch of at most kFlatMaxChunks chunks
+        int flat_mode = 1;
+        if (const char* e = std::getenv("IPO_HIP_GATHER_FLAT")) flat_mode = std::atoi(e);
+        int visit_slabs = kVisitSlots / kSlab;
+        if (const char* e = std::getenv("IPO_HIP_VISIT_SLOTS")) visit_slabs = std::max(1, std::atoi(e) / kSlab);
+        std::vector<int> kptr_v, late_b;
+        std::vector<std::vector<int3>> vis(plan_.nlevels + 1);   // per group: (unit, slot begin, slot end)
+        if (visits_) {
+            kptr_v.assign(nu + 1, 0);
+            late_b.assign(nu, 0);
+            std::vector<std::pair<int, int>> sl;   // (source level, slot)
+            std::vector<int> rl;
+            for (int l = 1; l < plan_.nlevels; l++)
+                for (int u = plan_.unit_level_ptr[l]; u < plan_.unit_level_ptr[l + 1]; u++) {
+                    sl.clear();
+                    for (int i = plan_.kslot_ptr[u]; i < plan_.kslot_ptr[u + 1]; i++) {
+                        const int k = plan_.kslot[i];
+                        if (k >= 0) sl.push_back({plan_.level[plan_.utasks[k >> 6].src], k});
+                    }
+                    std::stable_sort(sl.begin(), sl.end(),
+                                     [](const std::pair<int, int>& a, const std::pair<int, int>& b) { return a.first < b.first; });
+                    const int kb = static_cast<int>(kslot_v.size());
+                    rl.clear();
+                    for (size_t i = 0; i < sl.size(); i++) {
+                        kslot_v.push_back(sl[i].second);
+                        if (i % kSlab == 0) rl.push_back(sl[i].first);
+                        else rl.back() = std::max(rl.back(), sl[i].first);
+                    }
+                    while (kslot_v.size() % kSlab) kslot_v.push_back(-1);
+                    kptr_v[u + 1] = static_cast<int>(kslot_v.size());
+                    const int nsl = static_cast<int>(rl.size());
+                    int j = nsl;
+                    while (j > 0 && rl[j - 1] >= l - 1) j--;
+                    late_b[u] = kb + kSlab * j;
+                    // early slabs [0, j), backwards, as late as their sources allow
+                    int t = l - 1, end = j, cur = j;
+                    while (cur > 0) {
+                        if (end - cur >= visit_slabs && rl[cur - 1] <= t - 2) {
+                            vis[t].push_back(make_int3(u, kb + kSlab * cur, kb + kSlab * end));
+                            t--;
+                            end = cur;
+                        }
+                        cur--;
+                    }
+                    if (end > 0) vis[t].push_back(make_int3(u, kb, kb + kSlab * end));
+                }
+            // groups visit their units in unit order
+            for (auto& g : vis)
+                std::sort(g.begin(), g.end(), [](const int3& a, const int3& b) { return a.x < b.x; });
+        }
         std::vector<int> cu, cb, ce, cp, cq, su, sp0, sn;
         ck_ptr_.assign(plan_.nlevels + 2, 0);
         sp_ptr_.assign(plan_.nlevels + 2, 0);
         size_t max_part = 0;
         const int wg_target = 512, min_chunk = 64;     // 64: measured best of 16-256 on configs[3] and dfl001
-        auto group = [&](int u0, int u1, const std::vector<int>& kptr) {
+        // units [u0, u1), slots [kbeg(u), kend(u)) each, then the group's visits
+        auto group = [&](int u0, int u1, auto kbeg, auto kend, const std::vector<int3>* visits) {
             const long nck0 = static_cast<long>(cu.size());
             long sumk = 0;
-            for (int u = u0; u < u1; u++) sumk += kptr[u + 1] - kptr[u];
+            for (int u = u0; u < u1; u++) sumk += kend(u) - kbeg(u);
             // aim at >= wg_target workgroups per launch, chunks of min_chunk..512 slots
             long kmax = (sumk / wg_target + kSlab - 1) / kSlab * kSlab;
             kmax = std::max<long>(min_chunk, std::min<long>(kMaxChunkSlots, kmax));
-            int np = 0;
+            int np = 0, mx = 0;
             for (int u = u0; u < u1; u++) {
-                const int kb = kptr[u], ke = kptr[u + 1];
+                const int kb = kbeg(u), ke = kend(u);
                 if (ke == kb) continue;
                 const int nch = static_cast<int>((ke - kb + kmax - 1) / kmax);
+                mx = std::max(mx, nch);
                 if (nch > 1) { su.push_back(u); sp0.push_back(np); sn.push_back(nch); }
                 for (int j = 0; j < nch; j++) {
                     cu.push_back(u);
@@ -1965,26 +2276,37 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
                     cq.push_back(nch > 1 ? static_cast<int>(su.size()) - 1 : -1);
                 }
             }
+            if (visits)
+                for (const int3& v : *visits) {
+                    cu.push_back(v.x); cb.push_back(v.y); ce.push_back(v.z); cp.push_back(-1); cq.push_back(-1);
+                }
             max_part = std::max<size_t>(max_part, np);
             // a group of few chunks (about one per CU: occupancy does not
             // matter) whose units are split many ways waits on its partial
             // sums: sum them several at a time
-            int mx = 0;
-            for (int u = u0; u < u1; u++) {
-                const long k = kptr[u + 1] - kptr[u];
-                mx = std::max<int>(mx, static_cast<int>((k + kmax - 1) / kmax));
-            }
             ck_wide_.push_back(mx >= 4 && static_cast<long>(cu.size()) - nck0 <= 512);
+            ck_flat_.push_back(flat_mode == 2 || (flat_mode == 1 && visits_)
+                               ? static_cast<long>(cu.size()) - nck0 <= kFlatMaxChunks : false);
         };
+        const std::vector<int>& kp = plan_.kslot_ptr;
         ck_wide_.clear();
+        ck_flat_.clear();
         for (int l = 0; l < plan_.nlevels; l++) {
-            if (l > 0) group(plan_.unit_level_ptr[l], plan_.unit_level_ptr[l + 1], plan_.kslot_ptr);
-            else ck_wide_.push_back(false);
+            if (l == 0) { ck_wide_.push_back(false); ck_flat_.push_back(false); }
+            else if (visits_)
+                group(plan_.unit_level_ptr[l], plan_.unit_level_ptr[l + 1], [&](int u) { return late_b[u]; },
+                      [&](int u) { return kptr_v[u + 1]; }, &vis[l]);
+            else
+                group(plan_.unit_level_ptr[l], plan_.unit_level_ptr[l + 1], [&](int u) { return kp[u]; },
+                      [&](int u) { return kp[u + 1]; }, nullptr);
             ck_ptr_[l + 1] = static_cast<int>(cu.size());
             sp_ptr_[l + 1] = static_cast<int>(su.size());
         }
-        if (plan_.nt > 0) group(0, plan_.ntb * (plan_.ntb + 1) / 2, plan_.tail_kslot_ptr);
-        else ck_wide_.push_back(false);
+        const std::vector<int>& tp = plan_.tail_kslot_ptr;
+        if (plan_.nt > 0)
+            group(0, plan_.ntb * (plan_.ntb + 1) / 2, [&](int u) { return tp[u]; }, [&](int u) { return tp[u + 1]; },
+                  nullptr);
+        else { ck_wide_.push_back(false); ck_flat_.push_back(false); }
         ck_ptr_[plan_.nlevels + 1] = static_cast<int>(cu.size());
         sp_ptr_[plan_.nlevels + 1] = static_cast<int>(su.size());
         dck_u_.upload(cu, s);
@@ -2003,7 +2325,8 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     {   // launches per sweep and algorithmic work per phase occurrence
         fwd_launches_ = bwd_launches_ = sf_level_ < plan_.nlevels ? 1 : 0;
         for (int l = 0; l < sf_level_; l++) {
-            const int k = chunk_ptr_[l + 1] > chunk_ptr_[l] ? 2 : 1;
+            const int nsl = plan_.level_ptr[l + 1] - plan_.level_ptr[l];
+            const int k = chunk_ptr_[l + 1] > chunk_ptr_[l] ? 2 : (leaf_cnt_[l] > 0) + (nsl > leaf_cnt_[l]);
             fwd_launches_ += k;
             bwd_launches_ += k;
         }
@@ -2100,7 +2423,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             dst.upload(v, s);
             IPO_HIP_CHECK(hipStreamSynchronize(s));
         };
-        expand(plan_.kslot, plan_.utasks, dslot_rec_);
+        expand(visits_ ? kslot_v : plan_.kslot, plan_.utasks, dslot_rec_);
         if (plan_.nt > 0) expand(plan_.tail_kslot, plan_.tail_tasks, dtail_slot_rec_);
     }
     dutasks_.upload(reinterpret_cast<const uint64_t*>(plan_.utasks.data()), plan_.utasks.size() * 4, s);
@@ -2562,6 +2885,17 @@ int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, i
     // groups whose split units have many chunks sum their partials four
     // at a time (more registers: three waves per SIMD drop to two, which
     // the gathers of the other groups would pay for)
+    if (ck_flat_[group]) {
+        if (ck_wide_[group])
+        hipLaunchKernelGGL(k_update_flat<4>, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(),
+                           dck_b_.get(), dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(),
+                           dsp_p0_.get(), dsp_n_.get(), dSplitCnt_.get());
+        else
+        hipLaunchKernelGGL(k_update_flat<1>, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(),
+                           dck_b_.get(), dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(),
+                           dsp_p0_.get(), dsp_n_.get(), dSplitCnt_.get());
+        return 1;
+    }
     if (ck_wide_[group])
     hipLaunchKernelGGL(k_update<4>, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
                        dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(), dsp_n_.get(),
@@ -2624,8 +2958,13 @@ void KktDevice::sweep(double* dz, const double* epsp) {
             hipLaunchKernelGGL(k_fwd_gemv<R>, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(), cb,
                                V);
         } else {
-            hipLaunchKernelGGL(k_forward<R>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
-                               dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+            const int nl = leaf_cnt_[l];
+            if (nl > 0)
+                hipLaunchKernelGGL(k_fwd_leaf<R>, dim3(ceil_div(nl, NT / 64)), dim3(NT), 0, s, pv, dsweep_sups_.get(),
+                                   q0, nl, dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+            if (q1 - q0 > nl)
+                hipLaunchKernelGGL(k_forward<R>, dim3(q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(), q0 + nl,
+                                   dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
         }
     }
     if (sf_level_ < plan_.nlevels) {      // the narrow top levels in one launch
@@ -2667,7 +3006,13 @@ void KktDevice::sweep(double* dz, const double* epsp) {
             hipLaunchKernelGGL(k_bwd_finish<R>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
                                dsup_chunk0_.get(), dPartial_.get(), ps, V, epsp);
         } else {
-            hipLaunchKernelGGL(k_backward<R>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0, V, epsp);
+            const int nl = leaf_cnt_[l];
+            if (nl > 0)
+                hipLaunchKernelGGL(k_bwd_leaf<R>, dim3(ceil_div(nl, NT / 64)), dim3(NT), 0, s, pv, dsweep_sups_.get(),
+                                   q0, nl, V, epsp);
+            if (q1 - q0 > nl)
+                hipLaunchKernelGGL(k_backward<R>, dim3(q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(), q0 + nl,
+                                   V, epsp);
         }
     }
     ph_end(kPhBackward, bwd_launches_, s);
