@@ -809,7 +809,8 @@ __device__ long long g_sfst[1 << 15][10];
 template <int R, bool SC = false, bool STAGED = false>
 __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
                          const SweepVecs& V, const double (&eps)[R], double (*zl)[PC], double (*Ls)[PC + 1], int* lv,
-                         const int* sidx = nullptr, int stamp_it = -1, const int* sptr = nullptr) {
+                         const int* sidx = nullptr, int stamp_it = -1, const int* sptr = nullptr,
+                         double* zout = nullptr, size_t zos = 0) {
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -912,8 +913,14 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
         for (int r = 0; r < R; r++) zr[r] = lane < nc ? zl[r][lane] : 0.0;
         tri_lower<R>(zr, Ls, lv, nc, eps, bad);
         if (lane < nc) {
+            // zout: z_s goes to a mirror instead (the chunk items of one
+            // supernode each solve it and must all read its right-hand side)
 #pragma unroll
-            for (int r = 0; r < R; r++) { V.z[r * V.zs + c0 + lane] = zr[r]; zl[r][lane] = zr[r]; }
+            for (int r = 0; r < R; r++) {
+                if (zout) sc1_store(zout + r * zos + lane, zr[r]);
+                else V.z[r * V.zs + c0 + lane] = zr[r];
+                zl[r][lane] = zr[r];
+            }
         }
         flag_bad<R>(p, bad);
     }
@@ -1677,7 +1684,7 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
         const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
         const int par = sf.parent[s];
         const double* panel = p.Lx + p.off[s];
-        if (code < 0) {
+        if (code == -1) {
             // the factor does not depend on the hand-off: L11, the marks and
             // (whole supernodes, hb <= 128 rows: one per thread) this
             // thread's row of L21 are loaded before the wait
@@ -1734,30 +1741,34 @@ k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __r
                 }
                 if (par >= 0) { SF_STAMP(it, 3); sf_arrive_next(sf.cnt + par, slot, nxt); SF_STAMP(it, 4); }
                 else { SF_STAMP(it, 3); sf_next(slot, nxt); SF_STAMP(it, 4); }
-            } else {                // z_s for the chunk items
-                if (tid < nc) {
-#pragma unroll
-                    for (int r = 0; r < R; r++) sc1_store(sf.zpad + r * sf.zps + sf.zbase[s] + tid, zl[r][tid]);
-                }
-                { SF_STAMP(it, 3); sf_publish_next(sf.flag, s, sf.epoch, slot, nxt); SF_STAMP(it, 4); }
             }
-        } else {                    // y over one 64-row chunk (k_fwd_gemv)
+        } else {
+            // one 64-row chunk of a chunked supernode: the diagonal part
+            // (every chunk item of the supernode solves it, so the chain
+            // has one hand-off per level, not two; z_s to the zpad mirror,
+            // whence the backward sweep takes it), then y over the chunk's
+            // rows (k_fwd_gemv)
             const int i = chunk_r0[code] + lane, kq = wv * 16, nq = min(16, nc - kq);
-            double t[16];             // the factor tile is loaded before the wait
+            double t[16];             // the factor tile, L11, the marks and the list indices before the wait
             {
                 const double* __restrict__ row = panel + nc + min(i, hb - 1) + (size_t)(nq > 0 ? kq : 0) * h;
 #pragma unroll
                 for (int q = 0; q < 16; q++) t[q] = row[(size_t)min(q, max(nq, 1) - 1) * h];
             }
-            chain_wait(sf.flag, s, sf.epoch);
+            stage_l11(panel, h, nc, Ls);
+            if (tid < nc) lv[tid] = p.live[c0 + tid];
+            const int eb = yrow_ptr[c0], ne = yrow_ptr[c0 + nc] - eb;
+            int* sidx = reinterpret_cast<int*>(lds_pad);
+            const bool stg = ne <= kSfIdx;
+            if (stg)
+                for (int e = tid; e < ne; e += NT) sidx[e] = yrow_idx[eb + e];
+            if (tid <= nc) sptr[tid] = yrow_ptr[c0 + tid];
+            chain_wait(sf.cnt, s, sf.epoch * sf.need[s]);
             SF_STAMP(it, 1);
-            SF_STAMP(it, 2);
             if (tid == 0) nxt = sf_draw(sf);
-            if (tid < nc) {
-#pragma unroll
-                for (int r = 0; r < R; r++) zl[r][tid] = sc1_load(sf.zpad + r * sf.zps + sf.zbase[s] + tid);
-            }
-            __syncthreads();
+            fwd_diag<R, true, true>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv, stg ? sidx : nullptr, it,
+                                    stg ? sptr : nullptr, sf.zpad + sf.zbase[s], sf.zps);
+            SF_STAMP(it, 2);
             double acc[R];
 #pragma unroll
             for (int r = 0; r < R; r++) acc[r] = 0.0;
@@ -1792,6 +1803,42 @@ __device__ __forceinline__ void sf_zrow(const SfView& sf, const SweepVecs& V, in
     for (int r = 0; r < R; r++) zi[r] = pi >= 0 ? sc1_load(sf.zpad + r * sf.zps + pi) : V.z[r * V.zs + ri];
 }
 
+// Wave 0 of a backward item: z_s = D^-1 z_s - sub (dscale_rule on the
+// prefetched own z, d, mark; ldlt.c:473-480), then L11', z_s to z and to the
+// zpad mirror.  sub = the four wave partials of xs summed in k_bwd_finish's
+// order (chunked supernodes) or xs[r][0] (whole ones).
+template <int R>
+__device__ __forceinline__ void bwd_sf_solve(const PlanView& p, const SfView& sf, const SweepVecs& V, int s, int c0,
+                                             int nc, bool chunked, const double (&zown)[R], int lvo, double dgo,
+                                             const double (&eps)[R], const double (*Ls)[PC + 1], const int* lv,
+                                             const double (*xs)[4][PC]) {
+    const int lane = threadIdx.x & 63;
+    int bad[R] = {};
+    double zr[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const double sub = chunked ? ((xs[r][0][lane] + xs[r][1][lane]) + xs[r][2][lane]) + xs[r][3][lane]
+                                   : xs[r][0][lane];
+        double zd = 0.0;
+        if (lane < nc) {
+            zd = zown[r];
+            if (lvo) zd = zd / dgo;
+            else if (fabs(zd) > eps[r]) bad[r] = 1;
+            else zd = 0.0;
+        }
+        zr[r] = lane < nc ? zd - sub : 0.0;
+    }
+    tri_upper<R>(zr, Ls, lv, nc, eps, bad);
+    if (lane < nc) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            V.z[r * V.zs + c0 + lane] = zr[r];
+            sc1_store(sf.zpad + r * sf.zps + sf.zbase[s] + lane, zr[r]);
+        }
+    }
+    flag_bad<R>(p, bad);
+}
+
 template <int R>
 __global__ void __launch_bounds__(NT)
 k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __restrict__ sup_chunk0,
@@ -1805,6 +1852,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     double* red = lds_pad;   // colsum scratch
     __shared__ int tk[2];
+    __shared__ int lastc;
     if (tid == 0) { lds_pad[0] = 0.0; tk[0] = sf_draw(sf); }
     __syncthreads();
     for (int par_ = 0;; par_ ^= 1) {
@@ -1820,16 +1868,30 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
         const double* panel = p.Lx + p.off[s];
         const int* __restrict__ rows = p.rows + p.rowptr[s];
         const int kq = wv * 16, nq = min(16, nc - kq);
-        if (code >= 0) {            // partial sums of one 64-row chunk (k_bwd_partial)
+        if (code >= 0) {
+            // partial sums of one 64-row chunk (k_bwd_partial); the chunk
+            // whose arrival comes last finishes the supernode (k_bwd_finish:
+            // the partials in its order, D^-1, L11') -- one hand-off per
+            // level instead of a finish item waiting on the chunks
             const int i = chunk_r0[code] + lane;
             const bool okr = i < hb;
             const int ic = okr ? i : 0;
             const int ri = rows[ic];
             const int pi = sf.zpi[ri];
-            double t[16];             // the factor tile is loaded before the wait
+            double t[16];             // the factor tile, L11, the own z / d / mark before the wait
             const double* __restrict__ col = panel + nc + ic + (size_t)(nq > 0 ? kq : 0) * h;
 #pragma unroll
             for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, max(nq, 1) - 1) * h];
+            stage_l11(panel, h, nc, Ls);
+            if (tid < nc) lv[tid] = p.live[c0 + tid];
+            double zown[R], dgo = 1.0;
+            int lvo = 1;
+            if (wv == 0 && lane < nc) {
+#pragma unroll
+                for (int r = 0; r < R; r++) zown[r] = sc1_load(sf.zpad + r * sf.zps + sf.zbase[s] + lane);
+                lvo = p.live[c0 + lane];
+                dgo = p.dg[c0 + lane];
+            }
             if (par >= 0) chain_wait(sf.flag, par, sf.epoch);
             if (tid == 0) nxt = sf_draw(sf);
             if (nq > 0) {
@@ -1844,7 +1906,30 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             __syncthreads();
             if (tid < R * PC && tid % PC < nc)
                 sc1_store(part + (tid / PC) * ps + (size_t)code * PC + tid % PC, colsum_tree(red, tid / PC, tid % PC));
-            sf_arrive_next(sf.cnt + s, slot, nxt);
+            const int nch = (hb + 63) / 64;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                const int prev = __hip_atomic_fetch_add(sf.cnt + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lastc = prev + 1 == sf.epoch * nch;
+                *slot = nxt;
+            }
+            __syncthreads();
+            if (!lastc) continue;
+            const int cf = sup_chunk0[s];
+            double x[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) x[r] = 0.0;
+            if (lane < nc)
+                for (int c = wv; c < nch; c += 4) {
+#pragma unroll
+                    for (int r = 0; r < R; r++) x[r] += sc1_load(part + r * ps + (size_t)(cf + c) * PC + lane);
+                }
+#pragma unroll
+            for (int r = 0; r < R; r++) xs[r][wv][lane] = x[r];
+            __syncthreads();
+            if (wv == 0) bwd_sf_solve<R>(p, sf, V, s, c0, nc, true, zown, lvo, dgo, eps, Ls, lv, xs);
+            sf_publish_next(sf.flag, s, sf.epoch, slot, nxt);
             continue;
         }
         // nothing below depends on the hand-off but the z values of the
@@ -1857,8 +1942,10 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
         double zown[R], dgo = 1.0;
         int lvo = 1;
         if (wv == 0 && lane < nc) {
+            // a chunked supernode's forward z_s is in the zpad mirror (k_fwd_sf)
 #pragma unroll
-            for (int r = 0; r < R; r++) zown[r] = V.z[r * V.zs + c0 + lane];
+            for (int r = 0; r < R; r++)
+                zown[r] = code == -2 ? sc1_load(sf.zpad + r * sf.zps + sf.zbase[s] + lane) : V.z[r * V.zs + c0 + lane];
             lvo = p.live[c0 + lane];
             dgo = p.dg[c0 + lane];
         }
@@ -1941,32 +2028,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             if (tid < R * PC && tid % PC < nc) xs[tid / PC][0][tid % PC] = colsum_tree(red, tid / PC, tid % PC);
             __syncthreads();
         }
-        if (wv == 0) {
-            int bad[R] = {};
-            double zr[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const double sub = code == -2 ? ((xs[r][0][lane] + xs[r][1][lane]) + xs[r][2][lane]) + xs[r][3][lane]
-                                              : xs[r][0][lane];
-                double zd = 0.0;        // dscale_rule on the prefetched z, d, mark (ldlt.c:473-480)
-                if (lane < nc) {
-                    zd = zown[r];
-                    if (lvo) zd = zd / dgo;
-                    else if (fabs(zd) > eps[r]) bad[r] = 1;
-                    else zd = 0.0;
-                }
-                zr[r] = lane < nc ? zd - sub : 0.0;
-            }
-            tri_upper<R>(zr, Ls, lv, nc, eps, bad);
-            if (lane < nc) {
-#pragma unroll
-                for (int r = 0; r < R; r++) {
-                    V.z[r * V.zs + c0 + lane] = zr[r];
-                    sc1_store(sf.zpad + r * sf.zps + sf.zbase[s] + lane, zr[r]);
-                }
-            }
-            flag_bad<R>(p, bad);
-        }
+        if (wv == 0) bwd_sf_solve<R>(p, sf, V, s, c0, nc, code == -2, zown, lvo, dgo, eps, Ls, lv, xs);
         sf_publish_next(sf.flag, s, sf.epoch, slot, nxt);
     }
 }
@@ -2525,7 +2587,6 @@ void KktDevice::build_sync_free_plan() {
         for (int q = P.level_ptr[l]; q < P.level_ptr[l + 1]; q++) {
             const int sp = P.level_sups[q];
             if (!chunked(sp)) { fi.push_back(make_int2(sp, -1)); continue; }
-            fi.push_back(make_int2(sp, -2));
             for (int c = 0; c < nchunks(sp); c++) fi.push_back(make_int2(sp, h_chunk0_[sp] + c));
         }
     for (int l = P.nlevels - 1; l >= sf_level_; l--)
@@ -2533,7 +2594,6 @@ void KktDevice::build_sync_free_plan() {
             const int sp = P.level_sups[q];
             if (!chunked(sp)) { bi.push_back(make_int2(sp, -1)); continue; }
             for (int c = 0; c < nchunks(sp); c++) bi.push_back(make_int2(sp, h_chunk0_[sp] + c));
-            bi.push_back(make_int2(sp, -2));
         }
     nsf_f_ = static_cast<int>(fi.size());
     nsf_b_ = static_cast<int>(bi.size());
