@@ -205,8 +205,11 @@ class KktDevice {
     DevBuf<int> dchunk_sup_, dchunk_r0_, dsup_chunk0_;
     DevBuf<double> dPartial_;    // backward partial sums, one 64-vector per chunk
     // split-K gather chunks per group (sparse level l, group nlevels = tail)
-    bool visits_ = false;        // deep trees: early gather slots as visits in lower levels' launches
-    std::vector<bool> ck_wide_, ck_flat_;   // ck_flat_: k_update_flat (latency-bound launches of deep trees)      // per gather group: k_update<4> (few chunks, units split >= 4 ways)
+    bool visits_ = false;
+    int gst_group_ = -1, gst_n_ = 0;   // developer gather stamps (IPO_HIP_GATHER_STAMPS)
+    DevBuf<long long> dGStamp_;        // deep trees: early gather slots as visits in lower levels' launches
+    std::vector<int> ck_kind_;   // per gather group: 0 k_update, 1 k_update_flat, 2 k_update_quad
+    std::vector<bool> ck_wide_;   // ck_flat_: k_update_flat (latency-bound launches of deep trees)      // per gather group: k_update<4> (few chunks, units split >= 4 ways)
     std::vector<int> ck_ptr_, sp_ptr_;
     DevBuf<int> dck_u_, dck_b_, dck_e_, dck_part_, dsp_u_, dsp_p0_, dsp_n_;
     DevBuf<int> dck_q_;          // split-unit index of each chunk (-1: unsplit)

@@ -108,13 +108,33 @@ constexpr int KS = kSlab;
 // chunk's records in LDS; the values are then issued without a dependent
 // metadata round trip.  ra = L(row, k), rb = d_k * L(col, k) (the reference
 // form, ldlt.c:572,583), zero where the task leaves the tile entry untouched.
+// The loads are unconditional (an unmarked lane reads the slot's first
+// entry) and the mask / d_k product are applied after them (slot_fin): a
+// load under a lane branch whose result the branch itself consumes makes
+// the compiler wait for it before the branch joins -- one memory round trip
+// per slot, measured as ~0.45 us per slot and wave (IPO_HIP_GATHER_STAMPS).
+struct SlotLd {
+    double a, b, d;
+    bool ra, rb;
+};
+__device__ __forceinline__ SlotLd slot_ld(const SlotRec& m, const double* __restrict__ Lx,
+                                          const double* __restrict__ dg, int lane) {
+    const uint64_t below = (1ull << lane) - 1ull;
+    SlotLd v;
+    v.ra = (m.rmask >> lane) & 1ull;
+    v.rb = (m.cmask >> lane) & 1ull;
+    v.a = Lx[v.ra ? m.roff + __popcll(m.rmask & below) : m.roff];
+    v.b = Lx[v.rb ? m.roff + m.cdelta + __popcll(m.cmask & below) : m.roff];
+    v.d = dg[m.dk];
+    return v;
+}
+__device__ __forceinline__ void slot_fin(const SlotLd& v, double& ra, double& rb) {
+    ra = v.ra ? v.a : 0.0;
+    rb = v.rb ? v.d * v.b : 0.0;
+}
 __device__ __forceinline__ void slot_vals(const SlotRec& m, const double* __restrict__ Lx,
                                           const double* __restrict__ dg, int lane, double& ra, double& rb) {
-    const uint64_t below = (1ull << lane) - 1ull;
-    ra = 0.0;
-    rb = 0.0;
-    if ((m.rmask >> lane) & 1ull) ra = Lx[m.roff + __popcll(m.rmask & below)];
-    if ((m.cmask >> lane) & 1ull) rb = dg[m.dk] * Lx[m.roff + m.cdelta + __popcll(m.cmask & below)];
+    slot_fin(slot_ld(m, Lx, dg, lane), ra, rb);
 }
 
 // Output tile of one gather unit: a 64-row tile of a sparse panel
@@ -187,8 +207,11 @@ __device__ void gather_acc(const PlanView& p, const SlotRec* __restrict__ recs, 
         for (int j = 0; j < KS / 4; j++) mn[j] = wrec[slab * KS + j];
     };
     auto issue = [&]() {
+        SlotLd v[KS / 4];
 #pragma unroll
-        for (int j = 0; j < KS / 4; j++) slot_vals(mn[j], Lx, dg, lane, ra[j], rb[j]);
+        for (int j = 0; j < KS / 4; j++) v[j] = slot_ld(mn[j], Lx, dg, lane);
+#pragma unroll
+        for (int j = 0; j < KS / 4; j++) slot_fin(v[j], ra[j], rb[j]);
     };
     if (nslab > 0) { fetch(0); issue(); }
     if (1 < nslab) fetch(1);
@@ -382,8 +405,9 @@ k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
 // staged by the wave gather_acc gives it (k mod 16 in [4 wv, 4 wv + 4)) and
 // the MFMA steps and |terms| run in gather_acc's order: bitwise the same.
 constexpr int FK = 64;
+#define GST(k) do { if (st && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 __device__ void gather_acc_flat(const PlanView& p, const SlotRec* __restrict__ recs, int kb, int ke, int dcol,
-                                bool has_diag, double4_t (&acc)[2][2], double& dabs) {
+                                bool has_diag, double4_t (&acc)[2][2], double& dabs, long long* st = nullptr) {
     __shared__ double As[TR][FK + 1];
     __shared__ double Bs[TR][FK + 1];
     __shared__ SlotRec rl[FK];
@@ -401,14 +425,21 @@ __device__ void gather_acc_flat(const PlanView& p, const SlotRec* __restrict__ r
         if (tid < nk * 4)
             reinterpret_cast<uint64_t*>(rl)[tid] = reinterpret_cast<const uint64_t*>(recs + k0)[tid];
         __syncthreads();
+        if (k0 == kb) GST(1);
         double ra[FK / 16 * 4], rb[FK / 16 * 4];
+        SlotLd v[FK / 16 * 4];
+#pragma unroll
+        for (int sb = 0; sb < FK / KS; sb++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (sb < nsl) v[sb * 4 + j] = slot_ld(rl[sb * KS + wv * 4 + j], p.Lx, p.dg, lane);
 #pragma unroll
         for (int sb = 0; sb < FK / KS; sb++)
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 ra[sb * 4 + j] = 0.0;
                 rb[sb * 4 + j] = 0.0;
-                if (sb < nsl) slot_vals(rl[sb * KS + wv * 4 + j], p.Lx, p.dg, lane, ra[sb * 4 + j], rb[sb * 4 + j]);
+                if (sb < nsl) slot_fin(v[sb * 4 + j], ra[sb * 4 + j], rb[sb * 4 + j]);
             }
 #pragma unroll
         for (int sb = 0; sb < FK / KS; sb++)
@@ -419,6 +450,7 @@ __device__ void gather_acc_flat(const PlanView& p, const SlotRec* __restrict__ r
                     Bs[lane][sb * KS + wv * 4 + j] = rb[sb * 4 + j];
                 }
         __syncthreads();
+        if (k0 == kb) GST(2);
         for (int kk = 0; kk < nk; kk += 4) {
             double av[2], bv[2];
 #pragma unroll
@@ -440,6 +472,7 @@ __device__ void gather_acc_flat(const PlanView& p, const SlotRec* __restrict__ r
                 }
         }
         __syncthreads();
+        if (k0 == kb) GST(3);
     }
 }
 
@@ -452,7 +485,9 @@ k_update_flat(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ rec
               const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
               const int* __restrict__ ck_part, int c0, double* __restrict__ partial,
               const int* __restrict__ ck_q, const int* __restrict__ sp_p0, const int* __restrict__ sp_n,
-              int* __restrict__ split_cnt) {
+              int* __restrict__ split_cnt, long long* __restrict__ stamps) {
+    long long* st = stamps && blockIdx.x < 1024 ? stamps + blockIdx.x * 8 : nullptr;
+    GST(0);
     const int c = c0 + blockIdx.x;
     const int u = ck_u[c], kb = ck_b[c], ke = ck_e[c], pi = ck_part[c];
     const GatherTile g = unit_tile(p, tv, u, tail);
@@ -461,14 +496,18 @@ k_update_flat(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ rec
     const bool has_diag = g.dscale_col && dcol >= 0 && dcol < g.ncol && lane < g.nrow;
     double4_t acc[2][2];
     double dabs;
+    if (st && threadIdx.x == 0) st[6] = ke - kb;
     if (pi < 0) {
         double old[2][2][4];
         gather_old(g, old);
-        gather_acc_flat(p, recs, kb, ke, dcol, has_diag, acc, dabs);
+        gather_acc_flat(p, recs, kb, ke, dcol, has_diag, acc, dabs, st);
+        GST(4);
         gather_put(g, old, acc, dabs, has_diag, dcol);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        GST(5);
         return;
     }
-    gather_acc_flat(p, recs, kb, ke, dcol, has_diag, acc, dabs);
+    gather_acc_flat(p, recs, kb, ke, dcol, has_diag, acc, dabs, st);
     double* dst = partial + (size_t)pi * (TR * TR + 4 * TR);
     const int tid = threadIdx.x;
 #pragma unroll
@@ -492,6 +531,110 @@ k_update_flat(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ rec
     if (!last) return;
     split_sum<SG>(partial, sp_p0[q], np, acc, dabs);
     gather_store(g, acc, dabs, has_diag, dcol);
+}
+
+// Quadrant gather for the level chain of deep trees.  Measured there
+// (IPO_HIP_GATHER_STAMPS): a 64-slot flat round spends ~7.5 us staging its
+// values -- the CU's outstanding misses, ~8 cache lines per slot from as
+// many source columns -- not in the MFMA steps.  Here a unit's tile is
+// gathered by up to four workgroups, one per 32 x 32 quadrant (the ones
+// outside the tile or above the diagonal are not launched), each fetching
+// only its 32 rows and 32 columns of every slot (lanes 0-31 the rows, 32-63
+// the columns: one load per slot); wave w owns the quadrant's 16 x 16
+// fragment (w & 1, w >> 1).  Every tile entry sees gather_acc's MFMA steps
+// in its k order, and the diagonal's |terms| are summed in its four wave
+// partials, so the factor is bitwise k_update's with one chunk per unit.
+// ck_part holds -1 - quadrant (no split K: a quadrant loops over rounds).
+__global__ void __launch_bounds__(NT)
+k_update_quad(PlanView p, TailView tv, const SlotRec* __restrict__ recs, const int* __restrict__ ck_u,
+              const int* __restrict__ ck_b, const int* __restrict__ ck_e, const int* __restrict__ ck_part, int c0,
+              long long* __restrict__ stamps) {
+    __shared__ double As[32][FK + 1];
+    __shared__ double Bs[32][FK + 1];
+    __shared__ SlotRec rl[FK];
+    long long* st = stamps && blockIdx.x < 1024 ? stamps + blockIdx.x * 8 : nullptr;
+    GST(0);
+    const int c = c0 + blockIdx.x;
+    const int u = ck_u[c], kb = ck_b[c], ke = ck_e[c], q = -1 - ck_part[c];
+    const int qr = 32 * (q & 1), qc = 32 * (q >> 1);
+    const GatherTile g = unit_tile(p, tv, u, -1);
+    const int tid = threadIdx.x;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int fr = 16 * (wv & 1), fc = 16 * (wv >> 1);      // the wave's fragment inside the quadrant
+    const int li = lane & 15, lk = lane >> 4;
+    // the tile's old values of this lane's 4 fragment entries, before the gather
+    double old[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int rr = qr + fr + lk + 4 * i, cc = qc + fc + li;
+        const bool ok = rr < g.nrow && cc < g.ncol && g.row0 + rr >= g.col0 + cc;
+        old[i] = ok ? g.out[rr + (size_t)cc * g.ld] : 0.0;
+    }
+    // diagonal quadrant of a tile with diagonal entries: wave 0's lanes < 32
+    // keep the four wave partials of row qr + lane's |terms|
+    const bool dq = g.dscale_col && qr == qc;
+    const int drow = qr + (lane & 31), dcol = g.row0 + drow - g.col0;
+    const bool has_diag = dq && wv == 0 && lane < 32 && dcol >= 0 && dcol < g.ncol && drow < g.nrow;
+    double dp[4] = {0.0, 0.0, 0.0, 0.0};
+    double4_t acc = (double4_t){0.0, 0.0, 0.0, 0.0};
+    const int half = lane >> 5, idx = lane & 31;
+    const uint64_t bl = (1ull << ((half ? qc : qr) + idx)) - 1ull;
+    const int bit = (half ? qc : qr) + idx;
+    for (int k0 = kb; k0 < ke; k0 += FK) {
+        const int nk = min(FK, ke - k0);
+        if (tid < nk * 4)
+            reinterpret_cast<uint64_t*>(rl)[tid] = reinterpret_cast<const uint64_t*>(recs + k0)[tid];
+        __syncthreads();
+        if (k0 == kb) GST(1);
+        // wave w stages slots w, w + 4, ... (16 per 64-slot round, one load each)
+        // every load issued before any is used (unconditional, clamped to the
+        // slot's first entry; see slot_ld)
+        double v[FK / 4], dv[FK / 4];
+        bool on[FK / 4];
+#pragma unroll
+        for (int j = 0; j < FK / 4; j++) {
+            const int k = min(wv + 4 * j, nk - 1);
+            const SlotRec m = rl[k];
+            const uint64_t mk = half ? m.cmask : m.rmask;
+            on[j] = wv + 4 * j < nk && ((mk >> bit) & 1ull);
+            v[j] = p.Lx[on[j] ? m.roff + (half ? m.cdelta : 0) + __popcll(mk & bl) : m.roff];
+            dv[j] = p.dg[m.dk];
+        }
+#pragma unroll
+        for (int j = 0; j < FK / 4; j++) v[j] = on[j] ? (half ? dv[j] * v[j] : v[j]) : 0.0;
+#pragma unroll
+        for (int j = 0; j < FK / 4; j++) {
+            const int k = wv + 4 * j;
+            if (k < nk) {
+                if (half) Bs[idx][k] = v[j];
+                else As[idx][k] = v[j];
+            }
+        }
+        __syncthreads();
+        if (k0 == kb) GST(2);
+        for (int kk = 0; kk < nk; kk += 4)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(As[fr + li][kk + lk], Bs[fc + li][kk + lk], acc, 0, 0, 0);
+        if (has_diag) {
+            // gather_acc's wave partials: wave w's slots k % 16 in [4w, 4w + 4)
+            for (int sb = 0; sb < nk / KS; sb++)
+#pragma unroll
+                for (int w = 0; w < 4; w++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int k = sb * KS + w * 4 + j;
+                        dp[w] += fabs(As[idx][k] * Bs[idx][k]);
+                    }
+        }
+        __syncthreads();
+        if (k0 == kb) GST(3);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int rr = qr + fr + lk + 4 * i, cc = qc + fc + li;
+        if (rr < g.nrow && cc < g.ncol && g.row0 + rr >= g.col0 + cc) g.out[rr + (size_t)cc * g.ld] = old[i] - acc[i];
+    }
+    if (has_diag) g.dscale_col[dcol] += ((dp[0] + dp[1]) + dp[2]) + dp[3];
+    if (st) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); GST(5); }
 }
 
 // ------------------------------------------------- diagonal block LDL'
@@ -2262,6 +2405,11 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         // deep trees: IPO_HIP_GATHER_FLAT=0 never, 1 (default) deep trees,
         // 2 every launch of at most kFlatMaxChunks chunks
         int flat_mode = 1;
+        if (const char* e = std::getenv("IPO_HIP_GATHER_STAMPS")) gst_group_ = std::atoi(e);
+        // quadrant gathers (k_update_quad) on the narrow levels of deep trees
+        // (IPO_HIP_GATHER_QUAD=0: off)
+        bool quad_mode = true;
+        if (const char* e = std::getenv("IPO_HIP_GATHER_QUAD")) quad_mode = std::atoi(e) != 0;
         if (const char* e = std::getenv("IPO_HIP_GATHER_FLAT")) flat_mode = std::atoi(e);
         int visit_slabs = kVisitSlots / kSlab;
         if (const char* e = std::getenv("IPO_HIP_VISIT_SLOTS")) visit_slabs = std::max(1, std::atoi(e) / kSlab);
@@ -2316,10 +2464,31 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         size_t max_part = 0;
         const int wg_target = 512, min_chunk = 64;     // 64: measured best of 16-256 on configs[3] and dfl001
         // units [u0, u1), slots [kbeg(u), kend(u)) each, then the group's visits
+        // a sparse unit's 32 x 32 quadrants that hold lower-triangle entries (k_update_quad)
+        auto quadrants = [&](int u, int kb, int ke) {
+            const int sp = plan_.unit_sup[u], t = plan_.unit_tile[u];
+            const int nc = plan_.col0[sp + 1] - plan_.col0[sp], h = nc + plan_.rowptr[sp + 1] - plan_.rowptr[sp];
+            const int nrow = std::min(kTileRows, h - t * kTileRows);
+            for (int q = 0; q < 4; q++) {
+                const int qr = q & 1, qc = q >> 1;
+                if (32 * qr >= nrow || 32 * qc >= nc || (t == 0 && qc > qr)) continue;
+                cu.push_back(u); cb.push_back(kb); ce.push_back(ke); cp.push_back(-1 - q); cq.push_back(-1);
+            }
+        };
         auto group = [&](int u0, int u1, auto kbeg, auto kend, const std::vector<int3>* visits) {
             const long nck0 = static_cast<long>(cu.size());
-            long sumk = 0;
-            for (int u = u0; u < u1; u++) sumk += kend(u) - kbeg(u);
+            long sumk = 0, nun = 0;
+            for (int u = u0; u < u1; u++) { sumk += kend(u) - kbeg(u); nun += kend(u) > kbeg(u); }
+            // deep trees' narrow levels: quadrant gathers, one chunk per unit
+            const bool quad = quad_mode && visits && nun + static_cast<long>(visits->size()) <= kQuadMaxUnits;
+            if (quad) {
+                for (int u = u0; u < u1; u++)
+                    if (kend(u) > kbeg(u)) quadrants(u, kbeg(u), kend(u));
+                for (const int3& v : *visits) quadrants(v.x, v.y, v.z);
+                ck_wide_.push_back(false);
+                ck_kind_.push_back(2);
+                return;
+            }
             // aim at >= wg_target workgroups per launch, chunks of min_chunk..512 slots
             long kmax = (sumk / wg_target + kSlab - 1) / kSlab * kSlab;
             kmax = std::max<long>(min_chunk, std::min<long>(kMaxChunkSlots, kmax));
@@ -2347,14 +2516,14 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             // matter) whose units are split many ways waits on its partial
             // sums: sum them several at a time
             ck_wide_.push_back(mx >= 4 && static_cast<long>(cu.size()) - nck0 <= 512);
-            ck_flat_.push_back(flat_mode == 2 || (flat_mode == 1 && visits_)
-                               ? static_cast<long>(cu.size()) - nck0 <= kFlatMaxChunks : false);
+            ck_kind_.push_back(quad ? 2 : (flat_mode == 2 || (flat_mode == 1 && visits_)) &&
+                                               static_cast<long>(cu.size()) - nck0 <= kFlatMaxChunks ? 1 : 0);
         };
         const std::vector<int>& kp = plan_.kslot_ptr;
         ck_wide_.clear();
-        ck_flat_.clear();
+        ck_kind_.clear();
         for (int l = 0; l < plan_.nlevels; l++) {
-            if (l == 0) { ck_wide_.push_back(false); ck_flat_.push_back(false); }
+            if (l == 0) { ck_wide_.push_back(false); ck_kind_.push_back(0); }
             else if (visits_)
                 group(plan_.unit_level_ptr[l], plan_.unit_level_ptr[l + 1], [&](int u) { return late_b[u]; },
                       [&](int u) { return kptr_v[u + 1]; }, &vis[l]);
@@ -2368,7 +2537,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         if (plan_.nt > 0)
             group(0, plan_.ntb * (plan_.ntb + 1) / 2, [&](int u) { return tp[u]; }, [&](int u) { return tp[u + 1]; },
                   nullptr);
-        else { ck_wide_.push_back(false); ck_flat_.push_back(false); }
+        else { ck_wide_.push_back(false); ck_kind_.push_back(0); }
         ck_ptr_[plan_.nlevels + 1] = static_cast<int>(cu.size());
         sp_ptr_[plan_.nlevels + 1] = static_cast<int>(su.size());
         dck_u_.upload(cu, s);
@@ -2874,6 +3043,22 @@ bool KktDevice::finish_pass(bool fused) {
     IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 5 * sizeof(double), hipMemcpyDeviceToHost, s));
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
     IPO_HIP_CHECK(hipStreamSynchronize(s));
+    if (gst_n_ > 0) {      // developer stamps of one gather launch (IPO_HIP_GATHER_STAMPS)
+        std::vector<long long> st(1024 * 8);
+        IPO_HIP_CHECK(hipMemcpy(st.data(), dGStamp_.get(), st.size() * sizeof(long long), hipMemcpyDeviceToHost));
+        long long t0 = st[0];
+        for (int b = 0; b < std::min(gst_n_, 1024); b++) t0 = std::min(t0, st[b * 8]);
+        std::fprintf(stderr, "gather stamps group %d, %d workgroups (us from first start: start rec val mfma acc put slots)\n",
+                     gst_group_, gst_n_);
+        for (int b = 0; b < std::min(gst_n_, 1024); b++) {
+            const long long* q = st.data() + b * 8;
+            std::fprintf(stderr, "  wg %4d: %6.2f %6.2f %6.2f %6.2f %6.2f %6.2f  %lld\n", b, (q[0] - t0) / 100.0,
+                         (q[1] - t0) / 100.0, (q[2] - t0) / 100.0, (q[3] - t0) / 100.0, (q[4] - t0) / 100.0,
+                         (q[5] - t0) / 100.0, q[6]);
+        }
+        gst_n_ = 0;
+        gst_group_ = -1;
+    }
     {
         int f[3];
         std::memcpy(f, hScal_ + 3, sizeof(f));
@@ -2945,15 +3130,28 @@ int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, i
     // groups whose split units have many chunks sum their partials four
     // at a time (more registers: three waves per SIMD drop to two, which
     // the gathers of the other groups would pay for)
-    if (ck_flat_[group]) {
+    // developer stamps (IPO_HIP_GATHER_STAMPS=<group>): per workgroup
+    // s_memrealtime at start / records / values / MFMA / put / stores
+    long long* stq = nullptr;
+    if (gst_group_ == group && tail < 0 && ck_kind_[group] > 0) {
+        if (!dGStamp_.get()) dGStamp_.alloc(1024 * 8);
+        stq = dGStamp_.get();
+        gst_n_ = c1 - c0;
+    }
+    if (ck_kind_[group] == 2) {
+        hipLaunchKernelGGL(k_update_quad, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, recs, dck_u_.get(), dck_b_.get(),
+                           dck_e_.get(), dck_part_.get(), c0, stq);
+        return 1;
+    }
+    if (ck_kind_[group] == 1) {
         if (ck_wide_[group])
         hipLaunchKernelGGL(k_update_flat<4>, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(),
                            dck_b_.get(), dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(),
-                           dsp_p0_.get(), dsp_n_.get(), dSplitCnt_.get());
+                           dsp_p0_.get(), dsp_n_.get(), dSplitCnt_.get(), stq);
         else
         hipLaunchKernelGGL(k_update_flat<1>, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(),
                            dck_b_.get(), dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(),
-                           dsp_p0_.get(), dsp_n_.get(), dSplitCnt_.get());
+                           dsp_p0_.get(), dsp_n_.get(), dSplitCnt_.get(), stq);
         return 1;
     }
     if (ck_wide_[group])

@@ -81,7 +81,8 @@ struct SlotRec {
 constexpr int kMaxChunkSlots = 512;   // largest split-K chunk of the gather
 constexpr int kVisitLevels = 256;     // trees at least this deep gather early slots as visits (kkt_device.hip)
 constexpr int kVisitSlots = 64;       // slots per visit
-constexpr int kFlatMaxChunks = 2048;  // flat gathers for launches of at most this many chunks
+constexpr int kFlatMaxChunks = 2048;
+constexpr int kQuadMaxUnits = 512;    // quadrant gathers for deep-tree launches of at most this many units / visits
 
 struct KktPlan {
     int m = 0, n = 0, T = 0;
