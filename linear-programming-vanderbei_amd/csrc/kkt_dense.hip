@@ -366,6 +366,7 @@ k_tail_dep(PlanView p, TailView tv, int kb, double* __restrict__ st, int* __rest
     const int tid = threadIdx.x, tr = tid & 63, tp = tid >> 6, np = NT >> 6;
     const int row = nc + g * TR + tr;
     const bool rok = row < h;
+    if (sti[2]) return;           // the block column is done: a round enqueued past the end is a no-op
     const int kstart = sti[0], pending = sti[1] - 1;
     double* gmax = st + kDepState;
     if (kstart == 0) {

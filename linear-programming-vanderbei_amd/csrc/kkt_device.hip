@@ -3100,14 +3100,17 @@ void KktDevice::repair_tail() {
         ph_end(kPhSyrk, tb > 0, s);
         // block column tb with the dependent-pivot rule, one round per dependent pivot
         IPO_HIP_CHECK(hipMemsetAsync(dDepI_.get(), 0, 4 * sizeof(int), s));
-        for (int r = 0;; r++) {
+        // rounds enqueued kDepBatch at a time (a round after the last is a
+        // no-op), one host read-back per batch instead of per round
+        constexpr int kDepBatch = 4;
+        for (int r = 0;; r += kDepBatch) {
             if (r > kPanelCols + 1) throw std::runtime_error("kkt: dense-tail dependent-pivot rounds did not finish");
             ph_begin(s);
-            launch_tail_dep_round(pv, tv, tb, dDepSt_.get(), dDepI_.get(), s);
-            ph_end(kPhDiag, 1, s);
+            for (int b = 0; b < kDepBatch; b++) launch_tail_dep_round(pv, tv, tb, dDepSt_.get(), dDepI_.get(), s);
+            ph_end(kPhDiag, kDepBatch, s);
             IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 6, dDepI_.get() + 2, sizeof(int), hipMemcpyDeviceToHost, s));
             IPO_HIP_CHECK(hipStreamSynchronize(s));
-            tm_.tail_dep_rounds++;
+            tm_.tail_dep_rounds += kDepBatch;
             if (hFlags_[6]) break;
         }
         for (int t = tb + 1; t < plan_.ntb; t++) {
