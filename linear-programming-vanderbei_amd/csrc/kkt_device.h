@@ -176,6 +176,10 @@ class KktDevice {
     DevBuf<int> dunit_sup_, dunit_tile_, dtask_ptr_, dtask_pair_, dtask_i0_, dtask_i1_;
     DevBuf<int> dupd_src_, dupd_r0_, dupd_r1_, drel_, dlevel_sups_;
     DevBuf<int> dyrow_ptr_, dyrow_idx_;
+    // deep trees: the narrow range's update lists without the values from
+    // below the range, and those values' lists for the pre-pass (k_fwd_pre)
+    int pre_cols_ = 0;
+    DevBuf<int> dylate_ptr_, dylate_idx_, dpre_col_, dpre_ptr_, dpre_idx_;
     DevBuf<double> dYbuf_;
     // sync-free top levels of the sweeps (k_fwd_sf / k_bwd_sf)
     void build_sync_free_plan();

@@ -1796,6 +1796,43 @@ __device__ __forceinline__ void sf_publish_next(int* flags, int i, int epoch, in
 }
 
 
+// Forward pre-pass of deep trees (build_sync_free_plan): z_c -= the sum of
+// the update values column c of the narrow range receives from below the
+// range, in list order, one thread per column (eight loads in flight).
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_fwd_pre(int ncols, const int* __restrict__ col, const int* __restrict__ eptr, const int* __restrict__ eidx,
+          SweepVecs V) {
+    const int j = blockIdx.x * NT + threadIdx.x;
+    if (j >= ncols) return;
+    const int c = col[j];
+    double acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = 0.0;
+    int e = eptr[j];
+    const int e1 = eptr[j + 1];
+    for (; e + 7 < e1; e += 8) {
+        int ix[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) ix[u] = eidx[e + u];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            double yv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) yv[u] = V.y[r * V.ys + ix[u]];
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc[r] += yv[u];
+        }
+    }
+    for (; e < e1; e++) {
+        const int i0 = eidx[e];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] += V.y[r * V.ys + i0];
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) V.z[r * V.zs + c] -= acc[r];
+}
+
 template <int R>
 __global__ void __launch_bounds__(NT)
 k_fwd_sf(PlanView p, SfView sf, const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
@@ -2749,6 +2786,48 @@ void KktDevice::build_sync_free_plan() {
     }
     dyrow_idx_.upload(yidx, s);
     dybase_.upload(ybase, s);
+    // Deep trees: the update values a narrow-range column receives from
+    // supernodes below the range (on configs[3] the 10^6 leaves and the wide
+    // levels: ~30 scattered values per row, ~5 us of the chain item's loads)
+    // are all known once the bottom levels are swept.  They are subtracted
+    // from the right-hand side by one pre-pass launch (k_fwd_pre: per column,
+    // in list order), and the sync-free items sum only the values of
+    // supernodes inside the range (their own lists, ylate_*).
+    pre_cols_ = 0;
+    {
+        const char* ve = std::getenv("IPO_HIP_VISITS");
+        const bool deep = ve ? std::atoi(ve) != 0 : P.nlevels >= kVisitLevels;
+        if (deep && sf_level_ < P.nlevels) {
+            auto src_of = [&](int i) {        // the supernode whose row set holds R entry i
+                return static_cast<int>(std::upper_bound(P.rowptr.begin(), P.rowptr.end(), i) - P.rowptr.begin()) - 1;
+            };
+            std::vector<int> lptr(T_ + 1, 0), lidx, ecol, eptr{0}, eidx;
+            for (int v = 0; v < T_; v++) {
+                const int sv = v < P.tail_c0 ? P.sup_of[v] : -1;
+                const bool in_range = sv >= 0 && P.level[sv] >= sf_level_;
+                bool any_early = false;
+                // (columns outside the range keep empty late lists: only k_fwd_sf reads these)
+                for (int e = in_range ? P.yrow_ptr[v] : 0; e < (in_range ? P.yrow_ptr[v + 1] : 0); e++) {
+                    const bool early = P.level[src_of(P.yrow_idx[e])] < sf_level_;
+                    if (early) {
+                        if (!any_early) { ecol.push_back(v); any_early = true; }
+                        eidx.push_back(yidx[e]);
+                    } else {
+                        lidx.push_back(yidx[e]);
+                    }
+                }
+                if (any_early) eptr.push_back(static_cast<int>(eidx.size()));
+                lptr[v + 1] = static_cast<int>(lidx.size());
+            }
+            pre_cols_ = static_cast<int>(ecol.size());
+            dylate_ptr_.upload(lptr, s);
+            dylate_idx_.upload(lidx.empty() ? std::vector<int>{0} : lidx, s);
+            dpre_col_.upload(ecol.empty() ? std::vector<int>{0} : ecol, s);
+            dpre_ptr_.upload(eptr, s);
+            dpre_idx_.upload(eidx.empty() ? std::vector<int>{0} : eidx, s);
+            IPO_HIP_CHECK(hipStreamSynchronize(s));
+        }
+    }
     ybuf_stride_ = std::max<size_t>(yend, 1);
     dYbuf_.alloc(2 * ybuf_stride_);
     std::vector<int2> fi, bi;
@@ -3232,8 +3311,13 @@ void KktDevice::sweep(double* dz, const double* epsp) {
         const SfView sf{dsf_items_f_.get(), nsf_f_, dsf_fcnt_.get(), dsf_fflag_.get(), dsf_need_.get(), dsf_par_.get(),
                         dsf_zbase_.get(), dsf_zpi_.get(), dZpad_.get(), zpad_stride_, ++sf_fwd_epoch_,
                         dsf_ticket_.get(), sf_tbase(0, nsf_f_)};
+        const bool pre = pre_cols_ > 0 || dylate_ptr_.get();
+        if (pre_cols_ > 0)
+            hipLaunchKernelGGL(k_fwd_pre<R>, dim3(ceil_div(pre_cols_, NT)), dim3(NT), 0, s, pre_cols_, dpre_col_.get(),
+                               dpre_ptr_.get(), dpre_idx_.get(), V);
         hipLaunchKernelGGL(k_fwd_sf<R>, dim3(std::min(sf_grid_, nsf_f_)), dim3(NT), kChainLds, s, pv, sf,
-                           dyrow_ptr_.get(), dyrow_idx_.get(), dchunk_r0_.get(), V, epsp);
+                           pre ? dylate_ptr_.get() : dyrow_ptr_.get(), pre ? dylate_idx_.get() : dyrow_idx_.get(),
+                           dchunk_r0_.get(), V, epsp);
     }
     if (plan_.nt > 0) {
         const TailView tv = tail_view();

@@ -1,0 +1,8 @@
+#!/bin/bash
+# round-3 GPU call W: forward pre-pass of deep trees -- deep tests, banded probe, all GPU tests
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+S=tools/gpu_step.sh
+$S 300 r03w_deep.log python -u -m pytest tests/test_gpu_deep.py -m gpu -x -q --timeout 200 --timeout-method thread -rfEx || exit 1
+$S 200 r03w_bp.log python3 tools/banded_probe.py 3 1 || exit 1
+$S 500 r03w_tests.log python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -rfEx || exit 1
