@@ -147,8 +147,8 @@ k_reduce_jobs(RedJobs jobs, double* __restrict__ part);
 // Host helper: run jobs, finish into out[0..nj) (device), async on stream.
 // With g_ordered_reductions (default) dot jobs are summed in index order like
 // the reference's dotprod(); otherwise by a fixed-shape tree.
-// dots of at least kOrderedMaxLen entries use a fixed strided order instead
-// (dev_common.hip, k_reduce_ordered)
+// dots of at least kOrderedMaxLen entries use a fixed segmented order instead
+// (dev_common.hip, k_dot_segments / k_dot_finish; part: kRedBlocks per job)
 constexpr int kOrderedMaxLen = 1 << 19;
 extern bool g_ordered_reductions;
 void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st);

@@ -73,35 +73,7 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
         if (tid == 0) out[j] = acc;
         return;
     }
-    if (len >= kOrderedMaxLen) {
-        // very long vectors (synthetic LPs of 10^6 columns; no netlib problem
-        // comes near): one sequential chain of len adds took 4.3 ms.  Fixed
-        // strided order instead: thread t sums i = t, t + 256, ... in index
-        // order (eight loads in flight), the 256 partials are added in thread
-        // order -- deterministic, not the reference's rounding
-        __shared__ double part[kOrdThreads];
-        double acc = 0.0;
-        for (int i0 = 0; i0 < len; i0 += 8 * kOrdThreads) {
-            double pa[8], pb[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int i = i0 + u * kOrdThreads + tid;
-                pa[u] = i < len ? a[i] : 0.0;
-                pb[u] = i < len ? b[i] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (i0 + u * kOrdThreads + tid < len) acc += pa[u] * pb[u];
-        }
-        part[tid] = acc;
-        __syncthreads();
-        if (tid == 0) {
-            double s = 0.0;
-            for (int t = 0; t < kOrdThreads; t++) s += part[t];
-            out[j] = s;
-        }
-        return;
-    }
+    if (len >= kOrderedMaxLen) return;     // k_dot_segments / k_dot_finish (launch_reduce)
     constexpr int CH = 8192;
     __shared__ __attribute__((aligned(16))) double prod[CH + 16];   // + one batch of read-ahead
     double s = 0.0e0;
@@ -144,6 +116,54 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
     if (tid == 0) out[j] = s;
 }
 
+// Dots of at least kOrderedMaxLen entries (synthetic LPs of 10^6 columns; no
+// netlib problem comes near): one sequential chain of len adds took 4.3 ms,
+// one 256-thread block 1.1 ms.  Fixed segmented order instead: the vector
+// in kRedBlocks contiguous segments, segment g summed by block g (thread t
+// takes its entries i = t, t + 256, ... in index order, the 256 partials
+// added in thread order), the segment sums added in segment order by
+// k_dot_finish -- deterministic, not the reference's rounding.
+__global__ void __launch_bounds__(kOrdThreads)
+k_dot_segments(RedJobs jobs, double* __restrict__ part) {
+    const int j = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+    const int len = jobs.len[j];
+    if (jobs.op[j] != 0 || len < kOrderedMaxLen) return;
+    const long seg = (static_cast<long>(len) + kRedBlocks - 1) / kRedBlocks;
+    const long b = seg * g, e = min(static_cast<long>(len), b + seg);
+    const double* a = jobs.a[j];
+    const double* bb = jobs.b[j];
+    __shared__ double sh[kOrdThreads];
+    double acc = 0.0;
+    for (long i0 = b; i0 < e; i0 += 8 * kOrdThreads) {
+        double pa[8], pb[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const long i = i0 + u * kOrdThreads + tid;
+            pa[u] = i < e ? a[i] : 0.0;
+            pb[u] = i < e ? bb[i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (i0 + u * kOrdThreads + tid < e) acc += pa[u] * pb[u];
+    }
+    sh[tid] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        double s = 0.0;
+        for (int t = 0; t < kOrdThreads; t++) s += sh[t];
+        part[j * kRedBlocks + g] = s;
+    }
+}
+
+__global__ void __launch_bounds__(64)
+k_dot_finish(RedJobs jobs, const double* __restrict__ part, double* __restrict__ out) {
+    const int j = threadIdx.x;
+    if (j >= jobs.nj || jobs.op[j] != 0 || jobs.len[j] < kOrderedMaxLen) return;
+    double s = 0.0;
+    for (int g = 0; g < kRedBlocks; g++) s += part[j * kRedBlocks + g];
+    out[j] = s;
+}
+
 __global__ void __launch_bounds__(256)
 k_link_ax(int mrow, int m, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
           const double* __restrict__ x, double* __restrict__ out) {
@@ -167,6 +187,12 @@ bool g_ordered_reductions = true;
 void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st) {
     if (g_ordered_reductions) {
         hipLaunchKernelGGL(k_reduce_ordered, dim3(jobs.nj), dim3(kOrdThreads), 0, st, jobs, out);
+        bool longdot = false;
+        for (int j = 0; j < jobs.nj; j++) longdot |= jobs.op[j] == 0 && jobs.len[j] >= kOrderedMaxLen;
+        if (longdot) {     // part holds kRedBlocks partials per job (the callers' buffers: 8 jobs)
+            hipLaunchKernelGGL(k_dot_segments, dim3(kRedBlocks, jobs.nj), dim3(kOrdThreads), 0, st, jobs, part);
+            hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(64), 0, st, jobs, part, out);
+        }
         IPO_HIP_CHECK(hipGetLastError());
         return;
     }
