@@ -233,11 +233,19 @@ def hbm_roofline_leg(reps):
         gbs = byts / (ms * 1e-3) / 1e9
         kernels[k] = {"ms_per_launch": ms, "algorithmic_bytes_per_launch": byts, "achieved_gbs": gbs,
                       "frac": gbs / HBM_PEAK_GBS}
+    # measured HBM bytes per launch (profiles/<round>_pmc_hbm.json, rocprofv3
+    # FETCH_SIZE / WRITE_SIZE passes over the same kernels), when committed
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_hbm.json")))
+    hk = json.load(open(files[-1]))["kernels"] if files else {}
+    for k in kernels:
+        kernels[k]["traffic"] = hk.get(k, {}).get("hbm_bytes_per_launch")
+        kernels[k]["traffic_source"] = os.path.basename(files[-1]) if k in hk else None
     top = max(kernels, key=lambda k: kernels[k]["ms_per_launch"])
     t = kernels[top]
     return {"workload": HBM_WORKLOAD, "m": p.m, "n": p.n, "nz": p.nz, "launches_timed": reps, "kernels": kernels,
             "roofline": {"bound": "hbm", "kernel": top, "achieved": t["achieved_gbs"], "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": t["frac"], "traffic": None}}
+                         "unit": "GB/s", "frac": t["frac"], "traffic": t["traffic"]}}
 
 
 def with_watchdog(seconds, fn, on_timeout):

@@ -14,8 +14,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_trace -o
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${tag}_pmc_fetch -o run -- $B --no-timing --steps 1 > gpurun_out/${tag}_pmc_fetch.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${tag}_pmc_write -o run -- $B --no-timing --steps 1 > gpurun_out/${tag}_pmc_write.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/${tag}_pmc_mfma -o run -- $B --no-timing --steps 1 > gpurun_out/${tag}_pmc_mfma.log 2>&1 || exit 1
+# HBM traffic of the hbm_roofline leg's vector kernels (configs[3] uniform LP)
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${tag}_pmc_hfetch -o run -- python3 tools/hbm_probe.py 5 > gpurun_out/${tag}_pmc_hfetch.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${tag}_pmc_hwrite -o run -- python3 tools/hbm_probe.py 5 > gpurun_out/${tag}_pmc_hwrite.log 2>&1 || exit 1
 # the databases exceed what gpurun copies back: summarise here, keep the summaries
 mkdir -p gpurun_out/prof_${tag}
 python3 tools/profile_summary.py ${tag} gpurun_out gpurun_out/prof_${tag} || exit 1
-rm -rf gpurun_out/${tag}_trace gpurun_out/${tag}_pmc_fetch gpurun_out/${tag}_pmc_write gpurun_out/${tag}_pmc_mfma
+rm -rf gpurun_out/${tag}_trace gpurun_out/${tag}_pmc_fetch gpurun_out/${tag}_pmc_write gpurun_out/${tag}_pmc_mfma \
+       gpurun_out/${tag}_pmc_hfetch gpurun_out/${tag}_pmc_hwrite
 echo profile_round $tag done

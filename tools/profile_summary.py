@@ -132,6 +132,26 @@ if os.path.exists(mdb):
                              "MFMA-busy cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); MOPS_F64 in units of 512 "
                              "flops; tflops over the kernel-trace average duration",
                    "phases": mph, "kernels": mk}, fh, indent=1)
+# HBM bytes per launch of the hbm_roofline leg's kernels (tools/hbm_probe.py
+# under the same FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled)
+hf = os.path.join(src, f"{tag}_pmc_hfetch", "run_results.db")
+if os.path.exists(hf):
+    hfetch = per_kernel(hf, "FETCH_SIZE")
+    hwrite = per_kernel(os.path.join(src, f"{tag}_pmc_hwrite", "run_results.db"), "WRITE_SIZE")
+    hk = {}
+    for k in sorted(set(hfetch) | set(hwrite)):
+        kb = base(k)
+        if kb not in ("k_hsd_residuals", "k_hsd_directions", "k_step"):
+            continue
+        fs, fn = hfetch.get(k, (0.0, 0))
+        ws, wn = hwrite.get(k, (0.0, 0))
+        hk[kb] = {"launches": max(fn, wn), "fetch_bytes_per_launch": 2 * 1024 * fs / max(fn, 1),
+                  "write_bytes_per_launch": 1024 * ws / max(wn, 1)}
+        hk[kb]["hbm_bytes_per_launch"] = hk[kb]["fetch_bytes_per_launch"] + hk[kb]["write_bytes_per_launch"]
+    with open(os.path.join(dst, f"{tag}_pmc_hbm.json"), "w") as fh:
+        json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, tools/hbm_probe.py 5 (bench.py's "
+                             "hbm_roofline kernels, BASELINE configs[3] uniform LP); FETCH_SIZE doubled (gfx950)",
+                   "kernels": hk}, fh, indent=1)
 line = [ln for ln in open(os.path.join(src, f"{tag}_bench.log")) if ln.startswith("{")][-1]
 with open(os.path.join(dst, f"{tag}_bench.json"), "w") as fh:
     fh.write(line)
