@@ -670,99 +670,6 @@ __device__ __forceinline__ void win_solve(double (&a)[WIN], int cw0, int nc, boo
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
-// ------------------------------------------------ half-workgroup gather
-// One half (4 waves) of a 512-thread workgroup gathers k-slots [kb, ke) of
-// one sparse unit (SlotRec records, kkt_plan.h) into a 64 x 64 product: wave
-// hw's 32 x 32 quarter (rows 32 (hw & 1), columns 32 (hw >> 1)) in acc, and,
-// for the diagonal tile, its |terms| partial of row `lane` in dpart.  The
-// operations and their order are k_update's (kkt_device.hip: the slab k
-// order of the MFMA steps, wave hw's partial over the slots k % 16 in
-// [4 hw, 4 hw + 4)), so a tile updated here is bitwise one updated there.
-// Rounds of 32 slots; both halves run `nrounds` rounds (the barriers are
-// the workgroup's), a half with fewer slots idles through the rest.
-constexpr int HGK = 32;
-struct HalfGatherLds {
-    double A[TR][HGK + 1];
-    double B[TR][HGK + 1];
-    SlotRec rec[HGK];
-};
-static_assert(TR * (PC + 2) <= 2 * TR * (HGK + 1), "the transpose image fits the half's staging");
-
-__device__ __forceinline__ void half_gather(const PlanView& p, const SlotRec* __restrict__ recs, int kb, int ke,
-                                            int nrounds, int hw, bool terms, HalfGatherLds& L, double4_t (&acc)[2][2],
-                                            double& dpart) {
-    const int lane = threadIdx.x & 63, htid = threadIdx.x & 255;
-    const int wr = (hw & 1) * 32, wc = (hw >> 1) * 32, li = lane & 15, lk = lane >> 4;
-    const uint64_t below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
-    dpart = 0.0;
-    for (int r = 0; r < nrounds; r++) {
-        const int k0 = kb + r * HGK, nk = max(0, min(HGK, ke - k0));
-        if (htid < nk * 4)
-            reinterpret_cast<uint64_t*>(L.rec)[htid] = reinterpret_cast<const uint64_t*>(recs + k0)[htid];
-        __syncthreads();
-        // every load issued before any is used (unconditional, clamped)
-        double va[HGK / 16 * 4], vb[HGK / 16 * 4], vd[HGK / 16 * 4];
-        bool oa[HGK / 16 * 4], ob[HGK / 16 * 4];
-#pragma unroll
-        for (int sb = 0; sb < HGK / 16; sb++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int q = sb * 4 + j;
-                if (sb * 16 < nk) {
-                    const SlotRec m = L.rec[sb * 16 + hw * 4 + j];
-                    oa[q] = (m.rmask >> lane) & 1ull;
-                    ob[q] = (m.cmask >> lane) & 1ull;
-                    va[q] = p.Lx[oa[q] ? m.roff + __popcll(m.rmask & below) : m.roff];
-                    vb[q] = p.Lx[ob[q] ? m.roff + m.cdelta + __popcll(m.cmask & below) : m.roff];
-                    vd[q] = p.dg[m.dk];
-                }
-            }
-#pragma unroll
-        for (int sb = 0; sb < HGK / 16; sb++)
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int q = sb * 4 + j, k = sb * 16 + hw * 4 + j;
-                if (sb * 16 < nk) {
-                    L.A[lane][k] = oa[q] ? va[q] : 0.0;
-                    L.B[lane][k] = ob[q] ? vd[q] * vb[q] : 0.0;
-                }
-            }
-        __syncthreads();
-        for (int kk = 0; kk < nk; kk += 4) {
-            double av[2], bv[2];
-#pragma unroll
-            for (int a = 0; a < 2; a++) av[a] = L.A[wr + a * 16 + li][kk + lk];
-#pragma unroll
-            for (int b = 0; b < 2; b++) bv[b] = L.B[wc + b * 16 + li][kk + lk];
-#pragma unroll
-            for (int a = 0; a < 2; a++)
-#pragma unroll
-                for (int b = 0; b < 2; b++)
-                    acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
-        }
-        if (terms) {
-            for (int sb = 0; sb < nk / 16; sb++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int k = sb * 16 + hw * 4 + j;
-                    dpart += fabs(L.A[lane][k] * L.B[lane][k]);
-                }
-        }
-        __syncthreads();
-    }
-}
-
-// LDS of the fused late gather inside a panel workgroup (both halves, then
-// the four half-0 |terms| partials of each diagonal row)
-struct LateLds {
-    HalfGatherLds h[2];
-    double dred[4][TR];
-};
-
 // Dense-tail panels of the look-ahead factorisation first apply block
 // column t - 1's update to their own rows (the diagonal block and tile j +
 // 1), the way k_tail_syrk would: operands staged here, products (old - acc
@@ -792,9 +699,7 @@ struct PanelLds {
 // goes to wtail.
 __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __restrict__ fu_sup,
                                              const int* __restrict__ fu_j, int f0, const TailView& tv, int kb, int bid,
-                                             PanelLds& S, double* wtail, bool pre = false,
-                                             const SlotRec* __restrict__ grecs = nullptr,
-                                             int4 grng = make_int4(0, 0, 0, 0)) {
+                                             PanelLds& S, double* wtail, bool pre = false) {
     double (*Ct)[CTS] = S.Ct;
     double (*Lr)[PC] = S.Lr;
     double (*Lb)[PC] = S.Lb;
@@ -843,41 +748,6 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
     double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
     double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
-    if (grecs && (grng.x < grng.y || grng.z < grng.w)) {
-        // deep trees' chain levels (KktDevice, fused levels): the level's
-        // own gather of the diagonal unit (half 0: slots grng.x .. y) and of
-        // tile j + 1's unit (half 1: grng.z .. w), applied to the loaded
-        // rows -- what k_update_quad would have stored (bitwise), without
-        // its launch on the level chain
-        LateLds& G = *reinterpret_cast<LateLds*>(&S);
-        const int hw = wv & 3, hf = h1 ? 1 : 0;
-        const int nr = max((grng.y - grng.x + HGK - 1) / HGK, (grng.w - grng.z + HGK - 1) / HGK);
-        double4_t acc[2][2];
-        double dpart;
-        half_gather(p, grecs, h1 ? grng.z : grng.x, h1 ? grng.w : grng.y, nr, hw, !h1, G.h[hf], acc, dpart);
-        // products to LDS as [column][row] over the half's staging (free
-        // after the last round's barrier), the |terms| partials beside
-        double (*Am)[PC + 2] = reinterpret_cast<double (*)[PC + 2]>(&G.h[hf].A[0][0]);
-        const int wr = (hw & 1) * 32, wc = (hw >> 1) * 32;
-#pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int y = 0; y < 2; y++)
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    Am[wc + y * 16 + (lane & 15)][wr + x * 16 + (lane >> 4) + 4 * i] = acc[x][y][i];
-        if (!h1) G.dred[hw][lane] = dpart;
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < WIN; q++) {
-            const int c = cw0 + q;
-            if (rok && c < nc && (h1 || c <= row)) a[q] = a[q] - Am[c][lane];
-        }
-        if (!h1 && lane < nc && (lane >> 4) == w)
-            dsc = dsc + (((G.dred[0][lane] + G.dred[1][lane]) + G.dred[2][lane]) + G.dred[3][lane]);
-        dsc_pre = dsc;
-        __syncthreads();                   // the panel's LDS image overwrites G from here
-    }
     if (pre) {
         // dense tail, block column kb > 0: block kb - 1's update of this
         // workgroup's rows, k_tail_syrk's MFMA fragments and order; the
@@ -1043,8 +913,6 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
             }
         }
         if (pre && j == 0 && !h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc_pre;
-    } else if (grecs && j == 0 && !h1 && lane < nc && (lane >> 4) == w) {
-        p.dscale[c0 + lane] = dsc_pre;     // what the level's gather would have left there
     }
     if (j != 0) return;
     // workgroup 0: L11' into the upper slot through an LDS transpose (Ct is
@@ -1064,87 +932,6 @@ __global__ void __launch_bounds__(PNT)
 k_panel_w(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j, int f0, TailView tv, int kb) {
     __shared__ __attribute__((aligned(16))) char lds[sizeof(PanelLds)];
     panel_w_body(p, fu_sup, fu_j, f0, tv, kb, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), tv.W);
-}
-
-// A sparse unit's tile (kkt_device.hip's unit_tile for the sparse levels)
-struct UnitTile {
-    double* out;
-    int ld, nrow, ncol, c0;
-    bool diag;
-};
-__device__ __forceinline__ UnitTile sparse_unit(const PlanView& p, int u) {
-    const int s = p.unit_sup[u], t = p.unit_tile[u];
-    const int c0 = p.col0[s], nc = p.col0[s + 1] - c0, h = nc + (p.rowptr[s + 1] - p.rowptr[s]);
-    UnitTile g;
-    g.out = p.Lx + p.off[s] + t * TR;
-    g.ld = h;
-    g.nrow = min(TR, h - t * TR);
-    g.ncol = nc;
-    g.c0 = c0;
-    g.diag = t == 0;
-    return g;
-}
-
-// One launch per chain level of a deep tree (fused levels, KktDevice):
-// workgroups [0, nfu) are the level's windowed panels, each first applying
-// the level's own gather of its rows (frng[f]: slot ranges of the diagonal
-// unit and of tile j + 1's unit); the rest apply the level's visits (gathers
-// of later levels' units from finished supernodes), two per workgroup, one
-// per half (vis[v] = {unit, slot begin, slot end, -}), each a
-// read-modify-write of its tile in k_update_quad's operations.
-constexpr size_t kLevelLds = sizeof(PanelLds) > sizeof(LateLds) ? sizeof(PanelLds) : sizeof(LateLds);
-__global__ void __launch_bounds__(PNT)
-k_level(PlanView p, const SlotRec* __restrict__ recs, const int* __restrict__ fu_sup, const int* __restrict__ fu_j,
-        int f0, int nfu, const int4* __restrict__ frng, const int4* __restrict__ vis, int v0, int nv, TailView tv) {
-    __shared__ __attribute__((aligned(16))) char lds[kLevelLds];
-    if ((int)blockIdx.x < nfu) {
-        panel_w_body(p, fu_sup, fu_j, f0, tv, -1, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), nullptr, false, recs,
-                     frng[f0 + blockIdx.x]);
-        return;
-    }
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hw = wv & 3, hf = wv >> 2;
-    const int vi = 2 * (blockIdx.x - nfu) + hf;          // this half's visit
-    const bool has = vi < nv;
-    const int4 e = has ? vis[v0 + vi] : make_int4(0, 0, 0, 0);
-    const int4 o = vi + (hf ? -1 : 1) < nv ? vis[v0 + vi + (hf ? -1 : 1)] : make_int4(0, 0, 0, 0);
-    const int nr = max((e.z - e.y + HGK - 1) / HGK, (o.z - o.y + HGK - 1) / HGK);   // both halves' rounds
-    LateLds& G = *reinterpret_cast<LateLds*>(lds);
-    UnitTile g{};
-    if (has) g = sparse_unit(p, e.x);
-    const int wr = (hw & 1) * 32, wc = (hw >> 1) * 32;
-    double old[2][2][4];
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int y = 0; y < 2; y++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int rr = wr + x * 16 + (lane >> 4) + 4 * i, cc = wc + y * 16 + (lane & 15);
-                const bool ok = has && rr < g.nrow && cc < g.ncol && (!g.diag || rr >= cc);
-                old[x][y][i] = ok ? g.out[rr + (size_t)cc * g.ld] : 0.0;
-            }
-    double4_t acc[2][2];
-    double dpart;
-    half_gather(p, recs, e.y, has ? e.z : e.y, nr, hw, has && g.diag, G.h[hf], acc, dpart);
-    if (has) {
-#pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int y = 0; y < 2; y++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const int rr = wr + x * 16 + (lane >> 4) + 4 * i, cc = wc + y * 16 + (lane & 15);
-                    if (rr < g.nrow && cc < g.ncol && (!g.diag || rr >= cc))
-                        g.out[rr + (size_t)cc * g.ld] = old[x][y][i] - acc[x][y][i];
-                }
-    }
-    // the four wave partials of each diagonal row, added in wave order
-    // (k_update's dred) over the half's staging, free after the gather
-    double* dr = &G.h[hf].A[0][0];
-    dr[hw * TR + lane] = dpart;
-    __syncthreads();
-    if (has && g.diag && hw == 0 && lane < g.nrow && lane < g.ncol)
-        p.dscale[g.c0 + lane] += ((dr[lane] + dr[TR + lane]) + dr[2 * TR + lane]) + dr[3 * TR + lane];
 }
 
 // ------------------------------------------- dense tail: look-ahead steps
@@ -1467,13 +1254,6 @@ size_t tail_dep_state_doubles(int ntb) { return kDepState + static_cast<size_t>(
 
 void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, double* st, int* sti, hipStream_t s) {
     hipLaunchKernelGGL(k_tail_dep, dim3(tail_dep_tiles(tv, kb)), dim3(NT), 0, s, pv, tv, kb, st, sti);
-}
-
-void launch_level(const PlanView& pv, const SlotRec* recs, const int* fu_sup, const int* fu_j, int f0, int nfu,
-                  const int4* frng, const int4* vis, int v0, int nv, const TailView& tv, hipStream_t s) {
-    if (nfu + nv <= 0) return;
-    hipLaunchKernelGGL(k_level, dim3(nfu + (nv + 1) / 2), dim3(PNT), 0, s, pv, recs, fu_sup, fu_j, f0, nfu, frng, vis, v0,
-                       nv, tv);
 }
 
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s) {

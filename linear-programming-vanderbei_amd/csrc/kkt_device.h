@@ -196,10 +196,6 @@ class KktDevice {
     DevBuf<int> dybase_;                  // per supernode: first ybuf slot of its update values
     DevBuf<double> dZpad_;                // padded z slices of the range, 2 right-hand sides
     std::vector<int> fu_ptr_;             // per level: fused panel units [fu_ptr_[l], fu_ptr_[l+1])
-    std::vector<int> h_fu_sup_, h_fu_j_;  // host copies of the fused panel unit lists
-    std::vector<char> lvl_fused_;         // per level: gather + panel + visits in one k_level launch
-    std::vector<int> lvis_ptr_;           // per level: its visits in dlvis_
-    DevBuf<int4> dfrng_, dlvis_;          // per fused panel unit: late slot ranges; the fused levels' visits
     DevBuf<int> dfu_sup_, dfu_j_;         // fused panel unit -> supernode, tile pair index
     std::vector<int> small_ptr_;          // per level: small panels [small_ptr_[l], small_ptr_[l+1]) (k_panel_s)
     DevBuf<int> dsmall_sups_;

@@ -2365,8 +2365,6 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         }
         dfu_sup_.upload(fs, s);
         dfu_j_.upload(fj, s);
-        h_fu_sup_ = fs;
-        h_fu_j_ = fj;
         dsmall_sups_.upload(ss, s);
         IPO_HIP_CHECK(hipStreamSynchronize(s));
         // IPO_HIP_PANEL=0: per-phase kernels only (k_diag + k_trsm + k_tail_syrk,
@@ -2575,43 +2573,6 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         else { ck_wide_.push_back(false); ck_kind_.push_back(0); }
         ck_ptr_[plan_.nlevels + 1] = static_cast<int>(cu.size());
         sp_ptr_[plan_.nlevels + 1] = static_cast<int>(su.size());
-        // chain levels of deep trees in one launch each (k_level): levels
-        // gathered by quadrants whose supernodes all take the windowed panel;
-        // each panel workgroup gathers its rows' share of the level's own
-        // slots, the level's visits ride beside (IPO_HIP_LEVEL_FUSE=0: off)
-        lvl_fused_.assign(plan_.nlevels, 0);
-        const char* lf = std::getenv("IPO_HIP_LEVEL_FUSE");
-        if (visits_ && use_panel_ && !xch_ && (!lf || std::atoi(lf) != 0)) {
-            std::vector<int> ufirst(plan_.nsup, -1);
-            for (int u = nu - 1; u >= 0; u--) ufirst[plan_.unit_sup[u]] = u;
-            std::vector<int4> frng(h_fu_sup_.size(), make_int4(0, 0, 0, 0)), lv;
-            lvis_ptr_.assign(plan_.nlevels + 1, 0);
-            for (int l = 1; l < plan_.nlevels; l++) {
-                const bool ok = ck_kind_[l] == 2 && small_ptr_[l + 1] == small_ptr_[l] && fu_ptr_[l + 1] > fu_ptr_[l];
-                if (ok) {
-                    lvl_fused_[l] = 1;
-                    for (int f = fu_ptr_[l]; f < fu_ptr_[l + 1]; f++) {
-                        const int sp = h_fu_sup_[f], j = h_fu_j_[f];
-                        const int nc = plan_.col0[sp + 1] - plan_.col0[sp];
-                        const int h = nc + plan_.rowptr[sp + 1] - plan_.rowptr[sp];
-                        const int u0 = ufirst[sp];
-                        int4 r = make_int4(late_b[u0], kptr_v[u0 + 1], 0, 0);
-                        if ((j + 1) * kTileRows < h) {
-                            const int u1 = u0 + j + 1;
-                            r.z = late_b[u1];
-                            r.w = kptr_v[u1 + 1];
-                        }
-                        frng[f] = r;
-                    }
-                    for (const int3& v : vis[l]) lv.push_back(make_int4(v.x, v.y, v.z, 0));
-                }
-                lvis_ptr_[l + 1] = static_cast<int>(lv.size());
-            }
-            if (lv.empty()) lv.push_back(make_int4(0, 0, 0, 0));
-            dfrng_.upload(frng.empty() ? std::vector<int4>{make_int4(0, 0, 0, 0)} : frng, s);
-            dlvis_.upload(lv, s);
-            IPO_HIP_CHECK(hipStreamSynchronize(s));
-        }
         dck_u_.upload(cu, s);
         dck_b_.upload(cb, s);
         dck_e_.upload(ce, s);
@@ -3082,13 +3043,6 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
     for (int l = 0; l < plan_.nlevels; l++) {
         const int u0 = plan_.unit_level_ptr[l], u1 = plan_.unit_level_ptr[l + 1];
         if (u1 <= u0) continue;
-        if (fused && lvl_fused_[l]) {      // gather + panel + visits of a chain level in one launch
-            ph_begin(s);
-            launch_level(pv, dslot_rec_.get(), dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], fu_ptr_[l + 1] - fu_ptr_[l],
-                         dfrng_.get(), dlvis_.get(), lvis_ptr_[l], lvis_ptr_[l + 1] - lvis_ptr_[l], tv, s);
-            ph_end(kPhDiag, 1, s);
-            continue;
-        }
         if (l > 0) {
             ph_begin(s);
             const int nl = launch_gather(pv, tv, -1, l, s);

@@ -77,13 +77,6 @@ void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, doubl
 size_t tail_dep_state_doubles(int ntb);
 // Block t's update of block column t + 1 alone.
 void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, hipStream_t s);
-// Deep trees' chain levels in one launch (k_level): fused panel units
-// [f0, f0 + nfu), each applying its rows' share of the level's own gather
-// first (frng[f]: slot ranges of the diagonal unit and of tile j + 1's unit
-// in recs), beside the level's visits vis[v0 .. v0 + nv) = {unit, slot
-// begin, slot end, -}, two per workgroup.
-void launch_level(const PlanView& pv, const SlotRec* recs, const int* fu_sup, const int* fu_j, int f0, int nfu,
-                  const int4* frng, const int4* vis, int v0, int nv, const TailView& tv, hipStream_t s);
 // Fused panel of supernodes sups[q0 .. q0+count) that have at most 16
 // columns and 64 rows (one wave each, k_panel_s); same bail-out contract.
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s);

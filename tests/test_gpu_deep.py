@@ -1,9 +1,8 @@
 """The deep-tree schedule of the sparse factorisation (kkt_device.hip):
 gather slots of finished descendants as "visits" in the launches of lower
 levels (on by default from kkt_plan.h kVisitLevels levels up, BASELINE
-configs[3]: 2,785 levels), the quadrant / flat gather kernels, the fused
-chain-level launch (k_level), the forward pre-pass and the one-wave leaf
-sweeps.  Netlib problems are shallow, so the schedule is forced
+configs[3]: 2,785 levels), the flat gather kernel (k_update_flat) and the
+one-wave leaf sweeps.  Netlib problems are shallow, so the schedule is forced
 here (IPO_HIP_VISITS=1, read when a factor object is built) and held to the
 same bars as the default schedule: pivots and refined solutions against the
 oracle (test_gpu_kkt's tolerances), HSD traces against the golden ones
@@ -87,21 +86,6 @@ def test_flat_gather_bitwise(name):
             b = factor_solve(p, E, D, fy, fx)
         for u, v in zip(a, b):
             assert np.array_equal(np.asarray(u), np.asarray(v)), (name, visits)
-
-
-@pytest.mark.parametrize("name", ["afiro", "25fv47", "d6cube", "pds-02", "ship04s"])
-def test_fused_levels_bitwise(name):
-    """One launch per chain level (k_level: the panel workgroups gather their
-    rows' share of the level's own slots, the level's visits beside) gives
-    the separate quadrant-gather + panel launches' factor bit for bit."""
-    p = ipo_amd.load_mps(mps_path(name))
-    E, D, fy, fx = system(p)
-    with env(IPO_HIP_VISITS=1, IPO_HIP_LEVEL_FUSE=0):
-        a = factor_solve(p, E, D, fy, fx)
-    with env(IPO_HIP_VISITS=1, IPO_HIP_LEVEL_FUSE=1):
-        b = factor_solve(p, E, D, fy, fx)
-    for u, v in zip(a, b):
-        assert np.array_equal(np.asarray(u), np.asarray(v)), name
 
 
 @pytest.mark.parametrize("name", [n for n in ["afiro", "adlittle", "sc205", "israel", "scfxm2", "ship08s", "sctap1", "agg"]
