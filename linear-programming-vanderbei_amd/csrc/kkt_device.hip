@@ -2495,7 +2495,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         ck_ptr_.assign(plan_.nlevels + 2, 0);
         sp_ptr_.assign(plan_.nlevels + 2, 0);
         size_t max_part = 0;
-        const int wg_target = 512, min_chunk = 64;     // 64: measured best of 16-256 on configs[3] and dfl001
+        const int wg_target = 512;
+        int min_chunk = 64;     // 64: measured best of 16-256 on configs[3] and dfl001 (IPO_HIP_MIN_CHUNK)
+        if (const char* e = std::getenv("IPO_HIP_MIN_CHUNK")) min_chunk = std::max(kSlab, std::atoi(e) / kSlab * kSlab);
         // units [u0, u1), slots [kbeg(u), kend(u)) each, then the group's visits
         // a sparse unit's 32 x 32 quadrants that hold lower-triangle entries (k_update_quad)
         auto quadrants = [&](int u, int kb, int ke) {
