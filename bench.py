@@ -53,8 +53,8 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 METRIC = "IPM iterations/sec (ADA^T factor+solve) on netlib dfl001; duality gap ≤1e-8"
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, AMD spec (the guide has no fp64 row)
 PHASE_KERNELS = {"gather": "k_update|k_update_flat|k_update_quad",
-                 "diag": "k_panel_w|k_panel_s|k_tail_pr|k_diag", "trsm": "k_trsm",
-                 "tail_syrk": "k_tail_syrk",
+                 "diag": "k_panel_w|k_panel_s|k_diag", "trsm": "k_trsm",
+                 "tail_syrk": "k_tail_syrk", "tail": "k_tail_pr|k_tail_col|k_tail_dep",
                  "forward": "k_forward|k_fwd_leaf|k_fwd_diag|k_fwd_gemv|k_fwd_sf|k_tail_gather|k_tail_fwd|k_tail_fwd_chain",
                  "backward": "k_backward|k_bwd_leaf|k_bwd_partial|k_bwd_finish|k_bwd_sf|k_tail_dscale|k_tail_bwd|"
                              "k_tail_bwd_chain"}
@@ -402,6 +402,10 @@ def main():
                             "gflop_per_s": flops / secs / 1e9, "gbyte_per_s": byts / secs / 1e9,
                             "flops_per_occurrence": st_t["phase_flops"][i], "bytes_per_occurrence": st_t["phase_bytes"][i],
                             "occurrences": cnt}
+        # the dominant kernel: the phase with the most device time; its work
+        # is priced once per factorisation (a dense-tail repair's relaunches
+        # add launches and time, not work): the dense tail at SURVEY.md 8(d)'s
+        # nt^3 / 3 flops of a dense factor
         top = max(phases, key=lambda k: phases[k]["ms_total"])
         ph = phases[top]
         i = ipo_amd.PHASES.index(top)
@@ -424,8 +428,11 @@ def main():
             roof["mfma_util"] = mf["phases"][top]["mfma_util"]
             roof["mfma_source"] = mf["source"]
         roof.update({"phase": top, "kernels": ph["kernels"], "avg_launch_us": ph["avg_launch_us"],
-                     "launches": ph["launches"], "algorithmic_flops_per_launch": flops_l,
-                     "algorithmic_bytes_per_launch": bytes_l, "share_of_timed_region": ph["share_of_timed_region"]})
+                     "launches": ph["launches"], "occurrences": st_t["phase_count"][i],
+                     "algorithmic_flops_per_occurrence": st_t["phase_flops"][i],
+                     "algorithmic_flops_per_launch": flops_l,
+                     "algorithmic_bytes_per_launch": bytes_l, "share_of_timed_region": ph["share_of_timed_region"],
+                     "tail_repairs": st_t["tail_repairs"], "tail_dep_rounds": st_t["tail_dep_rounds"]})
 
     out = {
         "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": d.world, "steps": args.steps,
@@ -445,6 +452,11 @@ def main():
                    "refine_passes": st["refine_passes"],
                    "phase_timing": "second identical solve with HIP events" if not args.no_timing else None},
         "roofline": roof,
+        # the whole IPM iteration against SURVEY.md 8(d)'s algorithmic work
+        # (narth + sweeps + SpMVs + vectors), over the timed region
+        "iteration_roofline": (dict(roofline_of(*survey_work(st, p.m, p.n, p.nz), elapsed / max(iters, 1)),
+                                    per="IPM iteration (SURVEY.md 8(d) algorithmic work), timed region")
+                               if iters else None),
         "phases": phases,
         "mfma_counters": pmc_mfma(),
         "cpu_baseline": None,

@@ -67,14 +67,19 @@ typedef struct {
     long   update_launches, panel_launches;
     double flops_update;     /* algorithmic flops of the gather kernel per factorisation */
     double bytes_update;     /* algorithmic bytes of the gather kernel per factorisation */
-    /* per phase (timing mode): 0 gather (k_update + k_update_reduce), 1 diagonal
-     * block LDL' (k_diag), 2 panel solve (k_trsm), 3 dense-tail trailing update
-     * (k_tail_syrk), 4 forward sweep, 5 backward sweep */
-    double phase_ms[6];      /* device time (HIP events on the solver's stream)      */
-    long   phase_launches[6];/* kernel launches                                       */
-    long   phase_count[6];   /* occurrences (factorisations / sweeps)                 */
-    double phase_flops[6];   /* algorithmic flops of one occurrence                   */
-    double phase_bytes[6];   /* algorithmic bytes of one occurrence                   */
+    /* per phase (timing mode): 0 gather (k_update*), 1 sparse panels (k_panel_w /
+     * k_panel_s, or k_diag), 2 panel solve (k_trsm), 3 dense-tail trailing update
+     * of the per-phase path (k_tail_syrk), 4 forward sweep, 5 backward sweep,
+     * 6 dense-tail factor of the look-ahead path (k_tail_pr with its visits, and
+     * the repair launches k_tail_col / k_tail_dep), 7 unused */
+    double phase_ms[8];      /* device time (HIP events on the solver's stream)      */
+    long   phase_launches[8];/* kernel launches                                       */
+    long   phase_count[8];   /* occurrences: factorisations (each counted once, its
+                              * dense-tail repairs included) / substitution sweeps    */
+    double phase_flops[8];   /* algorithmic flops of one occurrence                   */
+    double phase_bytes[8];   /* algorithmic bytes of one occurrence                   */
+    long   tail_repairs;     /* dense-tail block columns redone after a bail-out      */
+    long   tail_dep_rounds;  /* k_tail_dep launches of those repairs                  */
 } ipo_hip_stats;
 
 /* method: 0 = hsd, 1 = intpt, 2 = hsdls.  trace may be NULL (silent).  timing != 0

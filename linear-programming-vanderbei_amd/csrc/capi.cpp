@@ -82,6 +82,9 @@ void fill_stats(ipo_hip_stats* st, const ipo::IpmResult& r, const ipo::KktDevice
     st->update_launches = r.kkt.phase_launches[ipo::kPhGather];
     st->panel_launches = r.kkt.phase_launches[ipo::kPhDiag] + r.kkt.phase_launches[ipo::kPhTrsm] +
                          r.kkt.phase_launches[ipo::kPhSyrk];
+    st->tail_repairs = r.kkt.tail_repairs;
+    st->tail_dep_rounds = r.kkt.tail_dep_rounds;
+    static_assert(ipo::kNumPhases <= 8, "ipo_hip_stats holds 8 phases");
     for (int ph = 0; ph < ipo::kNumPhases; ph++) {
         st->phase_ms[ph] = r.kkt.phase_ms[ph];
         st->phase_launches[ph] = r.kkt.phase_launches[ph];

@@ -347,11 +347,18 @@ k_trsm(PlanView p, int u0, TailView tv, int kb) {
 // the same decision: drop, or +-1e-8 by node class -- and goes on.  No grid
 // barrier, no co-residency assumption: one launch per dependent pivot.
 // State: st = B (PC x PC) | dv | lv | dsc | gmax[G]; sti = k0, 1 + pending
-// column (0: none), done, ndep.
+// column (0: none), done, ndep.  Two copies of each, selected by the round's
+// parity: round r reads copy r & 1 and writes copy (r + 1) & 1, so nothing a
+// launch reads is written in that launch (workgroups of one grid are not
+// ordered: a workgroup starting after workgroup 0 ended must still see the
+// round's input state, and the maxima of the pending column must not be
+// overwritten by those of the next failing column while a slower workgroup
+// still reduces them).
 constexpr int kDepState = PC * PC + 3 * PC;
 
 __global__ void __launch_bounds__(NT)
-k_tail_dep(PlanView p, TailView tv, int kb, double* __restrict__ st, int* __restrict__ sti) {
+k_tail_dep(PlanView p, TailView tv, int kb, const double* __restrict__ st_in, double* __restrict__ st_out,
+           const int* __restrict__ sti_in, int* __restrict__ sti_out) {
     __shared__ double B[PC][PC + 1];
     __shared__ double dv[PC];
     __shared__ int lv[PC];
@@ -366,9 +373,14 @@ k_tail_dep(PlanView p, TailView tv, int kb, double* __restrict__ st, int* __rest
     const int tid = threadIdx.x, tr = tid & 63, tp = tid >> 6, np = NT >> 6;
     const int row = nc + g * TR + tr;
     const bool rok = row < h;
-    if (sti[2]) return;           // the block column is done: a round enqueued past the end is a no-op
-    const int kstart = sti[0], pending = sti[1] - 1;
-    double* gmax = st + kDepState;
+    if (sti_in[2]) {              // the block column is done: a round enqueued past the end is a no-op
+        if (g == 0 && tid == 0) sti_out[2] = 1;
+        return;
+    }
+    const int kstart = sti_in[0], pending = sti_in[1] - 1;
+    const double* gmax_in = st_in + kDepState;
+    double* gmax_out = st_out + kDepState;
+    const double* st = st_in;
     if (kstart == 0) {
         for (int c = tp; c < nc; c += np) B[tr][c] = (tr < nc && tr >= c) ? panel[tr + (size_t)c * ld] : 0.0;
         for (int k = tid; k < nc; k += NT) { dsc[k] = p.dscale[c0 + k]; dv[k] = 0.0; lv[k] = 1; }
@@ -388,7 +400,7 @@ k_tail_dep(PlanView p, TailView tv, int kb, double* __restrict__ st, int* __rest
         const double t = panel[ok ? row + (size_t)c * ld : 0];
         a[q] = ok ? t : 0.0;
     }
-    if (tid == 0) ndep_sh = kstart == 0 ? 0 : sti[3];
+    if (tid == 0) ndep_sh = kstart == 0 ? 0 : sti_in[3];
     __syncthreads();
 #pragma unroll
     for (int qk = 0; qk < 16; qk++) {
@@ -411,7 +423,7 @@ k_tail_dep(PlanView p, TailView tv, int kb, double* __restrict__ st, int* __rest
                     if (tid == 0) {
                         double m2 = red[0];
                         for (int q = 1; q < np; q++) m2 = ref_max(m2, red[q]);
-                        gmax[g] = m2;
+                        gmax_out[g] = m2;
                     }
                     if (rok) {
 #pragma unroll
@@ -421,18 +433,18 @@ k_tail_dep(PlanView p, TailView tv, int kb, double* __restrict__ st, int* __rest
                         }
                     }
                     if (g == 0) {
-                        for (int c = tp; c < nc; c += np) st[tr * PC + c] = B[tr][c];
+                        for (int c = tp; c < nc; c += np) st_out[tr * PC + c] = B[tr][c];
                         for (int kk = tid; kk < nc; kk += NT) {
-                            st[PC * PC + kk] = dv[kk];
-                            st[PC * PC + PC + kk] = lv[kk];
-                            st[PC * PC + 2 * PC + kk] = dsc[kk];
+                            st_out[PC * PC + kk] = dv[kk];
+                            st_out[PC * PC + PC + kk] = lv[kk];
+                            st_out[PC * PC + 2 * PC + kk] = dsc[kk];
                         }
-                        if (tid == 0) { sti[0] = k; sti[1] = k + 1; sti[3] = ndep_sh; }
+                        if (tid == 0) { sti_out[0] = k; sti_out[1] = k + 1; sti_out[2] = 0; sti_out[3] = ndep_sh; }
                     }
                     return;
                 }
-                double mx = gmax[0];
-                for (int q = 1; q < G; q++) mx = ref_max(mx, gmax[q]);
+                double mx = gmax_in[0];
+                for (int q = 1; q < G; q++) mx = ref_max(mx, gmax_in[q]);
                 if (mx < 1.0e+6 * 1.0e-8) alive = 0;
                 else dk = (p.sign[c0 + k] < 0 ? -1.0 : 1.0) * 1.0e-8;
                 if (tid == 0) ndep_sh++;
@@ -478,7 +490,7 @@ k_tail_dep(PlanView p, TailView tv, int kb, double* __restrict__ st, int* __rest
     for (int k = tid; k < nc; k += NT) { p.dg[c0 + k] = dv[k]; p.live[c0 + k] = lv[k]; }
     if (tid == 0) {
         if (ndep_sh) atomicAdd(&p.flags[0], ndep_sh);
-        sti[2] = 1;
+        sti_out[2] = 1;
     }
 }
 
@@ -1250,10 +1262,14 @@ int tail_dep_tiles(const TailView& tv, int kb) {
     return std::max(1, (below + TR - 1) / TR);
 }
 
-size_t tail_dep_state_doubles(int ntb) { return kDepState + static_cast<size_t>(std::max(1, ntb)); }
+size_t tail_dep_state_doubles(int ntb) { return 2 * (kDepState + static_cast<size_t>(std::max(1, ntb))); }
 
-void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, double* st, int* sti, hipStream_t s) {
-    hipLaunchKernelGGL(k_tail_dep, dim3(tail_dep_tiles(tv, kb)), dim3(NT), 0, s, pv, tv, kb, st, sti);
+void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, int round, double* st, int* sti,
+                           hipStream_t s) {
+    const size_t half = tail_dep_state_doubles(tv.ntb) / 2;
+    const int in = round & 1, out = in ^ 1;
+    hipLaunchKernelGGL(k_tail_dep, dim3(tail_dep_tiles(tv, kb)), dim3(NT), 0, s, pv, tv, kb, st + in * half,
+                       st + out * half, sti + 4 * in, sti + 4 * out);
 }
 
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s) {

@@ -31,7 +31,8 @@ struct TailView {
 
 // Device-time phases of the KKT core (timing mode), with the algorithmic
 // work of one occurrence (one factorisation / one substitution sweep).
-enum KktPhase { kPhGather = 0, kPhDiag, kPhTrsm, kPhSyrk, kPhForward, kPhBackward, kNumPhases };
+// kPhTail: the look-ahead dense-tail factor (k_tail_pr and its repair launches).
+enum KktPhase { kPhGather = 0, kPhDiag, kPhTrsm, kPhSyrk, kPhForward, kPhBackward, kPhTail, kNumPhases };
 
 struct KktTimers {
     double phase_ms[kNumPhases] = {};       // accumulated device time per phase

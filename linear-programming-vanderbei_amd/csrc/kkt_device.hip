@@ -2623,6 +2623,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             lxs += (nc + hb) * nc;
             gb += 16.0 * (nc + hb) * nc;      // read-modify-write of every target panel
         }
+        const double sdf = df, sdb = db, stf = tf, stb = tb;     // sparse panels alone
         for (int kb = 0; kb < P.ntb; kb++) {
             const double nc = std::min(kPanelCols, P.nt - kb * kPanelCols), below = P.nt - kb * kPanelCols - nc;
             df += 2.0 * nc * nc * nc / 3.0;
@@ -2638,13 +2639,16 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         work_flops[kPhDiag] = df; work_bytes[kPhDiag] = db;
         work_flops[kPhTrsm] = tf; work_bytes[kPhTrsm] = tb;
         work_flops[kPhSyrk] = sf; work_bytes[kPhSyrk] = sb;
-        if (use_panel_) {   // k_panel_w does both: the diag phase carries the trsm work,
-            // and k_tail_pr the tail's trailing update (its visits)
-            double vf = 0, vb = 0;
-            if (P.ntb > 0) tail_visit_work(P.ntb, P.nt, vf, vb);
-            work_flops[kPhDiag] += tf + vf; work_bytes[kPhDiag] += tb + vb;
+        if (use_panel_) {   // k_panel_w does both: the diag phase carries the sparse trsm work;
+            // the dense tail is its own phase (k_tail_pr: panels + deferred
+            // trailing updates), priced as SURVEY.md 8(d) prices a dense
+            // factor: nt^3 / 3 flops, its lower triangle read and written once
+            work_flops[kPhDiag] = sdf + stf; work_bytes[kPhDiag] = sdb + stb;
             work_flops[kPhTrsm] = work_bytes[kPhTrsm] = 0;
             work_flops[kPhSyrk] = work_bytes[kPhSyrk] = 0;
+            const double nt = P.nt;
+            work_flops[kPhTail] = nt * nt * nt / 3.0;
+            work_bytes[kPhTail] = 16.0 * 0.5 * nt * (nt + 1.0);
         }
         // a sweep reads every factor entry once (sparse panels + the tail's
         // lower triangle) and the vector / update values it touches
@@ -2701,7 +2705,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dtail_tasks_.upload(reinterpret_cast<const uint64_t*>(plan_.tail_tasks.data()), plan_.tail_tasks.size() * 4, s);
         dW_.alloc(static_cast<size_t>(plan_.nt) * kPanelCols);   // W = L21 D of one block column (per-phase path)
         dDepSt_.alloc(tail_dep_state_doubles(plan_.ntb));
-        dDepI_.alloc(4);
+        dDepI_.alloc(8);
         dChainGran_.alloc(static_cast<size_t>(plan_.ntb) * 2 * 128);     // R <= 2 right-hand sides
         IPO_HIP_CHECK(hipMemsetAsync(dChainGran_.get(), 0, dChainGran_.bytes(), s));
         if (plan_.ntb <= kChainMaxBlocks) {
@@ -3023,6 +3027,10 @@ void KktDevice::factor_core(const double* dE, const double* dD) {
         else if (!factor_pass(dE, dD, false, repair) && repair && hFlags_[1] == 4 && hFlags_[4] > 0) repair_tail();
     }
     tm_.factors++;
+    // one occurrence per factorisation, whatever redos and repairs it took
+    // (their launches and time stay in the phases: the work is priced once)
+    if (timing_)
+        for (int ph : {kPhGather, kPhDiag, kPhTrsm, kPhSyrk, kPhTail}) tm_.phase_count[ph]++;
     ndep_ = xch_ ? static_cast<int>(hScal_[1]) : hFlags_[0];
     if (-hScal_[0] < 1.0e-14) epsdiag_ *= 10;
 }
@@ -3076,7 +3084,7 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
             for (int t = 0; t < plan_.ntb; t++) {
                 ph_begin(s);
                 launch_tail_step(pv, tv, t, s);
-                ph_end(kPhDiag, 1, s);
+                ph_end(kPhTail, 1, s);
             }
         } else
         for (int kb = 0; kb < plan_.ntb; kb++) {
@@ -3148,7 +3156,6 @@ bool KktDevice::finish_pass(bool fused) {
         IPO_HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
         tm_.factor_ms += ms;
         ph_collect();
-        for (int ph : {kPhGather, kPhDiag, kPhTrsm, kPhSyrk}) tm_.phase_count[ph]++;
     }
     const bool bail = xch_ ? hScal_[2] > 0 : hFlags_[1] != 0;
     return !(fused && bail);
@@ -3174,18 +3181,22 @@ void KktDevice::repair_tail() {
         TailView tv = tail_view();
         ph_begin(s);
         if (tb > 0) launch_tail_colupdate(pv, tv, tb - 1, s);
-        ph_end(kPhSyrk, tb > 0, s);
+        ph_end(kPhTail, tb > 0, s);
         // block column tb with the dependent-pivot rule, one round per dependent pivot
-        IPO_HIP_CHECK(hipMemsetAsync(dDepI_.get(), 0, 4 * sizeof(int), s));
+        IPO_HIP_CHECK(hipMemsetAsync(dDepI_.get(), 0, 8 * sizeof(int), s));
         // rounds enqueued kDepBatch at a time (a round after the last is a
-        // no-op), one host read-back per batch instead of per round
+        // no-op), one host read-back per batch instead of per round; round r
+        // writes state copy (r + 1) & 1, so the batch's last round wrote
+        // copy (r + kDepBatch) & 1
         constexpr int kDepBatch = 4;
         for (int r = 0;; r += kDepBatch) {
             if (r > kPanelCols + 1) throw std::runtime_error("kkt: dense-tail dependent-pivot rounds did not finish");
             ph_begin(s);
-            for (int b = 0; b < kDepBatch; b++) launch_tail_dep_round(pv, tv, tb, dDepSt_.get(), dDepI_.get(), s);
-            ph_end(kPhDiag, kDepBatch, s);
-            IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 6, dDepI_.get() + 2, sizeof(int), hipMemcpyDeviceToHost, s));
+            for (int b = 0; b < kDepBatch; b++)
+                launch_tail_dep_round(pv, tv, tb, r + b, dDepSt_.get(), dDepI_.get(), s);
+            ph_end(kPhTail, kDepBatch, s);
+            IPO_HIP_CHECK(hipMemcpyAsync(hFlags_ + 6, dDepI_.get() + 4 * ((r + kDepBatch) & 1) + 2, sizeof(int),
+                                         hipMemcpyDeviceToHost, s));
             IPO_HIP_CHECK(hipStreamSynchronize(s));
             tm_.tail_dep_rounds += kDepBatch;
             if (hFlags_[6]) break;
@@ -3193,7 +3204,7 @@ void KktDevice::repair_tail() {
         for (int t = tb + 1; t < plan_.ntb; t++) {
             ph_begin(s);
             launch_tail_step(pv, tail_view(), t, s);
-            ph_end(kPhDiag, 1, s);
+            ph_end(kPhTail, 1, s);
         }
         if (finish_pass(true)) break;
         if (hFlags_[1] != 4 || hFlags_[4] - 1 <= tb)   // cannot happen: a later tail column or nothing

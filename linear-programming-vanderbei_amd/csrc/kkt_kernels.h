@@ -70,10 +70,12 @@ int tail_visit_tiles(int ntb, int t);
 // algorithmic flops / bytes of every visit of one factorisation
 void tail_visit_work(int ntb, int nt, double& flops, double& bytes);
 // Repair path, block column kb of the dense tail with the dependent-pivot
-// rule: one round (k_tail_dep); sti = {k0, 1 + pending column, done, ndep},
-// zeroed before the first round; rounds until sti[2] (one per dependent
-// pivot).  st: tail_dep_state_doubles(ntb).
-void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, double* st, int* sti, hipStream_t s);
+// rule: one round (k_tail_dep); sti = two copies of {k0, 1 + pending column,
+// done, ndep}, both zeroed before round 0; round r reads copy r & 1 and
+// writes copy (r + 1) & 1, rounds until the written copy's done flag (one
+// round per dependent pivot + 1).  st: tail_dep_state_doubles(ntb) (two copies).
+void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, int round, double* st, int* sti,
+                           hipStream_t s);
 size_t tail_dep_state_doubles(int ntb);
 // Block t's update of block column t + 1 alone.
 void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, hipStream_t s);

@@ -52,6 +52,33 @@ struct KktOrdering {
 KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
                                     const int* kAt, const int* iAt, int nforced = 0);
 
+// Nested dissection (kkt_order_nd.cpp; not in the reference): the
+// elimination order used instead of the reference's on problems of at least
+// kNdMinNodes KKT nodes (every netlib problem is below: ken-11 has 72,086),
+// whose minimum-degree trees are thousands of levels deep on banded LPs.
+// perm[new] = old; forced rows last in natural order as above.  Pieces of
+// at most leaf_rows y-nodes are ordered x-nodes first, then y-nodes.
+std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
+                                        int nforced, int leaf_rows);
+// The symbolic factor (Lp, Li, iperm) of o.perm over the free nodes; forced
+// rows get empty columns (add the dense tail after).
+void symbolic_from_perm(KktOrdering& o, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced);
+// Pad chains of columns (parent(j) = j + 1) below column tc into panels of
+// at most kPanelCols columns holding at most zfrac explicit zeros (relaxed
+// supernodes; the padded entries stay exact zeros in the factor).
+void relax_supernodes(KktOrdering& o, int tc, double zfrac);
+// nested dissection, Lp/Li, forced tail, relaxed supernodes, narth (of the
+// unpadded pattern): the KktOrdering of that order
+KktOrdering order_nested_dissection(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
+                                    int nforced, int leaf_rows, double zfrac);
+constexpr int kNdMinNodes = 100000;
+constexpr int kNdDense = 64;         // smallest degree of a dense node (also > 10x its class mean)
+constexpr int kNdLeafRows = 1024;   // measured on configs[3]: 4.5e10 factor flops, 62 levels (256: 5.5e10, 61)
+constexpr double kNdRelax = 0.1;      // explicit-zero fraction of a relaxed panel
+// Which order build_kkt_plan uses: IPO_HIP_ORDER = md | nd | auto (default:
+// nd from kNdMinNodes KKT nodes up); true = nested dissection
+bool use_nested_dissection(int T);
+
 // One gather task into a 64x64 tile of the dense tail: the tail rows of
 // source panel `src` whose positions inside the tile's row block (rmask)
 // and column block (cmask) are given as bit masks; R_src indices start at

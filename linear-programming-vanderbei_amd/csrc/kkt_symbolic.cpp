@@ -8,6 +8,8 @@
 #include <iterator>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 
 namespace ipo {
@@ -103,6 +105,34 @@ void add_forced_tail(KktOrdering& o, int m, const int* kA, const int* iA, int nf
 }
 
 }  // namespace
+
+KktOrdering order_nested_dissection(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
+                                    int nforced, int leaf_rows, double zfrac) {
+    KktOrdering o;
+    o.m = m; o.n = n; o.T = m + n;
+    o.perm = nested_dissection_perm(m, n, kA, iA, kAt, iAt, nforced, leaf_rows);
+    symbolic_from_perm(o, kA, iA, kAt, iAt, nforced);
+    const int T = o.T;
+    if (nforced > 0) {
+        add_forced_tail(o, m, kA, iA, nforced);
+    } else {
+        int tc = T;
+        while (tc > 0 && o.Lp[tc] - o.Lp[tc - 1] == T - tc) tc--;
+        o.denwin = tc;
+    }
+    double na = 0.0;
+    for (int v = 0; v < T; v++) { double c = o.Lp[v + 1] - o.Lp[v]; na += c * c; }
+    o.narth = na + 3.0 * o.Lp[T] + T;
+    relax_supernodes(o, nforced > 0 ? T - nforced : o.denwin, zfrac);
+    return o;
+}
+
+bool use_nested_dissection(int T) {
+    const char* e = std::getenv("IPO_HIP_ORDER");
+    if (e && !std::strcmp(e, "md")) return false;
+    if (e && !std::strcmp(e, "nd")) return true;
+    return T >= kNdMinNodes;
+}
 
 KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
                                     const int* kAt, const int* iAt, int nforced) {
@@ -318,7 +348,12 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
 
 KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced,
                        double tail_density) {
-    KktOrdering o = order_tiered_min_degree(m, n, kA, iA, kAt, iAt, nforced);
+    int leaf = kNdLeafRows;
+    if (const char* e = std::getenv("IPO_HIP_ND_LEAF")) leaf = std::max(1, std::atoi(e));
+    double relax = kNdRelax;
+    if (const char* e = std::getenv("IPO_HIP_ND_RELAX")) relax = std::atof(e);
+    KktOrdering o = use_nested_dissection(m + n) ? order_nested_dissection(m, n, kA, iA, kAt, iAt, nforced, leaf, relax)
+                                                 : order_tiered_min_degree(m, n, kA, iA, kAt, iAt, nforced);
     KktPlan P;
     P.m = m; P.n = n; P.T = o.T;
     const int T = o.T;

@@ -49,8 +49,9 @@ class Stats(C.Structure):
         ("update_ms", C.c_double), ("panel_ms", C.c_double), ("sweep_ms", C.c_double),
         ("update_launches", C.c_long), ("panel_launches", C.c_long),
         ("flops_update", C.c_double), ("bytes_update", C.c_double),
-        ("phase_ms", C.c_double * 6), ("phase_launches", C.c_long * 6), ("phase_count", C.c_long * 6),
-        ("phase_flops", C.c_double * 6), ("phase_bytes", C.c_double * 6),
+        ("phase_ms", C.c_double * 8), ("phase_launches", C.c_long * 8), ("phase_count", C.c_long * 8),
+        ("phase_flops", C.c_double * 8), ("phase_bytes", C.c_double * 8),
+        ("tail_repairs", C.c_long), ("tail_dep_rounds", C.c_long),
     ]
 
     def as_dict(self) -> dict:
@@ -64,7 +65,7 @@ class Stats(C.Structure):
 _lib = None
 _libc = None
 
-PHASES = ["gather", "diag", "trsm", "tail_syrk", "forward", "backward"]
+PHASES = ["gather", "diag", "trsm", "tail_syrk", "forward", "backward", "tail", "unused"]
 
 EXPORTED = [
     "solver", "ldltfac", "forwardbackward", "inv_clo",

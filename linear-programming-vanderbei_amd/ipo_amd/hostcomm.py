@@ -66,6 +66,7 @@ class HostComm:
             peers = {}
             while len(peers) < self.world - 1:
                 c, _ = srv.accept()
+                c.settimeout(None)    # the timeout bounds the rendezvous, not later collectives
                 c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                 (r,) = struct.unpack("<i", _recv(c, 4))
                 peers[r] = c
@@ -81,6 +82,10 @@ class HostComm:
                     if time.time() - t0 > timeout:
                         raise
                     time.sleep(0.05)
+            # the connect timeout must not stay on the socket: a collective in
+            # which rank 0 is busy longer (setup of a large LP, rank-0-only
+            # bench legs) would raise socket.timeout here
+            s.settimeout(None)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             s.sendall(struct.pack("<i", self.rank))
             self.sock = s

@@ -395,9 +395,19 @@ static void numeric_ldlt(orc_kkt *K)
 void orc_kkt_factor(orc_kkt *K, const double *E, const double *D)
 {
     static int fcount = 0;
-    if (getenv("ORC_DUMP_ED")) {   /* debug: capture (E, D) of factorisation #N */
-        if (fcount == atoi(getenv("ORC_DUMP_ED"))) {
-            FILE *f = fopen("/tmp/orc_ed.bin", "wb");
+    if (getenv("ORC_DUMP_ED")) {   /* debug: capture (E, D) of factorisations #N1,N2,... */
+        int hit = 0;
+        for (const char *q = getenv("ORC_DUMP_ED"); *q;) {
+            char *e;
+            long v = strtol(q, &e, 10);
+            if (e == q) break;
+            if (v == fcount) hit = 1;
+            q = *e == ',' ? e + 1 : e;
+        }
+        if (hit) {
+            char fn[64];
+            snprintf(fn, sizeof fn, "/tmp/orc_ed_%d.bin", fcount);
+            FILE *f = fopen(fn, "wb");
             fwrite(&K->m, sizeof(int), 1, f); fwrite(&K->n, sizeof(int), 1, f);
             fwrite(E, sizeof(double), (size_t)K->m, f); fwrite(D, sizeof(double), (size_t)K->n, f);
             fwrite(&K->epsdiag, sizeof(double), 1, f);

@@ -5,9 +5,12 @@
 // explicit zeros).
 //   g++ -O2 -std=c++17 -I linear-programming-vanderbei_amd/csrc tools/plan_levels.cpp \
 //       linear-programming-vanderbei_amd/csrc/kkt_symbolic.cpp linear-programming-vanderbei_amd/csrc/lp_io.cpp \
-//       linear-programming-vanderbei_amd/csrc/synth.cpp -o tools/plan_levels
+//       linear-programming-vanderbei_amd/csrc/kkt_order_nd.cpp linear-programming-vanderbei_amd/csrc/synth.cpp \
+//       -o tools/plan_levels -lz
+//   (the order is build_kkt_plan's: IPO_HIP_ORDER=md|nd|auto, IPO_HIP_ND_LEAF)
 //   tools/plan_levels banded 200000 1000000 256      |  tools/plan_levels mps file.mps.gz
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -97,15 +100,25 @@ int main(int argc, char** argv) {
     std::vector<int> kAt, iAt;
     std::vector<double> A(iA.size(), 1.0), At;
     csc_transpose(m, n, kA.data(), iA.data(), A.data(), kAt, iAt, At);
-    KktOrdering o = order_tiered_min_degree(m, n, kA.data(), iA.data(), kAt.data(), iAt.data());
+    const bool nd = use_nested_dissection(m + n);
+    int leaf = kNdLeafRows;
+    if (const char* e = std::getenv("IPO_HIP_ND_LEAF")) leaf = std::atoi(e);
+    auto t0 = std::chrono::steady_clock::now();
+    KktOrdering o = nd ? order_nested_dissection(m, n, kA.data(), iA.data(), kAt.data(), iAt.data(), 0, leaf, std::getenv("IPO_HIP_ND_RELAX") ? std::atof(std::getenv("IPO_HIP_ND_RELAX")) : kNdRelax)
+                       : order_tiered_min_degree(m, n, kA.data(), iA.data(), kAt.data(), iAt.data());
+    std::printf("%s ordering %.2f s, narth %.3g\n", nd ? "nested-dissection" : "minimum-degree",
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), o.narth);
     int tc = o.T;
     while (tc > 0 && o.Lp[tc] - o.Lp[tc - 1] == o.T - tc) tc--;
     std::printf("m %d n %d T %d lnz %d dense window %d\n", m, n, o.T, o.Lp[o.T], o.T - tc);
     const double zf[] = {0.0, 0.05, 0.1, 0.2, 0.3};
     for (double z : zf) levels_of(o, tc, z, 64);
     if (argc > 5 || (argc > 1 && !std::strcmp(argv[1], "mps"))) {
+        t0 = std::chrono::steady_clock::now();
         KktPlan P = build_kkt_plan(m, n, kA.data(), iA.data(), kAt.data(), iAt.data(), 0, kTailDensity);
-        std::printf("plan: nsup %d levels %d nt %d\n", P.nsup, P.nlevels, P.nt);
+        std::printf("plan: nsup %d levels %d nt %d lnz %lld flops %.3g (%.2f s)\n", P.nsup, P.nlevels, P.nt,
+                    (long long)P.lnz, P.flops_factor,
+                    std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
         // per level: units, slots, slots whose source is on the level just below
         long tot = 0, recent = 0;
         for (int l = 1; l < P.nlevels; l++) {

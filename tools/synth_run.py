@@ -1,5 +1,7 @@
 """Developer tool: solve a synthetic LP on the GPU and print timing/plan stats.
-usage: python tools/synth_run.py random M N BAND [method] | blockang K MB NB L LNZ [method]"""
+usage: python tools/synth_run.py random M N BAND [method] | blockang K MB NB L LNZ [method] [shard]
+(shard: the block-angular LP as one shard of a 1-rank ShardContext -- linking rows forced into the tail,
+as bench.py's block_angular leg runs it)"""
 import json
 import os
 import sys
@@ -17,11 +19,11 @@ if kind == "random":
     p = ipo_amd.synth_random(m, n, 4, band)
 else:
     K, mb, nb, l, lnz = map(int, sys.argv[2:7])
-    method = sys.argv[7] if len(sys.argv) > 7 else "hsd"
+    method = sys.argv[7] if len(sys.argv) > 7 and sys.argv[7] != "shard" else "hsd"
     p = ipo_amd.synth_block_angular(K, mb, nb, 4, 256, l, lnz)
 print(f"generated m={p.m} n={p.n} nz={p.nz} in {time.time()-t0:.1f}s", flush=True)
 t0 = time.time()
-ctx = ipo_amd.Context(p)
+ctx = ipo_amd.Context(p) if "shard" not in sys.argv[2:] else ipo_amd.ShardContext(ipo_amd.shard_block_angular(p, 1, 0))
 print(f"setup {ctx.setup_seconds:.1f}s (wall {time.time()-t0:.1f}s)", flush=True)
 for timing in (False, True):
     t0 = time.time()
