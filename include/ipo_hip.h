@@ -43,8 +43,18 @@ int solver(int m, int n, int nz, int *iA, int *kA, double *A, double *b, double 
 void ldltfac(int m, int n, int *kA, int *iA, double *A, double *dn, double *dm,
              int *kAt, int *iAt, double *At, int verbose);
 void forwardbackward(double *Dn, double *Dm, double *dx, double *dy);
-/* releases the LU plug-in state (ldlt.c:507-513) */
+/* releases the LU plug-in state (ldlt.c:507-513), and a Q block set below */
 void inv_clo(void);
+/* The Q block of the reference's K (ldlt.c:178-185, 253-256, 391-394), for a
+ * caller of the LU plug-in that has one (the reference's inv_num reads it
+ * from lp->Q / kQ / iQ / max; ipo's own solvers never set it, ldlt.c:142-144):
+ * call before the first ldltfac (or after inv_clo).  Q is ldltfac's n x n,
+ * full symmetric CSC (both triangles and the diagonal, rows sorted in each
+ * column, as iolp.c:733-793 stores QUADS); it joins the block of dn:
+ * K = [ -(dn + max Q)  A' ; A  dm ], and the refinement residual carries
+ * max Q dx.  max = lp->max (-1 maximise, 1 minimise).  kQ == NULL removes it.
+ * Returns 0, or -1 after ldltfac (ipo_hip_last_error). */
+int ipo_hip_ldlt_set_q(int n, const int *kQ, const int *iQ, const double *Q, int max);
 
 /* ---- extended interface (not in the reference) ---------------------------- */
 typedef struct {
@@ -155,6 +165,13 @@ int ipo_hip_mps_load(const char *path, int *m, int *n, int *nz, int *kA, int *iA
 int ipo_hip_write_sol(const char *path, int flags, const double *x, const double *y, const double *z,
                       const char *solfile);
 
+/* The QUADS section of an MPS file as the reference's reader keeps it
+ * (iolp.c:583-645, symmetrised iolp.c:733-793): n x n over the file's
+ * columns, both triangles and the nonzero diagonal, rows sorted in each
+ * column.  Pass kQ = NULL to query n and qnz (-1: no QUADS section).
+ * Returns 0 or the reader's error number (36: QUADS columns out of order). */
+int ipo_hip_mps_quads(const char *path, int *n, int *qnz, int *kQ, int *iQ, double *Q);
+
 /* ipo_hip_mps_load with the flags of ipo_hip_run_mps_ex. */
 int ipo_hip_mps_load_ex(const char *path, int flags, int *m, int *n, int *nz, int *kA, int *iA, double *A,
                         double *b, double *c, double *f);
@@ -162,6 +179,10 @@ int ipo_hip_mps_load_ex(const char *path, int flags, int *m, int *n, int *nz, in
 /* KKT factor handle: symbolic + device numeric LDL' of K(E, D) for tests. */
 typedef struct ipo_hip_kkt ipo_hip_kkt;
 ipo_hip_kkt *ipo_hip_kkt_create(int m, int n, const int *kA, const int *iA, const double *A);
+/* the same with a Q block on the y-nodes (K_yy = -max(E, eps) - qmax Q, the
+ * first block of ldlt.c's K; Q m x m full symmetric CSC), NULL kQ: none */
+ipo_hip_kkt *ipo_hip_kkt_create_q(int m, int n, const int *kA, const int *iA, const double *A, const int *kQ,
+                                  const int *iQ, const double *Q, int qmax);
 void   ipo_hip_kkt_destroy(ipo_hip_kkt *k);
 int    ipo_hip_kkt_factor(ipo_hip_kkt *k, const double *E, const double *D);
 int    ipo_hip_kkt_solve(ipo_hip_kkt *k, const double *E, const double *D, double *fy, double *fx);
@@ -177,6 +198,11 @@ void   ipo_hip_kkt_set_epsdiag(ipo_hip_kkt *k, double epsdiag);
 /* Host-only symbolic analysis (no GPU needed): reference ordering stats. */
 int ipo_hip_symbolic(int m, int n, const int *kA, const int *iA, int *perm, long *lnz, double *narth,
                      int *denwin, int *pdf, int *nsup, int *nlevels);
+/* ipo_hip_symbolic with a Q block on the y-nodes (ipo_hip_kkt_create_q's
+ * convention; kQ == NULL: none): the reference ordering of ldlt.c's K with
+ * Q (Q neighbours in the adjacency ldlt.c:729-745, separability ldlt.c:675-682). */
+int ipo_hip_symbolic_q(int m, int n, const int *kA, const int *iA, const int *kQ, const int *iQ, int *perm,
+                       long *lnz, double *narth, int *denwin, int *pdf, int *nsup, int *nlevels);
 /* Same with the last nforced rows (linking rows) forced to the end of the
  * order and forming the dense tail (block-angular sharding); colcount[T]
  * = strict-lower nonzeros per column of L in the new order. */

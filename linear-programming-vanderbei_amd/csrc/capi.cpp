@@ -140,6 +140,15 @@ struct LuState {
     ipo::DevBuf<double> E, D, fy, fx;
 };
 LuState* g_lu = nullptr;
+// the Q block attached to the LU plug-in before its first ldltfac
+// (ipo_hip_ldlt_set_q): what a caller of the reference's inv_num puts in
+// lp->Q / kQ / iQ / max (ldlt.c:178-185)
+struct LuQ {
+    std::vector<int> kQ, iQ;
+    std::vector<double> Q;
+    int qmax = 1;
+};
+std::unique_ptr<LuQ> g_lu_q;
 
 }  // namespace
 
@@ -354,6 +363,20 @@ int ipo_hip_mps_dims(const char* path, int* m0, int* n0, int* nz0, int* m, int* 
     return st;
 }
 
+int ipo_hip_mps_quads(const char* path, int* n, int* qnz, int* kQ, int* iQ, double* Q) {
+    ipo::MpsProblem p;
+    std::string err;
+    const int rc = ipo::read_mps(path, p, &err);
+    if (rc) { set_err(err); return rc; }
+    const int nq = p.kQ.empty() ? 0 : p.kQ.back();
+    if (n) *n = p.n;
+    if (qnz) *qnz = p.kQ.empty() ? -1 : nq;
+    if (kQ && !p.kQ.empty()) std::memcpy(kQ, p.kQ.data(), sizeof(int) * (p.n + 1));
+    if (iQ && nq) std::memcpy(iQ, p.iQ.data(), sizeof(int) * nq);
+    if (Q && nq) std::memcpy(Q, p.Q.data(), sizeof(double) * nq);
+    return 0;
+}
+
 int ipo_hip_write_sol(const char* path, int flags, const double* x, const double* y, const double* z,
                       const char* solfile) {
     ipo::MpsProblem p, q;
@@ -407,7 +430,16 @@ void ldltfac(int m, int n, int* kA, int* iA, double* A, double* dn, double* dm, 
             IPO_HIP_CHECK(hipStreamCreateWithFlags(&g_lu->stream, hipStreamNonBlocking));
             g_lu->ms = n;
             g_lu->ns = m;
-            g_lu->kkt = std::make_unique<ipo::KktDevice>(n, m, kAt, iAt, At, g_lu->stream);
+            ipo::QBlock qb;
+            if (g_lu_q) {
+                if (static_cast<int>(g_lu_q->kQ.size()) != n + 1)
+                    throw std::invalid_argument("ldltfac: the Q block's order is not ldltfac's n");
+                qb.kQ = g_lu_q->kQ.data();
+                qb.iQ = g_lu_q->iQ.data();
+                qb.Q = g_lu_q->Q.data();
+                qb.qmax = g_lu_q->qmax;
+            }
+            g_lu->kkt = std::make_unique<ipo::KktDevice>(n, m, kAt, iAt, At, g_lu->stream, 0, g_lu_q ? &qb : nullptr);
             g_lu->E.alloc(n > 0 ? n : 1);
             g_lu->fy.alloc(n > 0 ? n : 1);
             g_lu->D.alloc(m > 0 ? m : 1);
@@ -442,7 +474,20 @@ void forwardbackward(double* Dn, double* Dm, double* dx, double* dy) {
     }
 }
 
+int ipo_hip_ldlt_set_q(int n, const int* kQ, const int* iQ, const double* Q, int max) {
+    if (g_lu) { set_err("ipo_hip_ldlt_set_q after ldltfac (call inv_clo first)"); return -1; }
+    if (!kQ || n < 0) { g_lu_q.reset(); return 0; }
+    auto q = std::make_unique<LuQ>();
+    q->kQ.assign(kQ, kQ + n + 1);
+    q->iQ.assign(iQ, iQ + kQ[n]);
+    q->Q.assign(Q, Q + kQ[n]);
+    q->qmax = max;
+    g_lu_q = std::move(q);
+    return 0;
+}
+
 void inv_clo(void) {
+    g_lu_q.reset();
     if (!g_lu) return;
     g_lu->kkt.reset();
     if (g_lu->stream) (void)hipStreamDestroy(g_lu->stream);
@@ -452,12 +497,19 @@ void inv_clo(void) {
 
 // ---- KKT handle for tests
 ipo_hip_kkt* ipo_hip_kkt_create(int m, int n, const int* kA, const int* iA, const double* A) {
+    return ipo_hip_kkt_create_q(m, n, kA, iA, A, nullptr, nullptr, nullptr, 1);
+}
+
+ipo_hip_kkt* ipo_hip_kkt_create_q(int m, int n, const int* kA, const int* iA, const double* A, const int* kQ,
+                                  const int* iQ, const double* Q, int qmax) {
     try {
         auto* k = new ipo_hip_kkt();
         IPO_HIP_CHECK(hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking));
         k->m = m;
         k->n = n;
-        k->kkt = std::make_unique<ipo::KktDevice>(m, n, kA, iA, A, k->stream);
+        ipo::QBlock qb;
+        qb.kQ = kQ; qb.iQ = iQ; qb.Q = Q; qb.qmax = qmax;
+        k->kkt = std::make_unique<ipo::KktDevice>(m, n, kA, iA, A, k->stream, 0, kQ ? &qb : nullptr);
         k->E.alloc(m > 0 ? m : 1);
         k->fy.alloc(m > 0 ? m : 1);
         k->D.alloc(n > 0 ? n : 1);
@@ -540,11 +592,19 @@ int ipo_hip_kkt_pivots(const ipo_hip_kkt* k, double* d, int* live) {
 
 int ipo_hip_symbolic(int m, int n, const int* kA, const int* iA, int* perm, long* lnz, double* narth, int* denwin,
                      int* pdf, int* nsup, int* nlevels) {
+    return ipo_hip_symbolic_q(m, n, kA, iA, nullptr, nullptr, perm, lnz, narth, denwin, pdf, nsup, nlevels);
+}
+
+int ipo_hip_symbolic_q(int m, int n, const int* kA, const int* iA, const int* kQ, const int* iQ, int* perm, long* lnz,
+                       double* narth, int* denwin, int* pdf, int* nsup, int* nlevels) {
     try {
         std::vector<int> kat, iat;
         std::vector<double> at, a(kA[n], 1.0);
         ipo::csc_transpose(m, n, kA, iA, a.data(), kat, iat, at);
-        ipo::KktPlan P = ipo::build_kkt_plan(m, n, kA, iA, kat.data(), iat.data());
+        ipo::QPattern qp;
+        qp.kQ = kQ;
+        qp.iQ = iQ;
+        ipo::KktPlan P = ipo::build_kkt_plan(m, n, kA, iA, kat.data(), iat.data(), 0, 1.0, kQ ? &qp : nullptr);
         if (perm) std::memcpy(perm, P.perm.data(), sizeof(int) * P.T);
         if (lnz) *lnz = P.lnz;
         if (narth) *narth = P.narth;

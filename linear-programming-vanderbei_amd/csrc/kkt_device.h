@@ -48,6 +48,16 @@ struct KktTimers {
     long tail_dep_rounds = 0; // k_tail_dep launches of those repairs
 };
 
+// The Q block of ldlt.c's K (ldlt.c:253-256, 391-394) on the y-nodes:
+// K_yy = -max(E, eps) - qmax Q, Q m x m full symmetric CSC (kkt_plan.h
+// QPattern), qmax = the reference's lp->max (-1 max, 1 min).
+struct QBlock {
+    const int* kQ = nullptr;
+    const int* iQ = nullptr;
+    const double* Q = nullptr;
+    int qmax = 1;
+};
+
 class KktDevice {
   public:
     // A is the solver's m x n matrix (CSC).  The plan (ordering, supernodes)
@@ -56,7 +66,9 @@ class KktDevice {
     // shard) form the dense tail (kkt_plan.h); with an Exchange set, the
     // tail Schur complement, the tail right-hand sides and the refinement
     // residual of those rows are summed over the shards (exchange.h).
-    KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream, int nforced = 0);
+    // qb: an optional Q block (not with nforced > 0).
+    KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream, int nforced = 0,
+              const QBlock* qb = nullptr);
     ~KktDevice();
     KktDevice(const KktDevice&) = delete;
     KktDevice& operator=(const KktDevice&) = delete;
@@ -171,6 +183,11 @@ class KktDevice {
     // matrix
     DevBuf<int> dkA_, diA_, dkAt_, diAt_;
     DevBuf<double> dA_, dAt_;
+    // Q block (qnz_ > 0): CSC, its assembly map, its diagonal by y-node (old order)
+    int qnz_ = 0, qmax_ = 1;
+    DevBuf<int> dkQ_, diQ_;
+    DevBuf<double> dQ_, dQdiag_;
+    DevBuf<int64_t> dqmap_;
     // plan
     DevBuf<int> dcol0_, drowptr_, drows_, dperm_, diperm_;
     DevBuf<int64_t> doff_, damap_, ddslot_, drelptr_;

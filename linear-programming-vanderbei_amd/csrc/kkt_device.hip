@@ -69,21 +69,37 @@ k_assemble_A(int nz, const double* __restrict__ A, const int64_t* __restrict__ a
     if (k < nz) Lx[amap[k]] = A[k];
 }
 
-// K's diagonal: -max(E, eps) on y-nodes, +max(D, eps) on x-nodes (ldlt.c:235-236)
+// -max Q below the diagonal (ldlt.c:253-256: the entry whose new row is below
+// its new column; its symmetric twin and the diagonal have qmap < 0)
+__global__ void __launch_bounds__(NT)
+k_assemble_Q(int nq, const double* __restrict__ Q, const int64_t* __restrict__ qmap, double qmax,
+             double* __restrict__ Lx) {
+    const int k = blockIdx.x * NT + threadIdx.x;
+    if (k < nq && qmap[k] >= 0) Lx[qmap[k]] = -qmax * Q[k];
+}
+
+// K's diagonal: -max(E, eps) on y-nodes, +max(D, eps) on x-nodes (ldlt.c:235-236),
+// then -max Q_jj on the y-nodes of a Q block (ldlt.c:256); |terms| of each
 __global__ void __launch_bounds__(NT)
 k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __restrict__ E,
                 const double* __restrict__ D, double eps, const int64_t* __restrict__ dslot,
                 double* __restrict__ Lx, int* __restrict__ live, double* __restrict__ dscale, int tail_from,
-                int* __restrict__ flags) {
+                int* __restrict__ flags, const double* __restrict__ qdiag, double qmax) {
     const int v = blockIdx.x * NT + threadIdx.x;
     if (v < 3) flags[v] = 0;      // the factorisation's flags (no fill launch of their own)
     if (v >= T) return;
     const int old = perm[v];
     // columns >= tail_from: replicated linking rows of a non-leading shard,
     // whose diagonal enters the summed tail once (from shard 0)
-    const double a = v >= tail_from ? 0.0 : old < m ? -ref_max(E[old], eps) : ref_max(D[old - m], eps);
+    double a = v >= tail_from ? 0.0 : old < m ? -ref_max(E[old], eps) : ref_max(D[old - m], eps);
+    double sc = fabs(a);
+    if (qdiag && old < m) {
+        const double q = qmax * qdiag[old];
+        a = a - q;
+        sc = sc + fabs(q);
+    }
     Lx[dslot[v]] = a;
-    dscale[v] = fabs(a);
+    dscale[v] = sc;
     live[v] = 1;
 }
 
@@ -2246,7 +2262,8 @@ k_kkt_residual(int m, int n, const int* __restrict__ kAt, const int* __restrict_
                const double* __restrict__ E, const double* __restrict__ D, const double* __restrict__ fy,
                const double* __restrict__ fx, const double* __restrict__ dy, const double* __restrict__ dx,
                double* __restrict__ ry, double* __restrict__ rx, double* __restrict__ part, int mrow,
-               const double* __restrict__ axl) {
+               const double* __restrict__ axl, const int* __restrict__ kQ, const int* __restrict__ iQ,
+               const double* __restrict__ Q, double qmax) {
     __shared__ double sh[kResThreads / 64];
     double mx = 0.0;
     for (int i = blockIdx.x * kResThreads + threadIdx.x; i < m + n; i += kRedBlocks * kResThreads) {
@@ -2255,7 +2272,10 @@ k_kkt_residual(int m, int n, const int* __restrict__ kAt, const int* __restrict_
             if (i >= mrow) s = axl[i - mrow];      // linking row: product summed over the shards
             else
                 s = sparse_dot(kAt[i], kAt[i + 1], At, iAt, dx);
-            const double r = fy[i] - (s - E[i] * dy[i]);
+            // a Q block: fy - ((A dx - E dy) - max Q dy), ldlt.c:391-394
+            // (Q symmetric: row i of Q dy summed over its column i in order)
+            const double r = kQ ? fy[i] - ((s - E[i] * dy[i]) - qmax * sparse_dot(kQ[i], kQ[i + 1], Q, iQ, dy))
+                                : fy[i] - (s - E[i] * dy[i]);
             ry[i] = r;
             mx = fmax(mx, ref_abs(r));
         } else {
@@ -2304,8 +2324,21 @@ __global__ void k_flag_to_scalar(const int* f, double* d) { d[0] = static_cast<d
 }  // namespace
 
 // ======================================================================
-KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream, int nforced)
+KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A, hipStream_t stream, int nforced,
+                     const QBlock* qb)
     : m_(m), n_(n), T_(m + n), nforced_(nforced), stream_(stream) {
+    if (qb && !qb->kQ) qb = nullptr;
+    if (qb && nforced > 0) throw std::invalid_argument("kkt: a Q block with forced rows is not supported");
+    QPattern qpat;
+    if (qb) { qpat.kQ = qb->kQ; qpat.iQ = qb->iQ; }
+    // IPO_HIP_SETUP_TIMES: where the host setup goes, to stderr
+    const bool st_on = std::getenv("IPO_HIP_SETUP_TIMES") != nullptr;
+    const auto st0 = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (st_on)
+            std::fprintf(stderr, "setup %-28s %9.1f ms\n", what,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - st0).count());
+    };
     std::vector<int> kat, iat;
     std::vector<double> at;
     csc_transpose(m, n, kA, iA, A, kat, iat, at);
@@ -2313,7 +2346,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     // (IPO_HIP_TAIL_DENSITY=1: only the reference's full dense window)
     double tail_density = kTailDensity;
     if (const char* e = std::getenv("IPO_HIP_TAIL_DENSITY")) tail_density = std::atof(e);
-    plan_ = build_kkt_plan(m, n, kA, iA, kat.data(), iat.data(), nforced, tail_density);
+    mark("transpose");
+    plan_ = build_kkt_plan(m, n, kA, iA, kat.data(), iat.data(), nforced, tail_density, qb ? &qpat : nullptr);
+    mark("ordering + symbolic plan");
     if (nforced > 0) dLinkAx_.alloc(2 * static_cast<size_t>(nforced));
     const int nz = kA[n];
     hipStream_t s = stream_;
@@ -2331,6 +2366,20 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     diperm_.upload(plan_.iperm, s);
     doff_.upload(plan_.off, s);
     damap_.upload(plan_.amap, s);
+    if (qb) {
+        qnz_ = qb->kQ[m];
+        qmax_ = qb->qmax;
+        dkQ_.upload(qb->kQ, m + 1, s);
+        diQ_.upload(qb->iQ, qnz_ > 0 ? qnz_ : 1, s);
+        dQ_.upload(qb->Q, qnz_ > 0 ? qnz_ : 1, s);
+        dqmap_.upload(plan_.qmap, s);
+        std::vector<double> qd(m > 0 ? m : 1, 0.0);
+        for (int j = 0; j < m; j++)
+            for (int k = qb->kQ[j]; k < qb->kQ[j + 1]; k++)
+                if (qb->iQ[k] == j) qd[j] = qb->Q[k];
+        dQdiag_.upload(qd, s);
+        IPO_HIP_CHECK(hipStreamSynchronize(s));
+    }
     ddslot_.upload(plan_.dslot, s);
     drelptr_.upload(plan_.relptr, s);
     dunit_sup_.upload(plan_.unit_sup, s);
@@ -2344,6 +2393,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     dupd_r1_.upload(plan_.upd_r1, s);
     drel_.upload(plan_.rel, s);
     dlevel_sups_.upload(plan_.level_sups, s);
+    mark("fused panel units (k_panel_w");
     {   // fused panel units (k_panel_w): per supernode max(1, tiles - 1) workgroups,
         // workgroup j holding the diagonal block and 64-row tile j + 1
         // (supernodes of at most 16 columns and 64 rows go to the one-wave
@@ -2371,6 +2421,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         // the dependent-pivot path), the bitwise reference of the fused ones
         if (const char* e = std::getenv("IPO_HIP_PANEL")) use_panel_ = std::atoi(e) != 0;
     }
+    mark("solve chunks: levels holding");
     {   // solve chunks: levels holding a panel with more than kChunkRows rows below
         // its diagonal block are solved in 64-row chunks (two launches each way)
         constexpr int kChunkRows = 128;
@@ -2398,6 +2449,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         IPO_HIP_CHECK(hipStreamSynchronize(s));   // csup / cr0 / chunk0 are stack vectors
         h_chunk0_ = chunk0;
     }
+    mark("sweep order of each level");
     {   // sweep order of each level: on levels without solve chunks the
         // single-column supernodes with <= 64 rows below come first (one wave
         // each, k_fwd_leaf / k_bwd_leaf), the rest after them
@@ -2430,6 +2482,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     // one small gather and the panel, the visits ride in the same launches
     // beside them.  IPO_HIP_VISITS=1/0 forces the schedule on / off.
     std::vector<int> kslot_v;
+    mark("gather chunks (split K)");
     {   // gather chunks (split K): groups = sparse levels, then the dense tail
         const int nu = static_cast<int>(plan_.unit_sup.size());
         const char* ve = std::getenv("IPO_HIP_VISITS");
@@ -2588,6 +2641,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dPartialTile_.alloc(std::max<size_t>(1, max_part) * (kTileRows * kTileRows + 4 * kTileRows));
         IPO_HIP_CHECK(hipStreamSynchronize(s));
     }
+    mark("launches per sweep and algor");
     {   // launches per sweep and algorithmic work per phase occurrence
         fwd_launches_ = bwd_launches_ = sf_level_ < plan_.nlevels ? 1 : 0;
         for (int l = 0; l < sf_level_; l++) {
@@ -2659,6 +2713,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             work_bytes[ph] = 8.0 * (lxs + tail_tri) + 8.0 * 2 * T_ + (ph == kPhForward ? 12.0 : 12.0) * nrowsR;
         }
     }
+    mark("per-task source descriptors ");
     {   // per-task source descriptors for the gather
         auto build = [&](const std::vector<TailTask>& ts, DevBuf<TaskSrc>& dst) {
             std::vector<TaskSrc> v(ts.size());
@@ -2696,6 +2751,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         expand(visits_ ? kslot_v : plan_.kslot, plan_.utasks, dslot_rec_);
         if (plan_.nt > 0) expand(plan_.tail_kslot, plan_.tail_tasks, dtail_slot_rec_);
     }
+    mark("dutasks_.upload(reinterpret_");
     dutasks_.upload(reinterpret_cast<const uint64_t*>(plan_.utasks.data()), plan_.utasks.size() * 4, s);
     if (plan_.nt > 0) {
         dtail_task_ptr_.upload(plan_.tail_task_ptr, s);
@@ -2717,6 +2773,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         }
     }
 
+    mark("dLx_.alloc(plan_.lx_size > 0");
     dLx_.alloc(plan_.lx_size > 0 ? plan_.lx_size : 1);
     dDg_.alloc(T_ > 0 ? T_ : 1);
     dLive_.alloc(T_ > 0 ? T_ : 1);
@@ -2745,6 +2802,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
     IPO_HIP_CHECK(hipEventCreate(&ev2_));
     IPO_HIP_CHECK(hipEventCreate(&ev3_));
     IPO_HIP_CHECK(hipStreamSynchronize(s));
+    mark("done");
 }
 
 // Sync-free top levels (k_fwd_sf / k_bwd_sf): from sf_level_ up every level
@@ -3046,9 +3104,13 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
     const int nz = static_cast<int>(plan_.amap.size());
     IPO_HIP_CHECK(hipMemsetAsync(dLx_.get(), 0, dLx_.bytes(), s));
     if (nz > 0) hipLaunchKernelGGL(k_assemble_A, dim3(ceil_div(nz, NT)), dim3(NT), 0, s, nz, dA_.get(), damap_.get(), dLx_.get());
+    if (qnz_ > 0)
+        hipLaunchKernelGGL(k_assemble_Q, dim3(ceil_div(qnz_, NT)), dim3(NT), 0, s, qnz_, dQ_.get(), dqmap_.get(),
+                           static_cast<double>(qmax_), dLx_.get());
     hipLaunchKernelGGL(k_assemble_diag, dim3(ceil_div(T_, NT)), dim3(NT), 0, s, T_, m_, dperm_.get(), dE, dD, epsdiag_,
                        ddslot_.get(), dLx_.get(), dLive_.get(), dDscale_.get(), shard_minor() ? plan_.tail_c0 : T_,
-                       dFlags_.get());
+                       dFlags_.get(), dkQ_.get() ? dQdiag_.get() : static_cast<const double*>(nullptr),
+                       static_cast<double>(qmax_));
     const TailView tv = tail_view();
     for (int l = 0; l < plan_.nlevels; l++) {
         const int u0 = plan_.unit_level_ptr[l], u1 = plan_.unit_level_ptr[l + 1];
@@ -3544,7 +3606,9 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
             }
             hipLaunchKernelGGL(k_kkt_residual, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, dkAt_.get(), diAt_.get(),
                                dAt_.get(), dkA_.get(), diA_.get(), dA_.get(), dE, dD, dfy[r], dfx[r], dyv(r), dxv(r),
-                               ryv(r), rxv(r), dPart_.get() + (size_t)nq * kRedBlocks, mrow, axl);
+                               ryv(r), rxv(r), dPart_.get() + (size_t)nq * kRedBlocks, mrow, axl,
+                               dkQ_.get() ? dkQ_.get() : static_cast<const int*>(nullptr), diQ_.get(), dQ_.get(),
+                               static_cast<double>(qmax_));
             nq++;
         }
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), nq, (1u << nq) - 1u,

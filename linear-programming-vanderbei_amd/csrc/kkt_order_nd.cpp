@@ -41,14 +41,21 @@ struct Job {
 }  // namespace
 
 std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
-                                        int nforced, int leaf_rows) {
+                                        int nforced, int leaf_rows, const QPattern* q) {
     const int T = m + n, mf = m - nforced, Tfree = T - nforced;
-    // free graph in CSR (forced rows left out, as in order_tiered_min_degree)
+    const bool hasq = q && q->kQ;
+    if (hasq && nforced > 0) throw std::invalid_argument("kkt: a Q block with forced rows is not supported");
+    // free graph in CSR (forced rows left out, as in order_tiered_min_degree);
+    // a Q block adds y-y edges, and the graph is then no longer bipartite
     std::vector<int> xadj(T + 1, 0), adj;
-    adj.reserve(2 * static_cast<size_t>(kA[n]));
+    adj.reserve(2 * static_cast<size_t>(kA[n]) + (hasq ? q->kQ[m] : 0));
     for (int r = 0; r < m; r++) {
-        if (r < mf)
+        if (r < mf) {
             for (int k = kAt[r]; k < kAt[r + 1]; k++) adj.push_back(m + iAt[k]);
+            if (hasq)
+                for (int k = q->kQ[r]; k < q->kQ[r + 1]; k++)
+                    if (q->iQ[k] != r) adj.push_back(q->iQ[k]);
+        }
         xadj[r + 1] = static_cast<int>(adj.size());
     }
     for (int c = 0; c < n; c++) {
@@ -194,7 +201,7 @@ std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* 
         {
             long bestc = -1;
             for (int l = 1; l + 1 < nl; l++) {
-                if ((l & 1) != ypar) continue;
+                if (!hasq && (l & 1) != ypar) continue;
                 const long b = before[l], a = size - before[l + 1];
                 const long rest = b + a;
                 if (10 * std::min(a, b) < 3 * rest) continue;        // both sides >= 30 %
@@ -203,7 +210,7 @@ std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* 
             if (sep < 0) {        // no balanced y-level: the one nearest the median
                 long bd = -1;
                 for (int l = 1; l + 1 < nl; l++) {
-                    if ((l & 1) != ypar) continue;
+                    if (!hasq && (l & 1) != ypar) continue;
                     const long d = std::labs(before[l] - (size - before[l + 1]));
                     if (bd < 0 || d < bd) { bd = d; sep = l; }
                 }
@@ -249,7 +256,8 @@ std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* 
 // nodes [0, Tfree) (forced rows excluded): column j holds K's entries below
 // j and every child's pattern below j (the row-merge rule over the
 // elimination tree, parent = first row).
-void symbolic_from_perm(KktOrdering& o, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced) {
+void symbolic_from_perm(KktOrdering& o, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced,
+                        const QPattern* q) {
     const int m = o.m, T = o.T, Tfree = T - nforced, mf = m - nforced;
     o.iperm.assign(T, -1);
     for (int j = 0; j < T; j++) o.iperm[o.perm[j]] = j;
@@ -266,6 +274,8 @@ void symbolic_from_perm(KktOrdering& o, const int* kA, const int* iA, const int*
         };
         if (v < m) {
             for (int k = kAt[v]; k < kAt[v + 1]; k++) add(iperm[m + iAt[k]]);
+            if (q && q->kQ)
+                for (int k = q->kQ[v]; k < q->kQ[v + 1]; k++) add(iperm[q->iQ[k]]);
         } else {
             for (int k = kA[v - m]; k < kA[v - m + 1]; k++)
                 if (iA[k] < mf) add(iperm[iA[k]]);

@@ -39,6 +39,17 @@ struct KktOrdering {
     double narth = 0.0;            // reference op count (ldlt.c:1243-1248)
 };
 
+// Sparsity of the Q block of ldlt.c's K (ldlt.c:253-256: -max Q added to the
+// first node class, here the y-nodes): m x m, full symmetric CSC (both
+// triangles and the diagonal, rows sorted in every column, as iolp.c:733-793
+// leaves QUADS).  Its off-diagonal entries are edges of the KKT graph
+// (ldlt.c:729-745) and make the problem non-separable (ldlt.c:675-682).
+struct QPattern {
+    const int* kQ = nullptr;
+    const int* iQ = nullptr;
+    bool separable(int m) const;
+};
+
 // ldlt.c:638-858 (inv_sym) + ldlt.c:860-1262 (lltsym), method _MD, dense = 3.
 //
 // nforced > 0 (not in the reference; block-angular sharding, SURVEY.md
@@ -50,7 +61,7 @@ struct KktOrdering {
 // problem, so blocks that share only the linking rows factor apart and meet
 // in the tail.  nforced = 0 is the reference ordering, unchanged.
 KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
-                                    const int* kAt, const int* iAt, int nforced = 0);
+                                    const int* kAt, const int* iAt, int nforced = 0, const QPattern* q = nullptr);
 
 // Nested dissection (kkt_order_nd.cpp; not in the reference): the
 // elimination order used instead of the reference's on problems of at least
@@ -59,10 +70,11 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
 // perm[new] = old; forced rows last in natural order as above.  Pieces of
 // at most leaf_rows y-nodes are ordered x-nodes first, then y-nodes.
 std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
-                                        int nforced, int leaf_rows);
+                                        int nforced, int leaf_rows, const QPattern* q = nullptr);
 // The symbolic factor (Lp, Li, iperm) of o.perm over the free nodes; forced
 // rows get empty columns (add the dense tail after).
-void symbolic_from_perm(KktOrdering& o, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced);
+void symbolic_from_perm(KktOrdering& o, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced,
+                        const QPattern* q = nullptr);
 // Pad chains of columns (parent(j) = j + 1) below column tc into panels of
 // at most kPanelCols columns holding at most zfrac explicit zeros (relaxed
 // supernodes; the padded entries stay exact zeros in the factor).
@@ -70,7 +82,7 @@ void relax_supernodes(KktOrdering& o, int tc, double zfrac);
 // nested dissection, Lp/Li, forced tail, relaxed supernodes, narth (of the
 // unpadded pattern): the KktOrdering of that order
 KktOrdering order_nested_dissection(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
-                                    int nforced, int leaf_rows, double zfrac);
+                                    int nforced, int leaf_rows, double zfrac, const QPattern* q = nullptr);
 constexpr int kNdMinNodes = 100000;
 constexpr int kNdDense = 64;         // smallest degree of a dense node (also > 10x its class mean)
 constexpr int kNdLeafRows = 1024;   // measured on configs[3]: 4.5e10 factor flops, 62 levels (256: 5.5e10, 61)
@@ -141,6 +153,9 @@ struct KktPlan {
 
     // assembly: A nonzero k (CSC order) -> slot in Lx; node v (new) -> diagonal slot
     std::vector<int64_t> amap;
+    // Q nonzero k (CSC order) -> its slot in Lx where its new row is below its
+    // new column, -1 where the symmetric twin carries it, -2 on the diagonal
+    std::vector<int64_t> qmap;
     std::vector<int64_t> dslot;     // [T]
     std::vector<int> dsign;         // [T] -1 for y-nodes, +1 for x-nodes (new index)
     int64_t lx_size = 0;
@@ -190,6 +205,6 @@ struct KktPlan {
 // whose lower triangle is at least that full (1: only the full triangle,
 // the reference's dense window)
 KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
-                       int nforced = 0, double tail_density = 1.0);
+                       int nforced = 0, double tail_density = 1.0, const QPattern* q = nullptr);
 
 }  // namespace ipo

@@ -106,12 +106,20 @@ void add_forced_tail(KktOrdering& o, int m, const int* kA, const int* iA, int nf
 
 }  // namespace
 
+bool QPattern::separable(int m) const {
+    if (!kQ) return true;
+    for (int j = 0; j < m; j++)
+        for (int k = kQ[j]; k < kQ[j + 1]; k++)
+            if (iQ[k] != j) return false;
+    return true;
+}
+
 KktOrdering order_nested_dissection(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt,
-                                    int nforced, int leaf_rows, double zfrac) {
+                                    int nforced, int leaf_rows, double zfrac, const QPattern* q) {
     KktOrdering o;
     o.m = m; o.n = n; o.T = m + n;
-    o.perm = nested_dissection_perm(m, n, kA, iA, kAt, iAt, nforced, leaf_rows);
-    symbolic_from_perm(o, kA, iA, kAt, iAt, nforced);
+    o.perm = nested_dissection_perm(m, n, kA, iA, kAt, iAt, nforced, leaf_rows, q);
+    symbolic_from_perm(o, kA, iA, kAt, iAt, nforced, q);
     const int T = o.T;
     if (nforced > 0) {
         add_forced_tail(o, m, kA, iA, nforced);
@@ -135,7 +143,9 @@ bool use_nested_dissection(int T) {
 }
 
 KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
-                                    const int* kAt, const int* iAt, int nforced) {
+                                    const int* kAt, const int* iAt, int nforced, const QPattern* q) {
+    const bool hasq = q && q->kQ;
+    if (hasq && nforced > 0) throw std::invalid_argument("kkt: a Q block with forced rows is not supported");
     KktOrdering o;
     o.m = m; o.n = n; o.T = m + n;
     const int T = o.T;
@@ -154,7 +164,8 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
         keep = keep * (1.0 - dens * dens);
     }
     const double fill_x_first = 0.5 * m * m * (1.0 - keep);
-    o.pdf = (3 * fill_y_first <= fill_x_first) ? 1 : 2;
+    // the primal priority needs a separable problem (ldlt.c:675-682, 710)
+    o.pdf = (3 * fill_y_first <= fill_x_first && (!hasq || q->separable(m))) ? 1 : 2;
 
     // adjacency of K, y-node r lists its x-nodes (column order), x-node c its rows
     // forced rows (y-nodes mf..m-1, see kkt_plan.h) stay out of the graph
@@ -162,8 +173,11 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
     std::vector<std::vector<int>> nb(T);
     std::vector<int> tier(T);
     for (int r = 0; r < mf; r++) {
-        nb[r].reserve(kAt[r + 1] - kAt[r]);
+        nb[r].reserve(kAt[r + 1] - kAt[r] + (hasq ? q->kQ[r + 1] - q->kQ[r] : 0));
         for (int k = kAt[r]; k < kAt[r + 1]; k++) nb[r].push_back(m + iAt[k]);
+        if (hasq)            // then the Q neighbours (ldlt.c:737-742)
+            for (int k = q->kQ[r]; k < q->kQ[r + 1]; k++)
+                if (q->iQ[k] != r) nb[r].push_back(q->iQ[k]);
         tier[r] = o.pdf == 1 ? 0 : 1;
     }
     for (int r = mf; r < m; r++) tier[r] = 0;
@@ -276,8 +290,14 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
         }
         // clique on the survivors: w gains, in group order, every member of
         // the group it is not adjacent to yet (the pairwise loop below appends
-        // exactly that sequence to every list)
-        if (bw > 0) {
+        // exactly that sequence to every list).  Nothing to add once the
+        // survivors form a complete graph (the reference's dense window:
+        // every survivor a neighbour of piv and of each other)
+        const int nsurv = Tfree - next;
+        bool complete = static_cast<int>(group.size()) == nsurv;
+        for (size_t a = 0; complete && a < group.size(); a++) complete = deg[group[a]] == nsurv - 1;
+        if (complete) {
+        } else if (bw > 0) {
             cg.resize(group.size());
             for (size_t a = 0; a < group.size(); a++) cg[a] = cidx[group[a]];
             for (size_t a = 0; a < group.size(); a++) {
@@ -347,13 +367,14 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
 }
 
 KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kAt, const int* iAt, int nforced,
-                       double tail_density) {
+                       double tail_density, const QPattern* q) {
     int leaf = kNdLeafRows;
     if (const char* e = std::getenv("IPO_HIP_ND_LEAF")) leaf = std::max(1, std::atoi(e));
     double relax = kNdRelax;
     if (const char* e = std::getenv("IPO_HIP_ND_RELAX")) relax = std::atof(e);
-    KktOrdering o = use_nested_dissection(m + n) ? order_nested_dissection(m, n, kA, iA, kAt, iAt, nforced, leaf, relax)
-                                                 : order_tiered_min_degree(m, n, kA, iA, kAt, iAt, nforced);
+    KktOrdering o = use_nested_dissection(m + n)
+                        ? order_nested_dissection(m, n, kA, iA, kAt, iAt, nforced, leaf, relax, q)
+                        : order_tiered_min_degree(m, n, kA, iA, kAt, iAt, nforced, q);
     KktPlan P;
     P.m = m; P.n = n; P.T = o.T;
     const int T = o.T;
@@ -688,6 +709,14 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
             const int a = P.iperm[iA[k]], b = P.iperm[m + c];
             P.amap[k] = slot_of(std::max(a, b), std::min(a, b));
         }
+    if (q && q->kQ) {       // ldlt.c:253-256: row > col stored, row == col on the diagonal
+        P.qmap.resize(q->kQ[m]);
+        for (int j = 0; j < m; j++)
+            for (int k = q->kQ[j]; k < q->kQ[j + 1]; k++) {
+                const int row = P.iperm[q->iQ[k]], col = P.iperm[j];
+                P.qmap[k] = row > col ? slot_of(row, col) : row == col ? -2 : -1;
+            }
+    }
     return P;
 }
 

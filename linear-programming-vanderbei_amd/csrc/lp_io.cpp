@@ -4,7 +4,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <unordered_map>
+#include <utility>
 
 namespace ipo {
 
@@ -53,6 +55,11 @@ int read_mps(const char* path, MpsProblem& P, std::string* err) {
     std::vector<int> row_kind;          // 0 = E/G, 1 = L (negated), 2 = N (dropped)
     std::vector<std::string> col_name;
     std::string obj_row, rhs_set, rng_set, bnd_set;
+    bool quads = false;                       // QUADS section seen
+    int q_prev = -1;                          // last QUADS column (iolp.c's j_previous)
+    std::vector<int> q_colptr, q_row;         // strictly lower entries by column
+    std::vector<double> q_val;
+    std::unordered_map<int, double> q_diag;
     char word0[256] = "", word1[256] = "";
     Card cd;
     cd.buf[79] = '\0';
@@ -194,17 +201,60 @@ int read_mps(const char* path, MpsProblem& P, std::string* err) {
             else P.warnings.push_back("unrecognized bound type " + k);
             break;
         }
-        case Section::Quads:   // ipo never hands Q to solver(); only the section flow matters
+        case Section::Quads: {   // iolp.c:583-645: the lower triangle of Q by columns
             if (cd.buf[0] != ' ') {
                 sec = section_from(cd.buf);
                 if (sec == Section::Unknown) { unknown_section(cd.buf); goto finish; }
+                break;
+            }
+            quads = true;
+            auto ct = col_id.find(cd.name0());
+            if (ct == col_id.end()) { P.warnings.push_back(std::string("column label missing: ") + cd.name0()); break; }
+            const int j = ct->second;
+            if (j > q_prev) {
+                q_colptr.resize(j + 1, static_cast<int>(q_row.size()));
+                q_prev = j;
+            } else if (j < q_prev) {
+                if (err) *err = "QUADS columns out of order";
+                rc = 36;
+                goto finish;
+            }
+            for (int fld = 0; fld < 2; fld++) {
+                if (cd.len < (fld ? 50 : 25)) continue;
+                const double v = std::atof(fld ? cd.num2() : cd.num1());
+                if (v == 0.0) continue;
+                auto rt = col_id.find(fld ? cd.name2() : cd.name1());
+                if (rt == col_id.end()) { P.warnings.push_back(std::string("column label missing: ") + (fld ? cd.name2() : cd.name1())); continue; }
+                const int i = rt->second;
+                if (i > j) { q_row.push_back(i); q_val.push_back(v); }
+                else if (i == j) q_diag[j] = v;
+                else P.warnings.push_back("QUADS entry above the diagonal ignored");
             }
             break;
+        }
         default:
             break;
         }
     }
     if (P.name.empty()) { if (err) *err = "NAME not found"; rc = 11; goto finish; }
+    if (quads) {   // symmetrise (iolp.c:733-793): both triangles + the nonzero diagonal, rows sorted
+        const int n = static_cast<int>(col_name.size());
+        q_colptr.resize(n + 1, static_cast<int>(q_row.size()));
+        std::vector<std::vector<std::pair<int, double>>> col(n);
+        for (int j = 0; j < n; j++) {
+            for (int k = q_colptr[j]; k < q_colptr[j + 1]; k++) col[j].push_back({q_row[k], q_val[k]});
+            auto d = q_diag.find(j);
+            if (d != q_diag.end() && d->second != 0.0) col[j].push_back({j, d->second});
+            for (int k = q_colptr[j]; k < q_colptr[j + 1]; k++) col[q_row[k]].push_back({j, q_val[k]});
+        }
+        P.kQ.assign(1, 0);
+        for (int j = 0; j < n; j++) {
+            std::stable_sort(col[j].begin(), col[j].end(),
+                             [](const std::pair<int, double>& a, const std::pair<int, double>& b) { return a.first < b.first; });
+            for (const auto& e : col[j]) { P.iQ.push_back(e.first); P.Q.push_back(e.second); }
+            P.kQ.push_back(static_cast<int>(P.iQ.size()));
+        }
+    }
     if (sec != Section::End) P.warnings.push_back("ENDATA not found");
     {
         const int n = static_cast<int>(col_name.size());

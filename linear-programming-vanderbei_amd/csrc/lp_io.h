@@ -26,9 +26,16 @@ struct MpsProblem {
     double inftol = 1.0e-5;         // INFTOL header keyword (iolp.c:98, :297)
     std::vector<std::string> rowlab, collab;   // field text, trailing blanks kept (iolp.c:387, :422)
     std::vector<std::string> warnings;
+    // QUADS (iolp.c:583-645, symmetrised as iolp.c:733-793): n x n, both
+    // triangles and the nonzero diagonal, rows sorted in each column; empty
+    // kQ when the file has no QUADS section.  solvelp() does not pass Q to
+    // solver() (solve.c:24-26 has no Q); the LU plug-in takes it
+    // (ipo_hip_ldlt_set_q, ldlt.c:253-256).
+    std::vector<int> kQ, iQ;
+    std::vector<double> Q;
 };
 
-// Returns 0 on success or the reference's error number (2, 11, 26, 35).
+// Returns 0 on success or the reference's error number (2, 11, 26, 35, 36).
 int read_mps(const char* path, MpsProblem& out, std::string* err);
 
 struct SolverForm {

@@ -78,6 +78,7 @@ EXPORTED = [
     "ipo_hip_ctx_setup_seconds", "ipo_hip_kkt_set_epsdiag",
     "ipo_hip_synth_random", "ipo_hip_synth_block_angular", "ipo_hip_symbolic_forced",
     "ipo_hip_set_device", "ipo_hip_rccl_unique_id", "ipo_hip_ctx_create_shard", "ipo_hip_vector_bench",
+    "ipo_hip_kkt_create_q", "ipo_hip_ldlt_set_q", "ipo_hip_symbolic_q", "ipo_hip_mps_quads",
 ]
 
 # int (*)(void *user, double *buf, long n, int op)  -- ipo_hip_allreduce_fn
@@ -123,6 +124,15 @@ def lib() -> C.CDLL:
     L.ipo_hip_mps_load.restype = _I
     L.ipo_hip_kkt_create.argtypes = [_I, _I, _P, _P, _P]
     L.ipo_hip_kkt_create.restype = _P
+    L.ipo_hip_kkt_create_q.argtypes = [_I, _I, _P, _P, _P, _P, _P, _P, _I]
+    L.ipo_hip_kkt_create_q.restype = _P
+    L.ipo_hip_ldlt_set_q.argtypes = [_I, _P, _P, _P, _I]
+    L.ipo_hip_ldlt_set_q.restype = _I
+    L.ipo_hip_symbolic_q.argtypes = [_I, _I, _P, _P, _P, _P, _P, C.POINTER(C.c_long), C.POINTER(_D), C.POINTER(_I),
+                                     C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]
+    L.ipo_hip_symbolic_q.restype = _I
+    L.ipo_hip_mps_quads.argtypes = [C.c_char_p, _P, _P, _P, _P, _P]
+    L.ipo_hip_mps_quads.restype = _I
     L.ipo_hip_kkt_destroy.argtypes = [_P]
     L.ipo_hip_kkt_destroy.restype = None
     L.ipo_hip_kkt_factor.argtypes = [_P, _P, _P]
@@ -239,6 +249,24 @@ def mps_dims(path: str):
 SPLIT_FREE = 1      # include/ipo_hip.h IPO_HIP_SPLIT_FREE
 
 
+def mps_quads(path: str):
+    """The QUADS section as the reference's reader keeps it (symmetric n x n
+    CSC over the file's columns): (kQ, iQ, Q), or None without QUADS."""
+    L = lib()
+    b = path.encode()
+    n, qnz = C.c_int(), C.c_int()
+    rc = L.ipo_hip_mps_quads(b, C.byref(n), C.byref(qnz), None, None, None)
+    if rc:
+        raise IpoHipError(f"mps_quads: error {rc}: " + last_error())
+    if qnz.value < 0:
+        return None
+    kQ = np.zeros(n.value + 1, np.int32)
+    iQ = np.zeros(max(qnz.value, 1), np.int32)
+    Q = np.zeros(max(qnz.value, 1), np.float64)
+    L.ipo_hip_mps_quads(b, None, None, _ptr(kQ), _ptr(iQ), _ptr(Q))
+    return kQ, iQ[:qnz.value], Q[:qnz.value]
+
+
 def load_mps(path: str, free: str = "abort") -> SolverForm:
     """Read + normalise an MPS file with the native front end (lp_io.cpp).
     free="split": the free-variable extension (split / reflected columns)
@@ -330,12 +358,19 @@ def solver(p: SolverForm, method: str = "hsd", trace: bool = False, max_iter: in
 class KktFactor:
     """Device LDL' of K = [-E A; A' D] for the solver's A (m x n CSC)."""
 
-    def __init__(self, m, n, kA, iA, A):
+    def __init__(self, m, n, kA, iA, A, q=None, qmax=1):
+        """q = (kQ, iQ, Q): a Q block on the y-nodes, K_yy = -max(E, eps) -
+        qmax Q (ldlt.c:253-256; Q m x m, full symmetric CSC)."""
         require_gpu()
         self.m, self.n = m, n
         self._keep = [np.ascontiguousarray(kA, np.int32), np.ascontiguousarray(iA, np.int32),
                       np.ascontiguousarray(A, np.float64)]
-        self.h = lib().ipo_hip_kkt_create(m, n, *[_ptr(a) for a in self._keep])
+        if q is None:
+            self.h = lib().ipo_hip_kkt_create(m, n, *[_ptr(a) for a in self._keep])
+        else:
+            self._keep += [np.ascontiguousarray(q[0], np.int32), np.ascontiguousarray(q[1], np.int32),
+                           np.ascontiguousarray(q[2], np.float64)]
+            self.h = lib().ipo_hip_kkt_create_q(m, n, *[_ptr(a) for a in self._keep], qmax)
         if not self.h:
             raise IpoHipError("kkt create: " + last_error())
 
@@ -490,15 +525,20 @@ class ShardContext(Context):
         self.setup_seconds = lib().ipo_hip_ctx_setup_seconds(self.h)
 
 
-def symbolic(m, n, kA, iA) -> dict:
-    """Host-only symbolic analysis (reference ordering); no GPU needed."""
+def symbolic(m, n, kA, iA, q=None) -> dict:
+    """Host-only symbolic analysis (reference ordering); no GPU needed.
+    q = (kQ, iQ[, Q]): a Q block's pattern on the y-nodes."""
     kA = np.ascontiguousarray(kA, np.int32)
     iA = np.ascontiguousarray(iA, np.int32)
     perm = np.zeros(m + n, np.int32)
     lnz, narth = C.c_long(), C.c_double()
     denwin, pdf, nsup, nlev = C.c_int(), C.c_int(), C.c_int(), C.c_int()
-    rc = lib().ipo_hip_symbolic(m, n, _ptr(kA), _ptr(iA), _ptr(perm), C.byref(lnz), C.byref(narth), C.byref(denwin),
-                                C.byref(pdf), C.byref(nsup), C.byref(nlev))
+    kQ = iQ = None
+    if q is not None:
+        kQ, iQ = np.ascontiguousarray(q[0], np.int32), np.ascontiguousarray(q[1], np.int32)
+    rc = lib().ipo_hip_symbolic_q(m, n, _ptr(kA), _ptr(iA), _ptr(kQ) if kQ is not None else None,
+                                  _ptr(iQ) if iQ is not None else None, _ptr(perm), C.byref(lnz), C.byref(narth),
+                                  C.byref(denwin), C.byref(pdf), C.byref(nsup), C.byref(nlev))
     if rc:
         raise IpoHipError("symbolic: " + last_error())
     return dict(perm=perm, lnz=lnz.value, narth=narth.value, denwin=denwin.value, pdf=pdf.value, nsup=nsup.value,

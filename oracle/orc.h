@@ -48,6 +48,9 @@ typedef struct {
     int sense;             /* 1 = MIN (default), -1 = MAX                     */
     char name[256];
     char **rowlab, **collab; /* [m], [n] field text (iolp.c:387, :422)        */
+    int qnz;               /* QUADS (iolp.c:583-645, symmetrised :733-793):   */
+    int *kQ, *iQ;          /* n x n full symmetric CSC, rows sorted; kQ NULL  */
+    double *Q;             /* when the file has no QUADS section              */
 } orc_mps;
 
 /* ---------- problem as handed to solver(): max c'x, Ax<=b, x>=0 ---------- */
@@ -66,6 +69,8 @@ typedef struct {
 /* Returns 0 on success, nonzero on fatal parse error (message on log). */
 int  orc_mps_read(const char *path, orc_mps *out, FILE *log);
 void orc_mps_free(orc_mps *p);
+/* QUADS of an MPS file: kQ == NULL queries n and qnz (-1: no section). */
+int  orc_mps_quads(const char *path, int *n, int *qnz, int *kQ, int *iQ, double *Q);
 
 /* solve.c:28-205.  Returns 0, or 3 when a free variable is present
  * ("dual unbounded", solve.c:79-87).  Prints "m = ..,n = ..,nz = .. " to log. */
@@ -87,6 +92,13 @@ typedef struct orc_kkt orc_kkt;
 
 orc_kkt *orc_kkt_create(int m, int n, const int *kA, const int *iA, const double *A,
                         const int *kAt, const int *iAt, const double *At);
+/* the same K with the Q block of ldlt.c on the y-nodes (ldlt.c's first node
+ * class, whose diagonal is -max(E, eps)): K_yy = -max(E, eps) - qmax Q, Q an
+ * m x m full symmetric CSC (both triangles, rows sorted, as iolp.c:733-793
+ * leaves it), qmax = lp->max (-1 max, 1 min); kQ == NULL: no Q */
+orc_kkt *orc_kkt_create_q(int m, int n, const int *kA, const int *iA, const double *A,
+                          const int *kAt, const int *iAt, const double *At,
+                          const int *kQ, const int *iQ, const double *Q, int qmax);
 void orc_kkt_destroy(orc_kkt *k);
 /* ldltfac / inv_num: numeric factorisation with row scaling E (m) and column scaling D (n) */
 void orc_kkt_factor(orc_kkt *k, const double *E, const double *D);

@@ -1,8 +1,12 @@
 /*
  * orc_kkt.c -- ORACLE (test infrastructure only, see orc.h).
  *
- * Restatement of src/ipo/ldlt.c for the way ipo uses it (Q empty, every
- * column "bounded below", every row "infinite" -- ldlt.c:140-160):
+ * Restatement of src/ipo/ldlt.c for the way ipo uses it (every column
+ * "bounded below", every row "infinite" -- ldlt.c:140-160; Q empty, or with
+ * orc_kkt_create_q the Q block of ldlt.c's first node class: separability
+ * test ldlt.c:675-682, Q neighbours in the adjacency ldlt.c:729-745,
+ * -max Q scattered into K ldlt.c:253-256, max Q dy in the refinement
+ * residual ldlt.c:391-394):
  *
  *   node numbering    y-nodes (solver rows) 0..m-1, x-nodes m..m+n-1
  *                     (ldlt.c's "n" first, then its "m": hsd.c:218 swaps)
@@ -43,6 +47,9 @@ struct orc_kkt {
     int m, n, T;                 /* solver rows, cols, T = m+n */
     const int *kA, *iA, *kAt, *iAt;
     const double *A, *At;
+    const int *kQ, *iQ;          /* Q block on the y-nodes (m x m, full symmetric CSC) or NULL */
+    const double *Q;
+    int qmax;                    /* lp->max of ldlt.c:185: -1 max, 1 min  */
     int *perm, *iperm;           /* perm[new] = old                       */
     int *Lp, *Li;                /* strict lower L, CSC, new indices      */
     double *Lx, *d;
@@ -52,7 +59,7 @@ struct orc_kkt {
     double narth, epsdiag;
     /* work */
     double *acc; int *first, *link, *pos;
-    double *zr, *dy, *dx, *ry, *rx;
+    double *zr, *dy, *dx, *ry, *rx, *qy;
     int passes;
 };
 
@@ -229,15 +236,25 @@ static void symbolic(orc_kkt *K)
     frac = 1.0;
     for (int i = 0; i < n; i++) { double dn = (double)(K->kA[i + 1] - K->kA[i]) / (m + 1); frac = frac * (1.0 - dn * dn); }
     double dfill = 0.5 * m * m * (1.0 - frac);
-    K->pdf = (3 * pfill <= dfill) ? 1 : 2;
+    /* a Q with off-diagonal entries makes the problem non-separable, which
+     * forces the dual priority (ldlt.c:675-682, 710) */
+    int separable = 1;
+    if (K->kQ)
+        for (int j = 0; j < m && separable; j++)
+            for (int k = K->kQ[j]; k < K->kQ[j + 1]; k++)
+                if (K->iQ[k] != j) { separable = 0; break; }
+    K->pdf = (3 * pfill <= dfill && separable) ? 1 : 2;
 
     int *deg = malloc(sizeof(int) * (size_t)T), *cap = malloc(sizeof(int) * (size_t)T);
     int **adj = malloc(sizeof(int *) * (size_t)T);
     int *tier = malloc(sizeof(int) * (size_t)T);
     for (int j = 0; j < m; j++) {
         int c = K->kAt[j + 1] - K->kAt[j];
-        adj[j] = malloc(sizeof(int) * (size_t)(c > 0 ? c : 1)); cap[j] = c; deg[j] = c;
+        int cq = K->kQ ? K->kQ[j + 1] - K->kQ[j] : 0;
+        adj[j] = malloc(sizeof(int) * (size_t)(c + cq > 0 ? c + cq : 1)); cap[j] = c + cq; deg[j] = c;
         for (int k = 0; k < c; k++) adj[j][k] = m + K->iAt[K->kAt[j] + k];
+        for (int k = 0; k < cq; k++)          /* then the Q neighbours, ldlt.c:737-742 */
+            if (K->iQ[K->kQ[j] + k] != j) adj[j][deg[j]++] = K->iQ[K->kQ[j] + k];
         tier[j] = K->pdf == 1 ? 0 : 1;
     }
     for (int i = 0; i < n; i++) {
@@ -264,9 +281,17 @@ static void symbolic(orc_kkt *K)
 orc_kkt *orc_kkt_create(int m, int n, const int *kA, const int *iA, const double *A,
                         const int *kAt, const int *iAt, const double *At)
 {
+    return orc_kkt_create_q(m, n, kA, iA, A, kAt, iAt, At, NULL, NULL, NULL, 1);
+}
+
+orc_kkt *orc_kkt_create_q(int m, int n, const int *kA, const int *iA, const double *A,
+                          const int *kAt, const int *iAt, const double *At,
+                          const int *kQ, const int *iQ, const double *Q, int qmax)
+{
     orc_kkt *K = calloc(1, sizeof(*K));
     K->m = m; K->n = n; K->T = m + n;
     K->kA = kA; K->iA = iA; K->A = A; K->kAt = kAt; K->iAt = iAt; K->At = At;
+    K->kQ = kQ; K->iQ = iQ; K->Q = Q; K->qmax = qmax;
     K->epsdiag = EPS_DIAG0;
     symbolic(K);
     int T = K->T;
@@ -280,6 +305,7 @@ orc_kkt *orc_kkt_create(int m, int n, const int *kA, const int *iA, const double
     K->zr = malloc(sizeof(double) * (size_t)T);
     K->dy = malloc(sizeof(double) * (size_t)(m ? m : 1));
     K->ry = malloc(sizeof(double) * (size_t)(m ? m : 1));
+    K->qy = malloc(sizeof(double) * (size_t)(m ? m : 1));
     K->dx = malloc(sizeof(double) * (size_t)(n ? n : 1));
     K->rx = malloc(sizeof(double) * (size_t)(n ? n : 1));
     return K;
@@ -290,7 +316,7 @@ void orc_kkt_destroy(orc_kkt *K)
     if (!K) return;
     free(K->perm); free(K->iperm); free(K->Lp); free(K->Li); free(K->Lx); free(K->d);
     free(K->live); free(K->acc); free(K->first); free(K->link); free(K->pos);
-    free(K->zr); free(K->dy); free(K->ry); free(K->dx); free(K->rx);
+    free(K->zr); free(K->dy); free(K->ry); free(K->dx); free(K->rx); free(K->qy);
     free(K);
 }
 
@@ -428,6 +454,12 @@ void orc_kkt_factor(orc_kkt *K, const double *E, const double *D)
             int r = iperm[m + K->iAt[k]];
             if (r > col) Lx[pos[r]] = K->At[k];
         }
+        if (K->kQ)                          /* -max Q (ldlt.c:253-256) */
+            for (int k = K->kQ[j]; k < K->kQ[j + 1]; k++) {
+                int r = iperm[K->iQ[k]];
+                if (r > col) Lx[pos[r]] = -K->qmax * K->Q[k];
+                else if (r == col) d[r] -= K->qmax * K->Q[k];
+            }
     }
     for (int i = 0; i < n; i++) {           /* x-node columns: entries A(:, i) */
         int col = iperm[m + i];
@@ -510,6 +542,10 @@ int orc_kkt_solve(orc_kkt *K, const double *E, const double *D, double *fy, doub
         /* rx = A' dy (row-major walk), ry = A dx (column walk) */
         orc_spmv(n, m, K->At, K->kAt, K->iAt, dy, rx);
         orc_spmv(m, n, K->A, K->kA, K->iA, dx, ry);
+        if (K->kQ) {                        /* ldlt.c:391-394 */
+            orc_spmv(m, m, K->Q, K->kQ, K->iQ, dy, K->qy);
+            for (int j = 0; j < m; j++) ry[j] = fy[j] - ((ry[j] - E[j] * dy[j]) - K->qmax * K->qy[j]);
+        } else
         for (int j = 0; j < m; j++) ry[j] = fy[j] - (ry[j] - E[j] * dy[j]);
         for (int i = 0; i < n; i++) rx[i] = fx[i] - (rx[i] + D[i] * dx[i]);
         rs_old = rs;

@@ -10,7 +10,9 @@
  *  - COLUMNS with 'MARKER' toggling, zero values skipped  (iolp.c:401-472)
  *  - RHS / RANGES: second field pair handled first        (iolp.c:474-534)
  *  - BOUNDS LO/UP/FX/FR/PL/MI/BV/LI/UI/SC                 (iolp.c:536-581)
- *  - QUADS: parsed for section flow only; ipo never passes Q to solver()
+ *  - QUADS: kept as iolp.c:583-645 reads it (strict lower triangle by
+ *    columns, diagonal apart) and symmetrised as iolp.c:733-793; solve.c
+ *    never passes Q to solver(), ldlt.c takes it (ldlt.c:253-256)
  *  - objective extraction, N rows dropped, L rows negated (iolp.c:670-727)
  * Label lookups overwrite on re-install like hash.c:99-119.
  */
@@ -102,6 +104,8 @@ int orc_mps_read(const char *path, orc_mps *P, FILE *log)
     double *b = NULL, *c = NULL, *lo = NULL;
     char **collab = NULL, **rowlab = NULL;
 
+    int quads = 0, qprev = -1, qn = 0, qcap = 0, *qk = NULL, *qi = NULL, qkcap = 0, qkn = 0;
+    double *qv = NULL, *qdiag = NULL;
     char line[240], w0[256] = "", w1[256] = "";
     line[79] = '\0';
     char *ty = line + 1, *l0 = line + 4, *l1 = line + 14, *v1 = line + 24, *l2 = line + 39, *v2 = line + 49;
@@ -231,9 +235,33 @@ int orc_mps_read(const char *path, orc_mps *P, FILE *log)
             else if (log) fprintf(log, "unrecognized bound type %s \n", ty);
             break;
         }
-        case S_QUAD:
-            if (line[0] != ' ') { st = section_of(line); if (st == S_BAD) { if (log) fprintf(log, "ERROR(26): unrecognized section label: \n   %s \n\n", line); rc = 26; goto done; } }
+        case S_QUAD: {
+            if (line[0] != ' ') { st = section_of(line); if (st == S_BAD) { if (log) fprintf(log, "ERROR(26): unrecognized section label: \n   %s \n\n", line); rc = 26; goto done; } break; }
+            if (!quads) { quads = 1; qdiag = calloc((size_t)(n > 0 ? n : 1), sizeof(double)); }
+            int j = lbl_get(&cols, tagged(key, l0, 'C'));
+            if (j == -1) { if (log) fprintf(log, "column label %s missing (34)\n", l0); break; }
+            if (j > qprev) {
+                for (int jj = qprev + 1; jj <= j; jj++) { GROW(qk, qkcap, qkn, int); qk[qkn++] = qn; }
+                qprev = j;
+            } else if (j < qprev) {
+                if (log) fprintf(log, "ERROR(36): QUADS columns out of order\n\n");
+                rc = 36; goto done;
+            }
+            for (int fld = 0; fld < 2; fld++) {
+                if (len < (fld ? 50 : 25)) continue;
+                double v = atof(fld ? v2 : v1);
+                if (v == 0.0) continue;
+                int i = lbl_get(&cols, tagged(key, fld ? l2 : l1, 'C'));
+                if (i == -1) { if (log) fprintf(log, "column label %s missing (34)\n", fld ? l2 : l1); continue; }
+                if (i > j) {
+                    GROW(qi, qcap, qn, int);
+                    qv = realloc(qv, (size_t)qcap * sizeof(double));
+                    qi[qn] = i; qv[qn] = v; qn++;
+                } else if (i == j) qdiag[j] = v;
+                else if (log) fprintf(log, "QUADS entry above the diagonal ignored (35)\n");
+            }
             break;
+        }
         default:
             break;
         }
@@ -289,13 +317,43 @@ int orc_mps_read(const char *path, orc_mps *P, FILE *log)
     P->rowlab = rowlab; P->collab = collab;
     colstart = NULL; ia = NULL; av = NULL; b = c = rng = lo = up = NULL;
     rowlab = collab = NULL;
+    P->kQ = NULL; P->iQ = NULL; P->Q = NULL; P->qnz = 0;
+    if (quads) {   /* symmetrise (iolp.c:733-793) */
+        for (int jj = qprev + 1; jj <= n; jj++) { GROW(qk, qkcap, qkn, int); qk[qkn++] = qn; }
+        int cnt = 0;
+        for (int j = 0; j < n; j++) if (qdiag[j] != 0.0) cnt++;
+        int tot = 2 * qn + cnt;
+        int *kq = malloc(sizeof(int) * (size_t)(n + 1)), *iq = malloc(sizeof(int) * (size_t)(tot > 0 ? tot : 1));
+        double *q = malloc(sizeof(double) * (size_t)(tot > 0 ? tot : 1));
+        int *w = calloc((size_t)(n + 1), sizeof(int));
+        for (int k = 0; k < qn; k++) w[qi[k]]++;
+        for (int j = 0; j < n; j++) if (qdiag[j] != 0.0) w[j]++;
+        kq[0] = 0;
+        for (int j = 0; j < n; j++) kq[j + 1] = kq[j] + qk[j + 1] - qk[j] + w[j];
+        for (int j = 0; j < n; j++) {
+            w[j] = kq[j];
+            for (int k = qk[j]; k < qk[j + 1]; k++) { q[w[j]] = qv[k]; iq[w[j]] = qi[k]; w[j]++; }
+        }
+        for (int j = 0; j < n; j++) {
+            if (qdiag[j] != 0.0) { iq[w[j]] = j; q[w[j]] = qdiag[j]; w[j]++; }
+            for (int k = qk[j]; k < qk[j + 1]; k++) { int r = qi[k]; iq[w[r]] = j; q[w[r]] = qv[k]; w[r]++; }
+        }
+        for (int j = 0; j < n; j++)          /* insertion sort by row (qksort) */
+            for (int a = kq[j] + 1; a < kq[j + 1]; a++) {
+                int ri = iq[a]; double rv = q[a]; int b2 = a - 1;
+                while (b2 >= kq[j] && iq[b2] > ri) { iq[b2 + 1] = iq[b2]; q[b2 + 1] = q[b2]; b2--; }
+                iq[b2 + 1] = ri; q[b2 + 1] = rv;
+            }
+        free(w);
+        P->kQ = kq; P->iQ = iq; P->Q = q; P->qnz = kq[n];
+    }
 
 done:
     fclose(fp);
     lbl_free(&rows); lbl_free(&cols);
     if (collab) { for (int j = 0; j < n; j++) free(collab[j]); free(collab); }
     if (rowlab) { for (int i = 0; i < m; i++) free(rowlab[i]); free(rowlab); }
-    free(kind);
+    free(kind); free(qk); free(qi); free(qv); free(qdiag);
     if (rc) { free(rng); free(colstart); free(up); free(ia); free(av); free(b); free(c); free(lo); }
     return rc;
 }
@@ -306,5 +364,21 @@ void orc_mps_free(orc_mps *p)
     if (p->collab) { for (int j = 0; j < p->n; j++) free(p->collab[j]); free(p->collab); }
     free(p->colptr); free(p->rowind); free(p->val); free(p->rhs); free(p->obj);
     free(p->range); free(p->lo); free(p->hi);
+    free(p->kQ); free(p->iQ); free(p->Q);
     memset(p, 0, sizeof(*p));
+}
+
+int orc_mps_quads(const char *path, int *n, int *qnz, int *kQ, int *iQ, double *Q)
+{
+    orc_mps p;
+    memset(&p, 0, sizeof(p));
+    int rc = orc_mps_read(path, &p, NULL);
+    if (rc) return rc;
+    if (n) *n = p.n;
+    if (qnz) *qnz = p.kQ ? p.qnz : -1;
+    if (kQ && p.kQ) memcpy(kQ, p.kQ, sizeof(int) * (size_t)(p.n + 1));
+    if (iQ && p.qnz) memcpy(iQ, p.iQ, sizeof(int) * (size_t)p.qnz);
+    if (Q && p.qnz) memcpy(Q, p.Q, sizeof(double) * (size_t)p.qnz);
+    orc_mps_free(&p);
+    return 0;
 }

@@ -63,6 +63,8 @@ def lib():
         P, I, D = C.c_void_p, C.c_int, C.c_double
         L.orc_kkt_create.restype = P
         L.orc_kkt_create.argtypes = [I, I, P, P, P, P, P, P]
+        L.orc_kkt_create_q.restype = P
+        L.orc_kkt_create_q.argtypes = [I, I, P, P, P, P, P, P, P, P, P, I]
         L.orc_kkt_destroy.argtypes = [P]
         L.orc_kkt_factor.argtypes = [P, P, P]
         L.orc_kkt_solve.argtypes = [P, P, P, P, P]
@@ -89,13 +91,20 @@ def lib():
 class OracleKkt:
     """orc_kkt: the reference's tiered-MD ordering + left-looking LDL'."""
 
-    def __init__(self, form):
+    def __init__(self, form, q=None, qmax=1):
+        """q = (kQ, iQ, Q): the Q block on the y-nodes (m x m, full symmetric
+        CSC), K_yy = -max(E, eps) - qmax Q (orc_kkt_create_q)."""
         L = lib()
         self.m, self.n = form.m, form.n
         kAt, iAt, At = form.transpose()
         self._keep = [np.ascontiguousarray(form.kA, np.int32), np.ascontiguousarray(form.iA, np.int32),
                       np.ascontiguousarray(form.A, np.float64), kAt, iAt, At]
-        self.h = L.orc_kkt_create(self.m, self.n, *[a.ctypes.data for a in self._keep])
+        if q is None:
+            self.h = L.orc_kkt_create(self.m, self.n, *[a.ctypes.data for a in self._keep])
+        else:
+            self._keep += [np.ascontiguousarray(q[0], np.int32), np.ascontiguousarray(q[1], np.int32),
+                           np.ascontiguousarray(q[2], np.float64)]
+            self.h = L.orc_kkt_create_q(self.m, self.n, *[a.ctypes.data for a in self._keep], qmax)
 
     def factor(self, E, D):
         E = np.ascontiguousarray(E, np.float64)

@@ -61,9 +61,10 @@ def test_factor_solve_matches_oracle(name):
     assert (np.abs(gd - od) <= 1e-9 * np.abs(od)).all(), np.argmax(np.abs(gd - od) / np.abs(od))
 
 
-def oracle_variants(p, E, D, eps):
-    """The oracle's classification under its three summation orders
-    (orc_set_perturb: lltnum's order, reversed, by source column)."""
+def oracle_variants(p, E, D, eps, fy=None, fx=None):
+    """The oracle under its three summation orders (orc_set_perturb:
+    lltnum's order, reversed, by source column): (ndep, live, pivots,
+    refined solution of (fy, fx) or None) per order."""
     L = oracle_lib.lib()
     out = []
     try:
@@ -72,10 +73,15 @@ def oracle_variants(p, E, D, eps):
             o = oracle_lib.OracleKkt(p)
             o.set_epsdiag(eps)
             o.factor(E, D)
-            out.append((o.info()["ndep"], o.live().copy()))
+            sol = o.solve(E, D, fy, fx)[:2] if fy is not None else None
+            out.append((o.info()["ndep"], o.live().copy(), o.diag().copy(), sol))
     finally:
         L.orc_set_perturb(0)
     return out
+
+
+def _rel(a, b):
+    return np.abs(a - b) / np.maximum(np.abs(b), 1e-300)
 
 
 STATES = sorted(f[:-4] for f in os.listdir(os.path.join(GOLDEN, "..", "kkt_states")) if f.endswith(".npz"))
@@ -94,11 +100,23 @@ def test_ipm_states_match_oracle(state):
         oracle's own three summation orders agree on it (every state without
         dependent pivots), the GPU's is identical; where they do not (every
         captured state with dependent pivots: e.g. 25fv47_85 gives 18 / 15 /
-        74, afiro_30 3 / 4 / 8 -- the reference tests d == 0 exactly,
-        ldlt.c:600, on a numerically singular system) the classification is
-        not a property of the algorithm, and the GPU must recognise the
-        singularity (some dependent pivot) and return finite values; the
-        IPM-level tests judge the outcome."""
+        74, afiro_30 3 / 4 / 8, dfl001_114 8 / 32 / 139 -- the reference
+        tests d == 0 exactly, ldlt.c:600, on a numerically singular system)
+        the classification is not a property of the algorithm, and the GPU
+        must recognise the singularity (some dependent pivot) and return
+        finite values; the IPM-level tests judge the outcome;
+      * pivot by pivot (every pivot live on the GPU and under all three
+        orders): the GPU's relative distance from the oracle's pivots, at
+        its 99th percentile and at its maximum, within twice the oracle's
+        own spread between its orders (floor 1e-9) -- late-iteration
+        systems are ill-conditioned enough that a reordered sum moves a
+        pivot by 1e-3 (dfl001_100) to O(1) (dfl001_110) under the
+        reference's own algorithm, so no fixed tolerance is right for all;
+      * the refined solutions (no dependent pivot anywhere, eps_diag still
+        1e-14): within max(1e-6 relative, twice the oracle orders' spread).
+    Measured on the GPU (tools/kkt_state_compare.py, round 4): the GPU's
+    pivot distance is below the orders' spread on every state, e.g.
+    dfl001_100 p99 1.1e-3 against 2.9e-3, dfl001_40 max 2.6e-9 against 3.4e-9."""
     name, it = state.rsplit("_", 1)
     st = np.load(os.path.join(GOLDEN, "..", "kkt_states", state + ".npz"))
     E, D, eps = st["E"], st["D"], float(st["epsdiag"])
@@ -114,8 +132,16 @@ def test_ipm_states_match_oracle(state):
     orc.factor(E, D)
     gi, oi = gpu.info(), orc.info()
     _, glive = gpu.pivots()
-    var = oracle_variants(p, E, D, eps)
+    var = oracle_variants(p, E, D, eps, fy, fx)
     robust = all(np.array_equal(v[1], var[0][1]) for v in var)
+    gd = gpu.pivots()[0]
+    both = glive.astype(bool) & var[0][1].astype(bool) & var[1][1].astype(bool) & var[2][1].astype(bool)
+    rg = _rel(gd[both], var[0][2][both])
+    rv = np.maximum(_rel(var[1][2][both], var[0][2][both]), _rel(var[2][2][both], var[0][2][both]))
+    if both.any():
+        for qq in (0.99, 1.0):
+            assert np.quantile(rg, qq) <= max(1e-9, 2 * np.quantile(rv, qq)), (qq, np.quantile(rg, qq),
+                                                                                 np.quantile(rv, qq))
     gy, gx, _ = gpu.solve(E, D, fy, fx)
     oy, ox, _ = orc.solve(E, D, fy, fx)
     bc = max(np.abs(fy).max(), np.abs(fx).max()) + 1
@@ -127,9 +153,11 @@ def test_ipm_states_match_oracle(state):
         assert gi["ndep"] == oi["ndep"] and np.array_equal(glive, var[0][1])
     if oi["ndep"] == 0 and gi["ndep"] == 0:
         assert rg <= max(100 * ro, 1e-9 * bc)
-        if eps <= 1e-14:
+        if eps <= 1e-14 and all(v[0] == 0 for v in var):
             scale = 1.0 + max(np.abs(oy).max(), np.abs(ox).max())
-            assert np.abs(gy - oy).max() <= 1e-6 * scale and np.abs(gx - ox).max() <= 1e-6 * scale
+            spread = max(max(np.abs(v[3][0] - oy).max(), np.abs(v[3][1] - ox).max()) for v in var[1:])
+            bound = max(1e-6 * scale, 2 * spread)
+            assert np.abs(gy - oy).max() <= bound and np.abs(gx - ox).max() <= bound, (bound, spread)
     else:
         assert gi["ndep"] > 0 or oi["ndep"] == 0
         assert np.isfinite(gy).all() and np.isfinite(gx).all()

@@ -43,7 +43,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, dims=DIMS, methods=METHODS):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path[:0] = [os.path.join(REPO, "linear-programming-vanderbei_amd"), os.path.join(REPO, "tests")]
     import ipo_amd
@@ -54,11 +54,12 @@ def _rank_main(rank, world, port, q):
     def allreduce(buf, op):
         comm.allreduce(buf, ops[op])
     try:
-        p = ipo_amd.synth_block_angular(*DIMS)
+        p = ipo_amd.synth_block_angular(*dims)
         loc = ipo_amd.shard_block_angular(p, world, rank)
+        del p
         ctx = ipo_amd.ShardContext(loc, world, rank, host_allreduce=allreduce)
         res = {}
-        for method in METHODS:
+        for method in methods:
             st, stats, text = ctx.run(method, trace=(rank == 0))
             res[method] = (st, stats["iters"], stats["final_pobj"], stats["final_dobj"], ctx.solution(), text)
         ctx.close()
@@ -85,25 +86,36 @@ def _references(p, method):
             (o["status"], o["iters"], o["final_pobj"], o["final_dobj"]))
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(300)
-def test_two_shards_on_one_gpu_match_unsharded_and_oracle():
+def _run_shards(world, dims=DIMS, methods=METHODS, timeout=240):
+    """world host-transport shards of the LP `dims` on the one GPU, one
+    spawned process each; their (rank, blocks, results, error) tuples."""
     import multiprocessing as mp
     ipo_amd.require_gpu()
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, dims, methods)) for r in range(world)]
     for pr in procs:
         pr.start()
-    out = sorted((q.get(timeout=240) for _ in procs), key=lambda t: t[0])
-    for pr in procs:
-        pr.join(timeout=60)
+    try:
+        out = sorted((q.get(timeout=timeout) for _ in procs), key=lambda t: t[0])
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+            if pr.is_alive():
+                pr.kill()
     for r in out:
         assert r[3] is None, r[3]
     for pr in procs:
         assert pr.exitcode == 0
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_two_shards_on_one_gpu_match_unsharded_and_oracle():
+    world = 2
+    out = _run_shards(world)
     p = ipo_amd.synth_block_angular(*DIMS)
     nl = DIMS[5]
     for method in METHODS:
@@ -166,3 +178,58 @@ def test_rccl_exchange_one_rank_matches_host_exchange(monkeypatch):
         assert np.array_equal(a, b)
     o = oracle_lib.solve_arrays(p, "hsd")
     assert abs(i0 - o["iters"]) <= 1
+
+
+# BASELINE configs[4] at its stated shape: 8 diagonal blocks of
+# 25,000 x 100,000 (banded, width 256, 4 nnz per column) + 512 linking rows
+# of 2,000 nonzeros each.  No oracle at this size (hours of CPU): the
+# one-process solve is held to HSD's own stop and the optimality
+# certificate, the 8-way split to the one-process solve.
+CONFIG4 = (8, 25000, 100000, 4, 256, 512, 2000)
+
+
+@pytest.fixture(scope="module")
+def config4_one_process():
+    p = ipo_amd.synth_block_angular(*CONFIG4)
+    loc = ipo_amd.shard_block_angular(p, 1, 0)
+    ctx = ipo_amd.ShardContext(loc)
+    try:
+        st, stats, _ = ctx.run("hsd")
+        sol = ctx.solution()
+    finally:
+        ctx.close()
+    return p, st, stats, sol
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_config4_full_size_one_process(config4_one_process):
+    """(a) the whole LP in one process, linking rows forced into the dense tail."""
+    p, st, stats, sol = config4_one_process
+    assert st == 0 and stats["final_mu"] < 1e-12      # HSD's stop, hsd.c:155
+    pr_, du, gap = certificate(p, *sol)
+    assert pr_ < 1e-6 and du < 1e-6 and gap < 1e-6, (pr_, du, gap)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_config4_eight_shards_on_one_gpu_match_one_process(config4_one_process):
+    """(b) the 8-way split (one block per shard, the code path of bench.py's
+    8-GPU run) as 8 host-transport shards sharing the test box's GPU:
+    every rank the same status and iteration count, the replicated
+    linking-row y and w bitwise identical on all ranks, and against the
+    one-process solve the same status, iterations within +-1, objectives
+    within 1e-6 relative; the assembled solution passes the certificate."""
+    p, st1, stats1, _ = config4_one_process
+    world, nl = 8, CONFIG4[5]
+    out = _run_shards(world, CONFIG4, ("hsd",), timeout=540)
+    r = [out[k][2]["hsd"] for k in range(world)]
+    for k in range(1, world):
+        assert r[k][:2] == r[0][:2], (k, r[k][:2], r[0][:2])
+        (_, y0, w0, _), (_, yk, wk, _) = r[0][4], r[k][4]
+        assert np.array_equal(y0[-nl:], yk[-nl:]) and np.array_equal(w0[-nl:], wk[-nl:]), k
+    assert f"m = {p.m},n = {p.n},nz = {p.nz}" in r[0][5]
+    _check(*r[0][:4], (st1, stats1["iters"], stats1["final_pobj"], stats1["final_dobj"]))
+    x, y, w, z = ipo_amd.assemble_block_angular([(out[k][1], out[k][2]["hsd"][4]) for k in range(world)])
+    pr_, du, gap = certificate(p, x, y, w, z)
+    assert pr_ < 1e-6 and du < 1e-6 and gap < 1e-6, (pr_, du, gap)

@@ -116,10 +116,35 @@ def test_gpu_small_synthetic_matches_oracle(name, kw, method):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("leaf", [16, 1024])
+@pytest.mark.parametrize("method", ["hsd", "intpt"])
+def test_gpu_nested_dissection_matches_oracle(monkeypatch, method, leaf):
+    """The nested-dissection order (kkt_order_nd.cpp, the default from
+    100,000 KKT nodes) forced on a small banded LP: the GPU factors K in
+    another elimination order than the oracle's minimum degree (the
+    reference's), so the solve is the same algorithm in another rounding --
+    same status, iterations within +-1, objectives within 1e-6 relative.
+    leaf 16: many separators (deep dissection), leaf 1024: one leaf per
+    piece of the band."""
+    monkeypatch.setenv("IPO_HIP_ORDER", "nd")
+    monkeypatch.setenv("IPO_HIP_ND_LEAF", str(leaf))
+    p = ipo_amd.synth_random(2000, 10000, 4, 64)
+    g = ipo_amd.solver(p, method)
+    o = oracle_lib.solve_arrays(p, method)
+    assert g["status"] == o["status"] == 0
+    assert abs(g["stats"]["iters"] - o["iters"]) <= 1, (g["stats"]["iters"], o["iters"])
+    for k in ("final_pobj", "final_dobj"):
+        assert abs(g["stats"][k] - o[k]) <= 1e-6 * max(1.0, abs(o[k])), (k, g["stats"][k], o[k])
+    pr, du, gap = certificate(p, g["x"], g["y"], g["w"], g["z"])
+    assert pr < 1e-6 and du < 1e-6 and gap < 1e-6
+
+
+@pytest.mark.gpu
 def test_gpu_config3_random_banded_full_size():
     """BASELINE configs[3]: m=200k, n=1M, 4 nnz/column, banded (width 256)."""
     p = ipo_amd.synth_random(200_000, 1_000_000, 4, 256)
     g = ipo_amd.solver(p, "hsd")
     assert g["status"] == 0             # HSD stops on mu < 1e-12 (hsd.c:155)
+    assert g["stats"]["nlevels"] < 100  # nested dissection (minimum degree: 2,785 levels)
     pr, du, gap = certificate(p, g["x"], g["y"], g["w"], g["z"])
     assert pr < 1e-6 and du < 1e-6 and gap < 1e-6, (pr, du, gap)

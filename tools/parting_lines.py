@@ -11,7 +11,9 @@ oracle (more than 1e-6 relative: beyond the 8 printed digits), or the
 length of the shorter trace when none does before one ends.  Before that
 line the reference's trajectory is a property of its algorithm, not of its
 rounding; tests/test_gpu_ipm.py holds the GPU to it line by line there on
-the rounding-unstable problems.  usage: python tools/parting_lines.py
+the rounding-unstable problems.  hsd.c (argument "hsd") gets the same
+column in the "problems" table: where its variants part from the golden
+trace.  usage: python tools/parting_lines.py [intpt] [hsdls] [hsd]
 """
 import concurrent.futures as cf
 import json
@@ -64,14 +66,20 @@ def main():
         others = [trace(fma, name, meth), trace(PLAIN, name, meth, "reverse"), trace(PLAIN, name, meth, "sorted")]
         return job, min(part(base, o) for o in others)
 
-    jobs = [(meth, name) for meth in ("intpt", "hsdls") for name in d[meth]]
+    # hsd's table is d["problems"] (its base trace is the golden one: the
+    # oracle reproduces all of them byte for byte)
+    table = {"intpt": "intpt", "hsdls": "hsdls", "hsd": "problems"}
+    meths = sys.argv[1:] or ["intpt", "hsdls"]
+    jobs = [(meth, name) for meth in meths for name in d[table[meth]]]
     with cf.ThreadPoolExecutor(8) as ex:
         for (meth, name), it in ex.map(one, jobs):
-            d[meth][name]["part_iter"] = it
+            d[table[meth]][name]["part_iter"] = it
     with open(dst, "w") as f:
         json.dump(d, f, indent=1, sort_keys=True)
-    for meth in ("intpt", "hsdls"):
-        print(meth, {n: (v["part_iter"], v["oracle_iters"]) for n, v in sorted(d[meth].items()) if not v["stable"]})
+    for meth in meths:
+        t = d[table[meth]]
+        print(meth, {n: (v["part_iter"], v.get("oracle_iters", v.get("golden_iters"))) for n, v in sorted(t.items())
+                     if not v["stable"]})
 
 
 if __name__ == "__main__":
