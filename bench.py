@@ -145,6 +145,8 @@ def block_angular_leg(d, args, sync):
     fl, by = d.sum(fl), d.sum(by)
     roof = roofline_of(fl / d.world, by / d.world, el / max(iters, 1))
     roof["per"] = "IPM iteration, per GPU (SURVEY.md 8(d) algorithmic work summed over the shards / N)"
+    if d.world == 1:
+        roof.update(leg_counters("blockang"))
     return {"workload": BA_WORKLOAD, "value": iters / el, "roofline": roof, "unit": "iterations/s", "scaling": "strong",
             "n_gpus": d.world, "parallelism": f"shard{d.world}" if d.world > 1 else "one process",
             "exchange": "RCCL allreduce over xGMI" if d.world > 1 else "none (linking rows in the dense tail)",
@@ -183,6 +185,24 @@ def roofline_of(flops, byts, seconds):
             "traffic": None, "algorithmic_flops": flops, "algorithmic_bytes": byts}
 
 
+def leg_counters(leg):
+    """HBM bytes and f64 MFMA flops per IPM iteration of a synthetic leg from
+    the newest committed probe profile (profiles/<round>_<leg>_profile.json,
+    tools/profile_round.sh + tools/profile_summary.py), or {}."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{leg}_profile.json")))
+    if not files:
+        return {}
+    d = json.load(open(files[-1]))
+    out = {"traffic_source": os.path.basename(files[-1])}
+    if "hbm_bytes_per_iteration" in d:
+        out["traffic"] = d["hbm_bytes_per_iteration"]
+    if d.get("mfma_util_over_kernel_time") is not None:
+        out["mfma_util"] = d["mfma_util_over_kernel_time"]
+        out["f64_mfma_flops_per_iteration"] = d.get("f64_mfma_flops_per_iteration")
+    return out
+
+
 def banded_leg(args):
     """BASELINE configs[3], banded variant: the whole HSD solve (factor +
     refined solves every iteration) on one GPU; it/s and the roofline
@@ -204,6 +224,7 @@ def banded_leg(args):
     flops, byts = survey_work(st, p.m, p.n, p.nz)
     roof = roofline_of(flops, byts, el / max(it, 1))
     roof["per"] = "IPM iteration (SURVEY.md 8(d) algorithmic work)"
+    roof.update(leg_counters("banded"))
     ph = {name: {"ms_per_iteration": stt["phase_ms"][i] / 5, "launches_per_iteration": stt["phase_launches"][i] / 5}
           for i, name in enumerate(ipo_amd.PHASES) if stt["phase_launches"][i]}
     return {"workload": BANDED_WORKLOAD, "value": it / el, "unit": "iterations/s", "n_gpus": 1,

@@ -1,5 +1,8 @@
 // dev_common.hip -- deterministic multi-job reductions (see dev_common.h).
 #include "dev_common.h"
+
+#include <algorithm>
+#include <cstdlib>
 #include "hip_util.h"
 
 namespace ipo {
@@ -179,6 +182,47 @@ void launch_link_ax(int mrow, int m, const int* kAt, const int* iAt, const doubl
                     hipStream_t st) {
     if (m <= mrow) return;
     hipLaunchKernelGGL(k_link_ax, dim3((m - mrow + 3) / 4), dim3(256), 0, st, mrow, m, kAt, iAt, At, x, out);
+    IPO_HIP_CHECK(hipGetLastError());
+}
+
+// Column-blocked row products (A x on CSR, row i summed over its columns in
+// ascending order like sparse_dot): pass b adds the entries of columns
+// [c0, c1) to the carried sum, so each pass gathers from one slice of x
+// that stays in the L2 of every XCD instead of a random line of all of x
+// per entry; the per-row sequence of additions is sparse_dot's, so the
+// result is bitwise the same.  pos[i] = first entry of row i not yet added.
+__global__ void __launch_bounds__(256)
+k_rows_ax_pass(int m, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
+               const double* __restrict__ x, int c1, int first, int* __restrict__ pos, double* __restrict__ ax) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= m) return;
+    int k = first ? kAt[i] : pos[i];
+    const int ke = kAt[i + 1];
+    double s = first ? 0.0 : ax[i];
+    for (; k < ke; k++) {
+        const int j = iAt[k];
+        if (j >= c1) break;
+        s += At[k] * x[j];
+    }
+    ax[i] = s;
+    pos[i] = k;
+}
+
+int rows_ax_blocks(int n) {
+    if (const char* e = std::getenv("IPO_HIP_AX_BLOCKS")) return std::max(1, std::atoi(e));
+    const long slice = kAxSliceBytes / static_cast<long>(sizeof(double));
+    return static_cast<int>((n + slice - 1) / slice);
+}
+
+void launch_rows_ax(int m, int n, int nblocks, const int* kAt, const int* iAt, const double* At, const double* x,
+                    int* pos, double* ax, hipStream_t st) {
+    if (m <= 0) return;
+    const int per = (n + nblocks - 1) / nblocks;
+    for (int b = 0; b < nblocks; b++) {
+        const int c1 = b + 1 == nblocks ? n : std::min(n, (b + 1) * per);
+        hipLaunchKernelGGL(k_rows_ax_pass, dim3((m + 255) / 256), dim3(256), 0, st, m, kAt, iAt, At, x, c1,
+                           b == 0 ? 1 : 0, pos, ax);
+    }
     IPO_HIP_CHECK(hipGetLastError());
 }
 

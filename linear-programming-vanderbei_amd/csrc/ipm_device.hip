@@ -363,6 +363,11 @@ IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A
     IPO_HIP_CHECK(hipEventCreateWithFlags(&ev_step_, hipEventDisableTiming));
     IPO_HIP_CHECK(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
     lax_.alloc(nforced_ > 0 ? nforced_ : 1);
+    axblocks_ = rows_ax_blocks(n_);
+    if (axblocks_ > 1) {
+        ax_.alloc(m_ > 0 ? m_ : 1);
+        axpos_.alloc(m_ > 0 ? m_ : 1);
+    }
     IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hs_), 16 * sizeof(double), hipHostMallocDefault));
     IPO_HIP_CHECK(hipStreamSynchronize(stream_));
     t_setup_ = now_s() - t0;
@@ -385,7 +390,13 @@ void IpmSolver::reduce(const RedJobs& j, int nout) {
     IPO_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
+void IpmSolver::row_ax(const double* x, hipStream_t st) {
+    if (xch_ || axblocks_ <= 1) return;
+    launch_rows_ax(m_, n_, axblocks_, kkt_->kAt(), kkt_->iAt(), kkt_->At(), x, axpos_.get(), ax_.get(), st);
+}
+
 void IpmSolver::link_ax(const double* x) {
+    row_ax(x, stream_);
     if (!xch_ || nforced_ == 0) return;
     launch_link_ax(m_ - nforced_, m_, kkt_->kAt(), kkt_->iAt(), kkt_->At(), x, lax_.get(), stream_);
     xsum(lax_.get(), nforced_, RedOp::Sum);
@@ -464,6 +475,7 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
             launch_reduce(j, part2_.get(), scal_.get(), side_);
             hipLaunchKernelGGL(k_hsd_mu, dim3(1), dim3(1), 0, side_, scal_.get(), static_cast<double>(ng_ + mg_ + 1), phi,
                                psi, iter > 0 ? 1 : 0);
+            row_ax(x_.get(), side_);
             hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, side_, m, n, K.kAt(), K.iAt(),
                                K.At(), K.kA(), K.iA(), K.A(), b_.get(), c_.get(), x_.get(), y_.get(), w_.get(), z_.get(),
                                phi, delta, 0.0, E_.get(), D_.get(), fy_.get(), fx_.get(), gy_.get(), gx_.get(),
@@ -789,15 +801,24 @@ void vector_bench(int m, int n, const int* kA, const int* iA, const double* A, i
     IPO_HIP_CHECK(hipEventCreate(&e0));
     IPO_HIP_CHECK(hipEventCreate(&e1));
     const int gv = static_cast<int>((N + NT - 1) / NT);
+    // the residuals as run_hsd forms them: A x column-blocked first when x
+    // exceeds one L2 slice (IpmSolver::row_ax), timed together
+    const int axb = rows_ax_blocks(n);
+    DevBuf<double> axv;
+    DevBuf<int> axpos;
+    if (axb > 1) { axv.alloc(m > 0 ? m : 1); axpos.alloc(m > 0 ? m : 1); }
     for (int kq = 0; kq < 3; kq++) {
         for (int r = -2; r < reps; r++) {                 // two untimed launches first
             if (r == 0) IPO_HIP_CHECK(hipEventRecord(e0, s));
-            if (kq == 0)
+            if (kq == 0) {
+                if (axb > 1) launch_rows_ax(m, n, axb, dkAt.get(), diAt.get(), dAt.get(), col(2), axpos.get(), axv.get(), s);
                 hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, dkAt.get(), diAt.get(),
                                    dAt.get(), dkA.get(), diA.get(), dA.get(), col(0) + n, col(1), col(2), col(3) + n,
                                    col(4) + n, col(5), 1.0, 0.5, 0.1, col(6) + n, col(7), col(8) + n, col(9),
-                                   col(10) + n, col(11), part, m, m, static_cast<const double*>(nullptr),
+                                   col(10) + n, col(11), part, axb > 1 ? 0 : m, m,
+                                   axb > 1 ? static_cast<const double*>(axv.get()) : static_cast<const double*>(nullptr),
                                    static_cast<const double*>(nullptr));
+            }
             else if (kq == 1)
                 hipLaunchKernelGGL(k_hsd_directions, dim3(kRedBlocks), dim3(NT), 0, s, m, n, dphi03.get(), 0.5, 0.1, col(9),
                                    col(11), col(8) + n, col(10) + n, col(2), col(5), col(3) + n, col(4) + n, col(7),

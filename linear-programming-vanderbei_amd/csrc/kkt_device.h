@@ -158,7 +158,7 @@ class KktDevice {
     // which in its own operation order catches exact cancellations; a
     // different summation order can leave a residue below one ulp of the
     // largest term instead).  1e-17 was chosen by sweeps over the netlib
-    // set (tools/kkt_emul.cpp on the host, tools/tau_sweep.py on the GPU):
+    // set (a host emulation of the GPU factor in round 1, tools/tau_sweep.py on the GPU):
     // 2^-46 over-flags twin-column pivots the reference keeps, exact zero
     // under-flags; 1e-17 matched the most hsd and intpt iteration counts.
     double pivot_tol_ = 1.0e-17;

@@ -3,9 +3,9 @@
 #include <cstdio>
 #include <string>
 #include <algorithm>
-#include "../kkt_plan.h"
-#include "../lp_io.h"
-#include "../synth.h"
+#include "kkt_plan.h"
+#include "lp_io.h"
+#include "synth.h"
 #include <cstdlib>
 
 int main(int argc, char** argv) {

@@ -5,7 +5,7 @@
 #   3. PMC passes, one counter group each (rocprofv3 does not split passes):
 #      FETCH_SIZE, WRITE_SIZE, and the f64 MFMA counters
 # Every step must exit 0 (no tolerance for a non-zero profiler exit).
-tag=${1:-r03}
+tag=${1:-r04}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 B="python3 bench.py --steps 2 --warmup 0 --cpu-iters 0 --block-angular off --hbm off --banded off"
@@ -17,9 +17,19 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUS
 # HBM traffic of the hbm_roofline leg's vector kernels (configs[3] uniform LP)
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${tag}_pmc_hfetch -o run -- python3 tools/hbm_probe.py 5 > gpurun_out/${tag}_pmc_hfetch.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${tag}_pmc_hwrite -o run -- python3 tools/hbm_probe.py 5 > gpurun_out/${tag}_pmc_hwrite.log 2>&1 || exit 1
+# the synthetic legs: BASELINE configs[3] banded and configs[4] block-angular
+# probes (5 HSD iterations each): kernel stats, FETCH / WRITE, f64 MFMA
+export PROBE_ITERS=5
+for leg in banded blockang; do
+  P="python3 tools/${leg}_probe.py $PROBE_ITERS 0"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${tag}_${leg}_trace -o run -- $P > gpurun_out/${tag}_${leg}_trace.log 2>&1 || exit 1
+  timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${tag}_${leg}_pmc_fetch -o run -- $P > gpurun_out/${tag}_${leg}_pmc_fetch.log 2>&1 || exit 1
+  timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${tag}_${leg}_pmc_write -o run -- $P > gpurun_out/${tag}_${leg}_pmc_write.log 2>&1 || exit 1
+  timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/${tag}_${leg}_pmc_mfma -o run -- $P > gpurun_out/${tag}_${leg}_pmc_mfma.log 2>&1 || exit 1
+done
 # the databases exceed what gpurun copies back: summarise here, keep the summaries
 mkdir -p gpurun_out/prof_${tag}
 python3 tools/profile_summary.py ${tag} gpurun_out gpurun_out/prof_${tag} || exit 1
 rm -rf gpurun_out/${tag}_trace gpurun_out/${tag}_pmc_fetch gpurun_out/${tag}_pmc_write gpurun_out/${tag}_pmc_mfma \
-       gpurun_out/${tag}_pmc_hfetch gpurun_out/${tag}_pmc_hwrite
+       gpurun_out/${tag}_pmc_hfetch gpurun_out/${tag}_pmc_hwrite gpurun_out/${tag}_banded_* gpurun_out/${tag}_blockang_*
 echo profile_round $tag done

@@ -12,6 +12,9 @@ FETCH_SIZE on gfx950 counts half of the bytes of wide streaming reads
 as reported.  Both are KB in rocprofv3.
   profiles/<tag>_tail_steps.json   k_tail_pr durations in dispatch order (the
                                     first 700: ten factorisations' look-ahead steps)
+  profiles/<tag>_{banded,blockang}_kernel_stats.csv, _profile.json
+                                    the synthetic legs' probes: kernel stats, HBM
+                                    bytes and f64 MFMA flops per IPM iteration
 usage: python tools/profile_summary.py r01 [gpurun_out] [profiles dir]"""
 import csv
 import json
@@ -152,6 +155,47 @@ if os.path.exists(hf):
         json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, tools/hbm_probe.py 5 (bench.py's "
                              "hbm_roofline kernels, BASELINE configs[3] uniform LP); FETCH_SIZE doubled (gfx950)",
                    "kernels": hk}, fh, indent=1)
+# the synthetic legs (BASELINE configs[3] banded, configs[4] block-angular):
+# kernel stats and HBM traffic / f64 MFMA per IPM iteration of a probe run
+# (tools/banded_probe.py, tools/blockang_probe.py, ITERS iterations, setup
+# uploads are copies, not kernels)
+for leg, probe in (("banded", "tools/banded_probe.py"), ("blockang", "tools/blockang_probe.py")):
+    tdb = os.path.join(src, f"{tag}_{leg}_trace", "run_results.db")
+    if not os.path.exists(tdb):
+        continue
+    iters = int(os.environ.get("PROBE_ITERS", "5"))
+    c2 = sqlite3.connect(tdb)
+    krows = list(c2.execute("select name, total_calls, total_duration, average, percentage from top_kernels "
+                            "order by total_duration desc"))
+    with open(os.path.join(dst, f"{tag}_{leg}_kernel_stats.csv"), "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["kernel", "calls", "total_us", "avg_us", "percent"])
+        for n, calls, tot, avg, pct in krows:
+            w.writerow([short(n), calls, f"{tot:.1f}", f"{avg:.2f}", f"{pct:.2f}"])
+    out = {"source": f"rocprofv3 --kernel-trace --stats / --pmc passes, python3 {probe} {iters} 0; FETCH_SIZE "
+                     f"doubled (gfx950); per IPM iteration = run total / {iters}",
+           "iterations": iters, "kernel_us_per_iteration": sum(r[2] for r in krows) / 1000.0 / iters}
+    f_ = os.path.join(src, f"{tag}_{leg}_pmc_fetch", "run_results.db")
+    w_ = os.path.join(src, f"{tag}_{leg}_pmc_write", "run_results.db")
+    if os.path.exists(f_) and os.path.exists(w_):
+        fe, wr = per_kernel(f_, "FETCH_SIZE"), per_kernel(w_, "WRITE_SIZE")
+        out["hbm_bytes_per_iteration"] = (2 * 1024 * sum(v for v, _ in fe.values())
+                                          + 1024 * sum(v for v, _ in wr.values())) / iters
+        top = {}
+        for k in sorted(set(fe) | set(wr), key=lambda k: -(fe.get(k, (0, 0))[0] * 2 + wr.get(k, (0, 0))[0]))[:12]:
+            top[k] = (2 * 1024 * fe.get(k, (0.0, 0))[0] + 1024 * wr.get(k, (0.0, 0))[0]) / iters
+        out["hbm_bytes_per_iteration_top_kernels"] = top
+    m_ = os.path.join(src, f"{tag}_{leg}_pmc_mfma", "run_results.db")
+    if os.path.exists(m_):
+        SIMDS, XCDS = 1024, 8
+        bu, mo, gu = (per_kernel(m_, k) for k in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_MFMA_MOPS_F64",
+                                                  "GRBM_GUI_ACTIVE"))
+        b = sum(v for v, _ in bu.values())
+        g = sum(v for v, _ in gu.values())
+        out["f64_mfma_flops_per_iteration"] = 512.0 * sum(v for v, _ in mo.values()) / iters
+        out["mfma_util_over_kernel_time"] = b / (g / XCDS * SIMDS) if g else None
+    with open(os.path.join(dst, f"{tag}_{leg}_profile.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
 line = [ln for ln in open(os.path.join(src, f"{tag}_bench.log")) if ln.startswith("{")][-1]
 with open(os.path.join(dst, f"{tag}_bench.json"), "w") as fh:
     fh.write(line)
