@@ -1742,6 +1742,252 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
     }
 }
 
+// The same chains with two 64-row blocks per workgroup ("pairs"): the
+// first block's z is handed to the second inside the workgroup (through LDS
+// after a barrier) instead of through memory, one hand-off per pair instead
+// of per block, while the first block's z is published at once for the
+// workgroups further down the chain.  Every entry sees the arithmetic of
+// k_tail_fwd_chain / k_tail_bwd_chain in the same order (the per-wave
+// partial sums over the earlier blocks, the internal block as their last
+// term, the same wave / column reductions and triangular solves): bitwise
+// the same sweep.  Forward: workgroup g owns blocks a = 2g, b = 2g + 1.
+constexpr size_t kPairFwdLds = 64 * 1024;                                   // dynamic pad: one per CU
+constexpr size_t kPairBwdLds = 2 * PC * (PC + 1) * sizeof(double);           // colsum scratch (R <= 2)
+
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_tail_fwd_pair(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, gran_t* __restrict__ gran,
+                unsigned epoch) {
+    extern __shared__ double lds_pad[];
+    __shared__ double Ls[2][PC][PC + 1];
+    __shared__ int lv[2][PC];
+    __shared__ double zb[R][PC];
+    __shared__ double red[R][4][64];
+    const int nt = tv.nt, tc = tv.tc, ntb = tv.ntb;
+    const int a = 2 * blockIdx.x, b = a + 1;
+    const bool hasb = b < ntb;
+    const int ka = a * PC, nca = min(PC, nt - ka), kb = b * PC, ncb = hasb ? min(PC, nt - kb) : 0;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    double eps[R], zown_a[R], zown_b[R];
+    load_eps<R>(epsp, eps);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        zown_a[r] = (wv == 0 && lane < nca) ? V.z[r * V.zs + tc + ka + lane] : 0.0;
+        zown_b[r] = (wv == 0 && lane < ncb) ? V.z[r * V.zs + tc + kb + lane] : 0.0;
+    }
+    if (tid == 0) lds_pad[0] = 0.0;
+    stage_l11(tv.S + ka + (size_t)ka * nt, nt, nca, Ls[0]);
+    if (hasb) stage_l11(tv.S + kb + (size_t)kb * nt, nt, ncb, Ls[1]);
+    if (tid < nca) lv[0][tid] = p.live[tc + ka + tid];
+    if (tid < ncb) lv[1][tid] = p.live[tc + kb + tid];
+    const int rowa = ka + (lane < nca ? lane : 0), rowb = kb + (lane < ncb ? lane : ka - kb);
+    double acca[R], accb[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) { acca[r] = 0.0; accb[r] = 0.0; }
+    for (int j = 0; j < a; j++) {
+        const size_t c0 = (size_t)(j * PC + wv * 16) * nt;
+        double ta[16], tb[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) { ta[q] = tv.S[rowa + c0 + (size_t)q * nt]; tb[q] = tv.S[rowb + c0 + (size_t)q * nt]; }
+        if (wv == 0) {
+            double zj[R];
+            gran_wait<R>(gran + (size_t)j * R * 128, epoch, lane, PC, zj);
+#pragma unroll
+            for (int r = 0; r < R; r++) zb[r][lane] = zj[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                acca[r] += ta[q] * zb[r][wv * 16 + q];
+                accb[r] += tb[q] * zb[r][wv * 16 + q];
+            }
+        }
+        __syncthreads();
+    }
+    // block b's term of block a (rows of b, columns of a): loaded before a's solve
+    double tba[16];
+    {
+        const size_t c0 = (size_t)(ka + wv * 16) * nt;
+#pragma unroll
+        for (int q = 0; q < 16; q++) tba[q] = tv.S[rowb + c0 + (size_t)q * nt];
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) red[r][wv][lane] = acca[r];
+    __syncthreads();
+    if (wv == 0) {
+        int bad[R] = {};
+        double zr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            zr[r] = lane < nca ? zown_a[r] - (((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane])
+                               : 0.0;
+        tri_lower<R>(zr, Ls[0], lv[0], nca, eps, bad);
+        if (lane < nca) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                gran_put(gran + (((size_t)a * R + r) * 64 + lane) * 2, epoch, zr[r]);
+                V.z[r * V.zs + tc + ka + lane] = zr[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) zb[r][lane] = lane < nca ? zr[r] : 0.0;
+        flag_bad<R>(p, bad);
+    }
+    if (!hasb) return;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+#pragma unroll
+        for (int r = 0; r < R; r++) accb[r] += tba[q] * zb[r][wv * 16 + q];
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) red[r][wv][lane] = accb[r];
+    __syncthreads();
+    if (wv == 0) {
+        int bad[R] = {};
+        double zr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            zr[r] = lane < ncb ? zown_b[r] - (((red[r][0][lane] + red[r][1][lane]) + red[r][2][lane]) + red[r][3][lane])
+                               : 0.0;
+        tri_lower<R>(zr, Ls[1], lv[1], ncb, eps, bad);
+        if (lane < ncb) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                gran_put(gran + (((size_t)b * R + r) * 64 + lane) * 2, epoch, zr[r]);
+                V.z[r * V.zs + tc + kb + lane] = zr[r];
+            }
+        }
+        flag_bad<R>(p, bad);
+    }
+}
+
+// Backward pairs, from the last block: workgroup g owns blocks hi = ntb - 1
+// - 2g and lo = hi - 1 (none for an odd count's first workgroup).
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_tail_bwd_pair(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, gran_t* __restrict__ gran,
+                unsigned epoch) {
+    extern __shared__ double lds_pad[];
+    __shared__ double Ls[2][PC][PC + 1];     // [0] block hi, [1] block lo; Ls[j][r] = L(j, r)
+    __shared__ int lv[2][PC];
+    __shared__ double zb[R][PC];
+    __shared__ double xs[R][PC];
+    const int nt = tv.nt, tc = tv.tc, ntb = tv.ntb;
+    const int hi = ntb - 1 - 2 * blockIdx.x, lo = hi - 1;
+    const bool haslo = lo >= 0;
+    const int kh = hi * PC, nch = min(PC, nt - kh), kl = haslo ? lo * PC : kh, ncl = haslo ? PC : 0;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    stage_l11(tv.S + kh + (size_t)kh * nt, nt, nch, Ls[0]);
+    if (haslo) stage_l11(tv.S + kl + (size_t)kl * nt, nt, ncl, Ls[1]);
+    if (tid < nch) lv[0][tid] = p.live[tc + kh + tid];
+    if (tid < ncl) lv[1][tid] = p.live[tc + kl + tid];
+    const int kq = wv * 16, nqh = min(16, nch - kq), nql = min(16, ncl - kq);
+    double eps[R], zdh[R], zdl[R];
+    int badh[R] = {}, badl[R] = {};
+    load_eps<R>(epsp, eps);
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        zdh[r] = (wv == 0 && lane < nch) ? dscale_rule(p, tc + kh + lane, V.z[r * V.zs + tc + kh + lane], eps[r], badh[r])
+                                         : 0.0;
+        zdl[r] = (wv == 0 && lane < ncl) ? dscale_rule(p, tc + kl + lane, V.z[r * V.zs + tc + kl + lane], eps[r], badl[r])
+                                         : 0.0;
+    }
+    double acch[R][16], accl[R][16];
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int q = 0; q < 16; q++) { acch[r][q] = 0.0; accl[r][q] = 0.0; }
+    for (int j = ntb - 1; j > hi; j--) {
+        const int r0 = j * PC, nr = min(PC, nt - r0);
+        const int rr = r0 + (lane < nr ? lane : 0);
+        const double* __restrict__ colh = tv.S + rr + (size_t)(kh + (nqh > 0 ? kq : 0)) * nt;
+        const double* __restrict__ coll = tv.S + rr + (size_t)(kl + (nql > 0 ? kq : 0)) * nt;
+        double th[16], tl[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            th[q] = colh[(size_t)min(q, max(nqh, 1) - 1) * nt];
+            tl[q] = coll[(size_t)min(q, max(nql, 1) - 1) * nt];
+        }
+        if (wv == 0) {
+            double zj[R];
+            gran_wait<R>(gran + (size_t)j * R * 128, epoch, lane, nr, zj);
+#pragma unroll
+            for (int r = 0; r < R; r++) zb[r][lane] = zj[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const double zr = lane < nr ? zb[r][lane] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                acch[r][q] += th[q] * zr;
+                accl[r][q] += tl[q] * zr;
+            }
+        }
+        __syncthreads();
+    }
+    // block lo's term of block hi (rows of hi, columns of lo): loaded before hi's solve
+    double tlh[16];
+    {
+        const int rr = kh + (lane < nch ? lane : 0);
+        const double* __restrict__ col = tv.S + rr + (size_t)(kl + (nql > 0 ? kq : 0)) * nt;
+#pragma unroll
+        for (int q = 0; q < 16; q++) tlh[q] = col[(size_t)min(q, max(nql, 1) - 1) * nt];
+    }
+    double* red = lds_pad;   // colsum scratch
+    if (hi < ntb - 1) {
+        if (nqh > 0) colsum_put<R>(red, acch, kq, nqh, lane);
+        __syncthreads();
+        if (tid < R * PC && tid % PC < nch) xs[tid / PC][tid % PC] = colsum_tree(red, tid / PC, tid % PC);
+        __syncthreads();
+    }
+    if (wv == 0) {
+        double zr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) zr[r] = lane < nch ? zdh[r] - (hi < ntb - 1 ? xs[r][lane] : 0.0) : 0.0;
+        tri_upper<R>(zr, Ls[0], lv[0], nch, eps, badh);
+        if (lane < nch) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                gran_put(gran + (((size_t)hi * R + r) * 64 + lane) * 2, epoch, zr[r]);
+                V.z[r * V.zs + tc + kh + lane] = zr[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) zb[r][lane] = zr[r];
+        flag_bad<R>(p, badh);
+    }
+    if (!haslo) return;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const double zr = lane < nch ? zb[r][lane] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) accl[r][q] += tlh[q] * zr;
+    }
+    if (nql > 0) colsum_put<R>(red, accl, kq, nql, lane);
+    __syncthreads();
+    if (tid < R * PC && tid % PC < ncl) xs[tid / PC][tid % PC] = colsum_tree(red, tid / PC, tid % PC);
+    __syncthreads();
+    if (wv == 0) {
+        double zr[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) zr[r] = lane < ncl ? zdl[r] - xs[r][lane] : 0.0;
+        tri_upper<R>(zr, Ls[1], lv[1], ncl, eps, badl);
+        if (lane < ncl) {
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                gran_put(gran + (((size_t)lo * R + r) * 64 + lane) * 2, epoch, zr[r]);
+                V.z[r * V.zs + tc + kl + lane] = zr[r];
+            }
+        }
+        flag_bad<R>(p, badl);
+    }
+}
+
 // ------------------------------------------- sync-free sweeps, top levels
 // The narrow top of the elimination tree (levels >= sf_level_, a few
 // supernodes each) in one persistent launch per direction instead of one or
@@ -2770,6 +3016,15 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
                                   reinterpret_cast<const void*>(&k_tail_bwd_chain<1>),
                                   reinterpret_cast<const void*>(&k_tail_bwd_chain<2>)})
                 IPO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
+            for (const void* f : {reinterpret_cast<const void*>(&k_tail_fwd_pair<1>),
+                                  reinterpret_cast<const void*>(&k_tail_fwd_pair<2>)})
+                IPO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kPairFwdLds));
+            for (const void* f : {reinterpret_cast<const void*>(&k_tail_bwd_pair<1>),
+                                  reinterpret_cast<const void*>(&k_tail_bwd_pair<2>)})
+                IPO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kPairBwdLds));
+            // two 64-row blocks per chain workgroup (IPO_HIP_CHAIN_PAIRS=1; default: one)
+            const char* cp = std::getenv("IPO_HIP_CHAIN_PAIRS");
+            chain_pairs_ = cp && std::atoi(cp) != 0;
         }
     }
 
@@ -3396,15 +3651,23 @@ void KktDevice::sweep(double* dz, const double* epsp) {
         hipLaunchKernelGGL(k_tail_gather<R>, dim3(ceil_div(plan_.nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(),
                            dyrow_idx_.get(), V);
         tail_rhs_end(dz, R);
-        hipLaunchKernelGGL(k_tail_fwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
-                           dChainGran_.get(), ++chain_epoch_);
+        if (chain_pairs_)
+            hipLaunchKernelGGL(k_tail_fwd_pair<R>, dim3((plan_.ntb + 1) / 2), dim3(NT), kPairFwdLds, s, pv, tv, V, epsp,
+                               dChainGran_.get(), ++chain_epoch_);
+        else
+            hipLaunchKernelGGL(k_tail_fwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
+                               dChainGran_.get(), ++chain_epoch_);
     }
     ph_end(kPhForward, fwd_launches_, s);
     ph_begin(s);
     if (plan_.nt > 0) {
         const TailView tv = tail_view();
-        hipLaunchKernelGGL(k_tail_bwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
-                           dChainGran_.get(), ++chain_epoch_);
+        if (chain_pairs_)
+            hipLaunchKernelGGL(k_tail_bwd_pair<R>, dim3((plan_.ntb + 1) / 2), dim3(NT), kPairBwdLds, s, pv, tv, V, epsp,
+                               dChainGran_.get(), ++chain_epoch_);
+        else
+            hipLaunchKernelGGL(k_tail_bwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
+                               dChainGran_.get(), ++chain_epoch_);
     }
     if (sf_level_ < plan_.nlevels) {
         const SfView sf{dsf_items_b_.get(), nsf_b_, dsf_bcnt_.get(), dsf_bflag_.get(), dsf_need_.get(), dsf_par_.get(),

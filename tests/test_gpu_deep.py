@@ -96,3 +96,29 @@ def test_hsd_trace_with_visit_schedule(name):
     with env(IPO_HIP_VISITS=1, IPO_HIP_GATHER_FLAT=1):
         status, text, st = ipo_amd.run_mps(mps_path(name), "hsd")
     check_hsd(name, text)
+
+
+def test_deep_schedule_envelope_banded():
+    """A banded LP whose minimum-degree tree is deep (m 20,000, n 100,000,
+    band 256: 468 levels; the order forced to minimum degree, which large LPs
+    no longer get by default, kkt_order_nd.cpp), solved with the deep-tree
+    schedule (visits and the forward pre-pass k_fwd_pre, on by default at
+    this depth) and without it (IPO_HIP_VISITS=0).  The pre-pass subtracts the
+    update values from below the narrow range first ((z - pre) - late), so the
+    forward sums are not bitwise the level path's: the two solves
+    are held to each other at the synthetic LPs' tolerance (same status,
+    iterations within +-1, final objectives within 1e-6 relative, HSD's stop
+    mu < 1e-12)."""
+    p = ipo_amd.synth_random(20000, 100000, 4, 256)
+    out = {}
+    for visits in (0, 1):
+        with env(IPO_HIP_ORDER="md", IPO_HIP_VISITS=visits):
+            r = ipo_amd.solver(p, "hsd")
+        assert r["stats"]["nlevels"] >= 256
+        out[visits] = r
+    a, b = out[0], out[1]
+    assert a["status"] == b["status"] == 0
+    assert abs(a["stats"]["iters"] - b["stats"]["iters"]) <= 1
+    for k in ("final_pobj", "final_dobj"):
+        assert abs(a["stats"][k] - b["stats"][k]) <= 1e-6 * max(1.0, abs(a["stats"][k]))
+    assert max(a["stats"]["final_mu"], b["stats"]["final_mu"]) < 1e-12

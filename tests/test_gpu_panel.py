@@ -106,3 +106,12 @@ def test_hsd_overlap_bitwise():
     (IPO_HIP_OVERLAP=0): the device mu / phi / psi / theta are the host's
     operations in the host's order, so the solves are identical."""
     assert _solve_env("IPO_HIP_OVERLAP", "0") == _solve_env("IPO_HIP_OVERLAP", "1")
+
+
+def test_tail_chain_pairs_bitwise():
+    """Dense-tail substitution chains with two 64-row blocks per workgroup
+    (k_tail_fwd_pair / k_tail_bwd_pair, default) against one block per
+    workgroup (IPO_HIP_CHAIN_PAIRS=0): the same arithmetic in the same order,
+    the first block's z handed on inside the workgroup -- identical dfl001
+    HSD solves (trace and final values)."""
+    assert _solve_env("IPO_HIP_CHAIN_PAIRS", "0") == _solve_env("IPO_HIP_CHAIN_PAIRS", "1")
