@@ -133,11 +133,9 @@ std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* 
     auto leaf = [&](Job& J) {
         std::vector<int>& v = J.nodes;
         // x-nodes first, then y-nodes, each in natural order
-        std::sort(v.begin(), v.end(), [&](int a, int b) {
-            const bool xa = a >= m, xb = b >= m;
-            if (xa != xb) return xa;
-            return a < b;
-        });
+        const auto mid = std::partition(v.begin(), v.end(), [&](int a) { return a >= m; });
+        std::sort(v.begin(), mid);
+        std::sort(mid, v.end());
         std::copy(v.begin(), v.end(), perm.begin() + J.lo);
     };
 
@@ -264,13 +262,22 @@ void symbolic_from_perm(KktOrdering& o, const int* kA, const int* iA, const int*
     const std::vector<int>& iperm = o.iperm;
     std::vector<int> Lp(T + 1, 0), Li;
     Li.reserve(static_cast<size_t>(kA[o.n]) * 4);
-    std::vector<int> mark(Tfree, -1), head(Tfree, -1), next(Tfree, -1);
+    std::vector<int> mark(Tfree, -1), head(Tfree, -1), next(Tfree, -1), rest;
     for (int j = 0; j < Tfree; j++) {
         const size_t start = Li.size();
         mark[j] = j;
         const int v = o.perm[j];
+        // the longest child's pattern below j is already sorted: it is merged
+        // with the sorted rest (K's entries, the other children) instead of
+        // sorting the whole column
+        int big = -1;
+        for (int c = head[j]; c >= 0; c = next[c])
+            if (big < 0 || Lp[c + 1] - Lp[c] > Lp[big + 1] - Lp[big]) big = c;
+        if (big >= 0)
+            for (int k = Lp[big] + 1; k < Lp[big + 1]; k++) mark[Li[k]] = j;   // Li[Lp[big]] == j
+        rest.clear();
         auto add = [&](int i) {
-            if (i > j && i < Tfree && mark[i] != j) { mark[i] = j; Li.push_back(i); }
+            if (i > j && i < Tfree && mark[i] != j) { mark[i] = j; rest.push_back(i); }
         };
         if (v < m) {
             for (int k = kAt[v]; k < kAt[v + 1]; k++) add(iperm[m + iAt[k]]);
@@ -281,10 +288,15 @@ void symbolic_from_perm(KktOrdering& o, const int* kA, const int* iA, const int*
                 if (iA[k] < mf) add(iperm[iA[k]]);
         }
         for (int c = head[j]; c >= 0; c = next[c])
-            for (int k = Lp[c]; k < Lp[c + 1]; k++) add(Li[k]);
-        std::sort(Li.begin() + start, Li.end());
-        if (Li.size() > static_cast<size_t>(INT32_MAX))
+            if (c != big)
+                for (int k = Lp[c]; k < Lp[c + 1]; k++) add(Li[k]);
+        std::sort(rest.begin(), rest.end());
+        const size_t nb = big >= 0 ? static_cast<size_t>(Lp[big + 1] - Lp[big] - 1) : 0;
+        if (start + nb + rest.size() > static_cast<size_t>(INT32_MAX))
             throw std::length_error("symbolic: more than 2^31 nonzeros in L");
+        Li.resize(start + nb + rest.size());
+        const int* bp = Li.data() + (big >= 0 ? Lp[big] + 1 : 0);
+        std::merge(bp, bp + nb, rest.begin(), rest.end(), Li.begin() + start);
         Lp[j + 1] = static_cast<int>(Li.size());
         if (Li.size() > start) {
             const int p = Li[start];

@@ -236,7 +236,8 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
     constexpr int kBitsNodes = 8192;
     int bw = 0;                                  // words per bit-matrix row (0: lists only)
     std::vector<uint64_t> bits;
-    std::vector<int> cidx(T, -1), cg;
+    std::vector<int> cidx(T, -1), gpos, miss;
+    std::vector<uint64_t> gmask;
     while (step < Tfree) {
         const int piv = hp.slot[1];
         const int dg = deg[piv];
@@ -298,19 +299,36 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
         for (size_t a = 0; complete && a < group.size(); a++) complete = deg[group[a]] == nsurv - 1;
         if (complete) {
         } else if (bw > 0) {
-            cg.resize(group.size());
-            for (size_t a = 0; a < group.size(); a++) cg[a] = cidx[group[a]];
+            // word-parallel: the group members after w that w is not adjacent
+            // to are gmask & ~row(w) (gmask: the members not processed yet);
+            // they are taken in group order, as the pairwise loop would
+            int wlo = bw, whi = -1;
             for (size_t a = 0; a < group.size(); a++) {
-                const int w = group[a], cw = cg[a];
+                const int c = cidx[group[a]];
+                gpos[c] = static_cast<int>(a);
+                gmask[c >> 6] |= 1ull << (c & 63);
+                wlo = std::min(wlo, c >> 6);
+                whi = std::max(whi, c >> 6);
+            }
+            for (size_t a = 0; a < group.size(); a++) {
+                const int w = group[a], cw = cidx[w];
+                gmask[cw >> 6] &= ~(1ull << (cw & 63));
                 uint64_t* row = bits.data() + static_cast<size_t>(cw) * bw;
-                for (size_t b = a + 1; b < group.size(); b++) {
-                    const int c2 = cg[b];
-                    if (!((row[c2 >> 6] >> (c2 & 63)) & 1ull)) {
-                        const int w2 = group[b];
-                        nb[w].push_back(w2); nb[w2].push_back(w); deg[w]++; deg[w2]++;
-                        row[c2 >> 6] |= 1ull << (c2 & 63);
-                        bits[static_cast<size_t>(c2) * bw + (cw >> 6)] |= 1ull << (cw & 63);
+                miss.clear();
+                for (int k = wlo; k <= whi; k++) {
+                    uint64_t x = gmask[k] & ~row[k];
+                    while (x) {
+                        const int c2 = (k << 6) + __builtin_ctzll(x);
+                        x &= x - 1;
+                        miss.push_back(gpos[c2]);
                     }
+                }
+                if (miss.size() > 1) std::sort(miss.begin(), miss.end());
+                for (int b : miss) {
+                    const int w2 = group[b], c2 = cidx[w2];
+                    nb[w].push_back(w2); nb[w2].push_back(w); deg[w]++; deg[w2]++;
+                    row[c2 >> 6] |= 1ull << (c2 & 63);
+                    bits[static_cast<size_t>(c2) * bw + (cw >> 6)] |= 1ull << (cw & 63);
                 }
             }
         } else {
@@ -340,6 +358,8 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
             const int R = Tfree - step;
             bw = (R + 63) / 64;
             bits.assign(static_cast<size_t>(R) * bw, 0ull);
+            gmask.assign(bw, 0ull);
+            gpos.assign(R, -1);
             int c = 0;
             for (int k = 1; k <= hp.count; k++) {
                 const int v = hp.slot[k];
@@ -356,9 +376,22 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
         }
     }
     o.denwin = denwin;
-    o.Li.resize(lrows.size());
-    for (size_t k = 0; k < lrows.size(); k++) o.Li[k] = iperm[lrows[k]];
-    for (int v = 0; v < Tfree; v++) std::sort(o.Li.begin() + o.Lp[v], o.Li.begin() + o.Lp[v + 1]);
+    // relabel and sort every column: bucket the entries by row (columns
+    // ascending inside a row), then deal the rows out in ascending order
+    {
+        const size_t nz = lrows.size();
+        std::vector<int> rptr(T + 1, 0), rcol(nz);
+        for (size_t k = 0; k < nz; k++) rptr[iperm[lrows[k]] + 1]++;
+        for (int v = 0; v < T; v++) rptr[v + 1] += rptr[v];
+        std::vector<int> fill(rptr.begin(), rptr.end() - 1);
+        for (int s = 0; s < Tfree; s++)
+            for (int k = o.Lp[s]; k < o.Lp[s + 1]; k++) rcol[fill[iperm[lrows[k]]]++] = s;
+        std::vector<int>().swap(lrows);
+        o.Li.resize(nz);
+        std::copy(o.Lp.begin(), o.Lp.end() - 1, fill.begin());
+        for (int r = 0; r < T; r++)
+            for (int k = rptr[r]; k < rptr[r + 1]; k++) o.Li[fill[rcol[k]]++] = r;
+    }
     if (nforced > 0) add_forced_tail(o, m, kA, iA, nforced);
     double na = 0.0;
     for (int v = 0; v < T; v++) { double c = o.Lp[v + 1] - o.Lp[v]; na += c * c; }

@@ -108,6 +108,12 @@ int main(int argc, char** argv) {
                        : order_tiered_min_degree(m, n, kA.data(), iA.data(), kAt.data(), iAt.data());
     std::printf("%s ordering %.2f s, narth %.3g\n", nd ? "nested-dissection" : "minimum-degree",
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(), o.narth);
+    {
+        unsigned long long h = 1469598103934665603ull;
+        for (const std::vector<int>* v : {&o.perm, &o.Lp, &o.Li})
+            for (int x : *v) { h ^= static_cast<unsigned>(x); h *= 1099511628211ull; }
+        std::printf("pattern hash %016llx\n", h);
+    }
     int tc = o.T;
     while (tc > 0 && o.Lp[tc] - o.Lp[tc - 1] == o.T - tc) tc--;
     std::printf("m %d n %d T %d lnz %d dense window %d\n", m, n, o.T, o.Lp[o.T], o.T - tc);
