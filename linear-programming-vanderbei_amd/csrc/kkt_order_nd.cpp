@@ -22,9 +22,13 @@
 // leaves: their x-nodes first (independent single-column supernodes), then
 // their y-nodes in natural order (one dense band segment, nested columns).
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
 #include <stdexcept>
+#include <thread>
 #include <vector>
 
 #include "kkt_plan.h"
@@ -98,9 +102,18 @@ std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* 
         }
     }
 
-    std::vector<int> inset(T, -1), dist(T, -1);
-    int stamp = 0;
-    std::vector<Job> stack;
+    // The pieces are independent: a pool of threads takes them from a shared
+    // list (large pieces) or a private stack (small ones).  Each piece's
+    // outcome depends only on its own node list and first index, so the
+    // permutation does not depend on the schedule.  Every thread marks the
+    // nodes of its piece in arrays of its own (stamps are unique per piece):
+    // shared mark arrays would have the threads' writes to neighbouring
+    // nodes of different pieces contend for the same cache lines.
+    std::atomic<int> stamp{0};
+    std::vector<Job> shared;
+    std::mutex mu;
+    std::condition_variable cv;
+    int busy = 0;
     {
         Job root;
         root.lo = 0;
@@ -109,142 +122,187 @@ std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* 
         for (int v : dense) isd[v] = 1;
         for (int v = 0; v < T; v++)
             if ((v < mf || v >= m) && !isd[v]) root.nodes.push_back(v);
-        stack.push_back(std::move(root));
+        shared.push_back(std::move(root));
     }
-    // BFS inside the set stamped `st`; fills dist (relative), returns the number of levels
-    auto bfs = [&](int src, int st, std::vector<int>& order) -> int {
-        order.clear();
-        order.push_back(src);
-        dist[src] = 0;
-        int nl = 1;
-        for (size_t h = 0; h < order.size(); h++) {
-            const int v = order[h], dv = dist[v];
-            for (int k = xadj[v]; k < xadj[v + 1]; k++) {
-                const int w = adj[k];
-                if (inset[w] == st && dist[w] < 0) {
-                    dist[w] = dv + 1;
-                    nl = std::max(nl, dv + 2);
-                    order.push_back(w);
-                }
-            }
-        }
-        return nl;
-    };
-    auto leaf = [&](Job& J) {
-        std::vector<int>& v = J.nodes;
-        // x-nodes first, then y-nodes, each in natural order
-        const auto mid = std::partition(v.begin(), v.end(), [&](int a) { return a >= m; });
-        std::sort(v.begin(), mid);
-        std::sort(mid, v.end());
-        std::copy(v.begin(), v.end(), perm.begin() + J.lo);
-    };
+    constexpr size_t kSharedMin = 16384;      // pieces at least this large go to the shared list
 
-    std::vector<int> order;
-    while (!stack.empty()) {
-        Job J = std::move(stack.back());
-        stack.pop_back();
-        const int size = static_cast<int>(J.nodes.size());
-        if (size == 0) continue;
-        int ny = 0;
-        for (int v : J.nodes) ny += v < m;
-        if (ny <= leaf_rows) { leaf(J); continue; }
-        const int st = ++stamp;
-        for (int v : J.nodes) { inset[v] = st; dist[v] = -1; }
-        // connected components: each its own piece (independent subtrees)
-        int nl = bfs(J.nodes[0], st, order);
-        if (static_cast<int>(order.size()) < size) {
-            std::vector<Job> comps;
-            int lo = J.lo;
-            auto take = [&]() {
-                Job c;
-                c.lo = lo;
-                c.nodes = order;
-                for (int w : order) inset[w] = -2;
-                lo += static_cast<int>(order.size());
-                comps.push_back(std::move(c));
-            };
-            take();
-            for (int v : J.nodes)
-                if (inset[v] == st) { bfs(v, st, order); take(); }
-            for (int v : J.nodes) { inset[v] = -1; dist[v] = -1; }
-            for (auto& c : comps) stack.push_back(std::move(c));
-            continue;
-        }
-        // pseudo-peripheral root: restart from a minimum-degree node of the
-        // last level while the eccentricity grows
-        int root = J.nodes[0];
-        for (int it = 0; it < 4; it++) {
-            int best = -1, bdeg = 0;
-            for (size_t q = order.size(); q-- > 0;) {
-                const int v = order[q];
-                if (dist[v] != nl - 1) break;
-                const int d = xadj[v + 1] - xadj[v];
-                if (best < 0 || d < bdeg) { best = v; bdeg = d; }
-            }
-            for (int v : order) dist[v] = -1;
-            const int nl2 = bfs(best, st, order);
-            if (nl2 > nl) { root = best; nl = nl2; continue; }
-            if (nl2 == nl) { root = best; break; }
-            for (int v : order) dist[v] = -1;     // shorter: back to the previous root
-            nl = bfs(root, st, order);
-            break;
-        }
-        // level sizes; y-levels are those of the root's class parity
-        std::vector<int> cnt(nl, 0);
-        for (int v : order) cnt[dist[v]]++;
-        const int ypar = root < m ? 0 : 1;
-        std::vector<long> before(nl + 1, 0);
-        for (int l = 0; l < nl; l++) before[l + 1] = before[l] + cnt[l];
-        int sep = -1;
-        {
-            long bestc = -1;
-            for (int l = 1; l + 1 < nl; l++) {
-                if (!hasq && (l & 1) != ypar) continue;
-                const long b = before[l], a = size - before[l + 1];
-                const long rest = b + a;
-                if (10 * std::min(a, b) < 3 * rest) continue;        // both sides >= 30 %
-                if (bestc < 0 || cnt[l] < bestc) { bestc = cnt[l]; sep = l; }
-            }
-            if (sep < 0) {        // no balanced y-level: the one nearest the median
-                long bd = -1;
-                for (int l = 1; l + 1 < nl; l++) {
-                    if (!hasq && (l & 1) != ypar) continue;
-                    const long d = std::labs(before[l] - (size - before[l + 1]));
-                    if (bd < 0 || d < bd) { bd = d; sep = l; }
-                }
-            }
-        }
-        if (sep < 0) {            // no interior y-level
-            for (int v : J.nodes) { inset[v] = -1; dist[v] = -1; }
-            leaf(J);
-            continue;
-        }
-        Job P1, P2;
-        std::vector<int> S;
-        for (int v : order) {
-            const int d = dist[v];
-            if (d < sep) P1.nodes.push_back(v);
-            else if (d > sep) P2.nodes.push_back(v);
-            else {
-                // a separator node with no neighbour beyond the separator
-                // belongs to the near side
-                bool far = false;
+    auto worker = [&]() {
+        std::vector<int> inset(T, -1), dist(T, -1), order;
+        auto inset_of = [&](int w) { return inset[w]; };
+        auto set_inset = [&](int w, int st) { inset[w] = st; };
+        std::vector<Job> local;
+        // BFS inside the set stamped `st`; fills dist (relative), returns the number of levels
+        auto bfs = [&](int src, int st, std::vector<int>& ord) -> int {
+            ord.clear();
+            ord.push_back(src);
+            dist[src] = 0;
+            int nl = 1;
+            for (size_t h = 0; h < ord.size(); h++) {
+                const int v = ord[h], dv = dist[v];
                 for (int k = xadj[v]; k < xadj[v + 1]; k++) {
                     const int w = adj[k];
-                    if (inset[w] == st && dist[w] == sep + 1) { far = true; break; }
+                    if (inset_of(w) == st && dist[w] < 0) {
+                        dist[w] = dv + 1;
+                        nl = std::max(nl, dv + 2);
+                        ord.push_back(w);
+                    }
                 }
-                if (far) S.push_back(v);
-                else P1.nodes.push_back(v);
+            }
+            return nl;
+        };
+        auto leaf = [&](Job& J) {
+            std::vector<int>& v = J.nodes;
+            // x-nodes first, then y-nodes, each in natural order
+            const auto mid = std::partition(v.begin(), v.end(), [&](int a) { return a >= m; });
+            std::sort(v.begin(), mid);
+            std::sort(mid, v.end());
+            std::copy(v.begin(), v.end(), perm.begin() + J.lo);
+        };
+        auto emit = [&](Job&& c) {
+            if (c.nodes.size() >= kSharedMin) {
+                std::lock_guard<std::mutex> g(mu);
+                shared.push_back(std::move(c));
+                cv.notify_one();
+            } else {
+                local.push_back(std::move(c));
+            }
+        };
+        // one piece: a leaf, its connected components, or two halves and a separator
+        auto split = [&](Job J) {
+            const int size = static_cast<int>(J.nodes.size());
+            if (size == 0) return;
+            int ny = 0;
+            for (int v : J.nodes) ny += v < m;
+            if (ny <= leaf_rows) { leaf(J); return; }
+            const int st = ++stamp;
+            for (int v : J.nodes) { set_inset(v, st); dist[v] = -1; }
+            // connected components: each its own piece (independent subtrees)
+            int nl = bfs(J.nodes[0], st, order);
+            if (static_cast<int>(order.size()) < size) {
+                std::vector<Job> comps;
+                int lo = J.lo;
+                auto take = [&]() {
+                    Job c;
+                    c.lo = lo;
+                    c.nodes = order;
+                    for (int w : order) set_inset(w, -2);
+                    lo += static_cast<int>(order.size());
+                    comps.push_back(std::move(c));
+                };
+                take();
+                for (int v : J.nodes)
+                    if (inset[v] == st) { bfs(v, st, order); take(); }
+                for (int v : J.nodes) { set_inset(v, -1); dist[v] = -1; }
+                for (auto& c : comps) emit(std::move(c));
+                return;
+            }
+            // pseudo-peripheral root: restart from a minimum-degree node of the
+            // last level while the eccentricity grows
+            int root = J.nodes[0];
+            for (int it = 0; it < 4; it++) {
+                int best = -1, bdeg = 0;
+                for (size_t q = order.size(); q-- > 0;) {
+                    const int v = order[q];
+                    if (dist[v] != nl - 1) break;
+                    const int d = xadj[v + 1] - xadj[v];
+                    if (best < 0 || d < bdeg) { best = v; bdeg = d; }
+                }
+                for (int v : order) dist[v] = -1;
+                const int nl2 = bfs(best, st, order);
+                if (nl2 > nl) { root = best; nl = nl2; continue; }
+                if (nl2 == nl) { root = best; break; }
+                for (int v : order) dist[v] = -1;     // shorter: back to the previous root
+                nl = bfs(root, st, order);
+                break;
+            }
+            // level sizes; y-levels are those of the root's class parity
+            std::vector<int> cnt(nl, 0);
+            for (int v : order) cnt[dist[v]]++;
+            const int ypar = root < m ? 0 : 1;
+            std::vector<long> before(nl + 1, 0);
+            for (int l = 0; l < nl; l++) before[l + 1] = before[l] + cnt[l];
+            int sep = -1;
+            {
+                long bestc = -1;
+                for (int l = 1; l + 1 < nl; l++) {
+                    if (!hasq && (l & 1) != ypar) continue;
+                    const long b = before[l], a = size - before[l + 1];
+                    const long rest = b + a;
+                    if (10 * std::min(a, b) < 3 * rest) continue;        // both sides >= 30 %
+                    if (bestc < 0 || cnt[l] < bestc) { bestc = cnt[l]; sep = l; }
+                }
+                if (sep < 0) {        // no balanced y-level: the one nearest the median
+                    long bd = -1;
+                    for (int l = 1; l + 1 < nl; l++) {
+                        if (!hasq && (l & 1) != ypar) continue;
+                        const long d = std::labs(before[l] - (size - before[l + 1]));
+                        if (bd < 0 || d < bd) { bd = d; sep = l; }
+                    }
+                }
+            }
+            if (sep < 0) {            // no interior y-level
+                for (int v : J.nodes) { set_inset(v, -1); dist[v] = -1; }
+                leaf(J);
+                return;
+            }
+            Job P1, P2;
+            std::vector<int> S;
+            // one allocation each (big vectors grown by doubling come and go
+            // through mmap / munmap, and every munmap stalls all threads)
+            P1.nodes.reserve(before[sep + 1]);
+            P2.nodes.reserve(size - before[sep + 1]);
+            for (int v : order) {
+                const int d = dist[v];
+                if (d < sep) P1.nodes.push_back(v);
+                else if (d > sep) P2.nodes.push_back(v);
+                else {
+                    // a separator node with no neighbour beyond the separator
+                    // belongs to the near side
+                    bool far = false;
+                    for (int k = xadj[v]; k < xadj[v + 1]; k++) {
+                        const int w = adj[k];
+                        if (inset_of(w) == st && dist[w] == sep + 1) { far = true; break; }
+                    }
+                    if (far) S.push_back(v);
+                    else P1.nodes.push_back(v);
+                }
+            }
+            for (int v : J.nodes) { set_inset(v, -1); dist[v] = -1; }
+            std::sort(S.begin(), S.end());
+            P1.lo = J.lo;
+            P2.lo = J.lo + static_cast<int>(P1.nodes.size());
+            std::copy(S.begin(), S.end(), perm.begin() + P2.lo + static_cast<int>(P2.nodes.size()));
+            emit(std::move(P2));
+            emit(std::move(P1));
+        };
+        for (;;) {
+            Job J;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return !shared.empty() || busy == 0; });
+                if (shared.empty()) return;            // nothing queued and nobody working: done
+                J = std::move(shared.back());
+                shared.pop_back();
+                busy++;
+            }
+            split(std::move(J));
+            while (!local.empty()) {
+                Job c = std::move(local.back());
+                local.pop_back();
+                split(std::move(c));
+            }
+            {
+                std::lock_guard<std::mutex> g(mu);
+                busy--;
+                if (busy == 0 && shared.empty()) cv.notify_all();
             }
         }
-        for (int v : J.nodes) { inset[v] = -1; dist[v] = -1; }
-        std::sort(S.begin(), S.end());
-        P1.lo = J.lo;
-        P2.lo = J.lo + static_cast<int>(P1.nodes.size());
-        std::copy(S.begin(), S.end(), perm.begin() + P2.lo + static_cast<int>(P2.nodes.size()));
-        stack.push_back(std::move(P2));
-        stack.push_back(std::move(P1));
-    }
+    };
+    const int nth = setup_threads();
+    std::vector<std::thread> pool;
+    for (int i = 1; i < nth; i++) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
     for (int v = 0; v < T; v++)
         if (perm[v] < 0) throw std::logic_error("nested dissection: incomplete permutation");
     return perm;

@@ -90,6 +90,9 @@ constexpr double kNdRelax = 0.1;      // explicit-zero fraction of a relaxed pan
 // Which order build_kkt_plan uses: IPO_HIP_ORDER = md | nd | auto (default:
 // nd from kNdMinNodes KKT nodes up); true = nested dissection
 bool use_nested_dissection(int T);
+// Host threads of the parallel setup steps (the nested-dissection pieces):
+// IPO_HIP_SETUP_THREADS, default min(16, hardware threads)
+int setup_threads();
 
 // One gather task into a 64x64 tile of the dense tail: the tail rows of
 // source panel `src` whose positions inside the tile's row block (rmask)

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
 
 namespace ipo {
 
@@ -140,6 +141,12 @@ bool use_nested_dissection(int T) {
     if (e && !std::strcmp(e, "md")) return false;
     if (e && !std::strcmp(e, "nd")) return true;
     return T >= kNdMinNodes;
+}
+
+int setup_threads() {
+    if (const char* e = std::getenv("IPO_HIP_SETUP_THREADS")) return std::max(1, std::atoi(e));
+    const int hw = static_cast<int>(std::thread::hardware_concurrency());
+    return std::max(1, std::min(16, hw));
 }
 
 KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
