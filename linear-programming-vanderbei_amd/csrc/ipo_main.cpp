@@ -38,6 +38,7 @@ int main(int argc, char** argv) {
         if (f) std::fclose(f);
     }
     ipo_hip_stats st;
+    std::memset(&st, 0, sizeof st);          // a run that stops before the solve fills none of it
     const int status = ipo_hip_run_mps_ex(argv[1], method, flags, solfile.empty() ? nullptr : solfile.c_str(), stdout,
                                           1, &st);
     std::fprintf(stderr,

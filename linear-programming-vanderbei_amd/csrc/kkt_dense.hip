@@ -1035,17 +1035,16 @@ constexpr int kVisitBlocks = 4;      // blocks per deferred trailing update of a
 // pass, S(bi, bj) -= sum_b L(bi, b) W(bj, b)', W = L D formed on the load
 // (no W array: bitwise the product the panel would store), the products summed
 // in the MFMA accumulators (k ascending inside a block, blocks ascending),
-// one read-modify-write of the tile for all of them.  Two blocks' operands
-// are in flight while a third is multiplied from LDS (the visits are bound by
-// their operand loads: ~5 us per block and workgroup with one block in
-// flight).  On a diagonal tile the |terms| of every block go to dscale (one
-// add).
+// one read-modify-write of the tile for all of them.  Block b + 1's operands
+// are loaded into registers while block b's are multiplied from LDS (two
+// blocks in flight measured no faster: tools/ubench_tail, round 4).  On a
+// diagonal tile the |terms| of every block go to dscale (one add).
 __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView& tv, int bi, int bj, int b0, int b1,
                                               SyrkLds& L) {
     const int nt = tv.nt, tid = threadIdx.x;
     constexpr int NU = TR * PC / PNT;
-    double va0[NU], vb0[NU], va1[NU], vb1[NU];
-    auto load = [&](int b, double (&va)[NU], double (&vb)[NU]) {
+    double va[NU], vb[NU];
+    auto load = [&](int b) {
         const int k0 = b * PC, nc = min(PC, nt - k0);
         const double* __restrict__ Lcol = tv.S + (size_t)k0 * nt;
 #pragma unroll
@@ -1068,9 +1067,8 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
 #pragma unroll
     for (int a = 0; a < 2; a++) acc[a] = (double4_t){0.0, 0.0, 0.0, 0.0};
     double as = 0.0;
-    // block b: operands from registers into LDS, block b + 2's loads issued
-    // into the freed registers, then block b's MFMA steps
-    auto step = [&](int b, double (&va)[NU], double (&vb)[NU]) {
+    load(b0);
+    for (int b = b0; b < b1; b++) {
 #pragma unroll
         for (int u = 0; u < NU; u++) {
             const int idx = tid + u * PNT;
@@ -1078,7 +1076,7 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
             L.Bs[idx % TR][idx / TR] = vb[u];
         }
         __syncthreads();
-        if (b + 2 < b1) load(b + 2, va, vb);
+        if (b + 1 < b1) load(b + 1);
 #pragma unroll
         for (int kk = 0; kk < PC; kk += 4) {
             double av[2];
@@ -1093,12 +1091,6 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
             for (int k = 0; k < nc; k++) as += fabs(L.As[tid][k] * L.Bs[tid][k]);
         }
         __syncthreads();
-    };
-    load(b0, va0, vb0);
-    if (b0 + 1 < b1) load(b0 + 1, va1, vb1);
-    for (int b = b0; b < b1; b += 2) {
-        step(b, va0, vb0);
-        if (b + 1 < b1) step(b + 1, va1, vb1);
     }
     double old[2][4];
 #pragma unroll

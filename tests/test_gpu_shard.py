@@ -206,7 +206,7 @@ def config4_one_process():
 def test_config4_full_size_one_process(config4_one_process):
     """(a) the whole LP in one process, linking rows forced into the dense tail."""
     p, st, stats, sol = config4_one_process
-    assert st == 0 and stats["final_mu"] < 1e-12      # HSD's stop, hsd.c:155
+    assert st == 0, st            # HSD's stop (mu < 1e-12 in its homogeneous variables, hsd.c:155) with phi > psi
     pr_, du, gap = certificate(p, *sol)
     assert pr_ < 1e-6 and du < 1e-6 and gap < 1e-6, (pr_, du, gap)
 

@@ -1,0 +1,85 @@
+// Microbenchmark of the dense tail's deferred trailing update (visit_tile512,
+// kkt_dense.hip; developer tool, not part of the library): G workgroups each
+// apply a chunk of `chunk` blocks to their own 64 x 64 tile of an nt x nt
+// tail, with the LDS footprint of the fused step kernel (one workgroup per
+// CU) or of the visit alone (two per CU); "same" makes every workgroup read
+// the operands of one tile (cache-resident: the compute + LDS bound).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off \
+//         -I linear-programming-vanderbei_amd/csrc tools/ubench_visit.hip -o tools/ubench_visit
+//   tools/ubench_visit [nt]
+#include "../linear-programming-vanderbei_amd/csrc/kkt_dense.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("%s: %s\n", #x, hipGetErrorString(e_)); std::exit(1); } } while (0)
+
+namespace ipo {
+
+// workgroup g -> tile g of the lower triangle of block columns >= c0 (or tile (c0, c0) for all: same)
+template <size_t LDSB>
+__global__ void __launch_bounds__(PNT) k_visit_bench(PlanView p, TailView tv, int c0, int b0, int b1, int same) {
+    __shared__ __attribute__((aligned(16))) char lds[LDSB];
+    int tile = blockIdx.x, c = c0;
+    if (!same)
+        while (tile >= tv.ntb - c) { tile -= tv.ntb - c; c++; }
+    else
+        tile = 0;
+    if (c >= tv.ntb) return;
+    visit_tile512(p, tv, c + tile, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
+}
+
+}  // namespace ipo
+
+int main(int argc, char** argv) {
+    const int nt = argc > 1 ? std::atoi(argv[1]) : 4441;
+    const int ntb = (nt + 63) / 64;
+    const size_t bytes = (size_t)nt * nt * sizeof(double);
+    double *dS, *ddg, *ddsc;
+    CK(hipMalloc(&dS, bytes)); CK(hipMalloc(&ddg, nt * 8)); CK(hipMalloc(&ddsc, nt * 8));
+    std::vector<double> S((size_t)nt * nt);
+    for (size_t i = 0; i < S.size(); i++) S[i] = 1e-3 * (double)((i * 2654435761u) % 1000) / 1000.0;
+    std::vector<double> g(nt, 1.0);
+    CK(hipMemcpy(dS, S.data(), bytes, hipMemcpyHostToDevice));
+    CK(hipMemcpy(ddg, g.data(), nt * 8, hipMemcpyHostToDevice));
+    CK(hipMemset(ddsc, 0, nt * 8));
+    ipo::PlanView pv{};
+    pv.dg = ddg; pv.dscale = ddsc; pv.tau = 1e-17;
+    ipo::TailView tv{};
+    tv.S = dS; tv.nt = nt; tv.ntb = ntb; tv.tc = 0;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    const int c0 = 20;        // columns 20.. : 50 + 49 + ... tiles available, blocks 0..19 as operands
+    const int maxg = (ntb - c0) * (ntb - c0 + 1) / 2;
+    std::printf("nt %d; visit of G tiles, chunk blocks each; us per launch (us per block)\n", nt);
+    for (int same = 0; same < 2; same++)
+        for (int big = 1; big >= 0; big--) {
+            std::printf("%s operands, LDS %s:\n", same ? "one tile's" : "own", big ? "of the step kernel (1 WG/CU)" : "of the visit (2 WG/CU)");
+            for (int chunk : {1, 2, 4, 8}) {
+                std::printf("  chunk %d:", chunk);
+                for (int G : {1, 16, 64, 128, 256, 384, 512, 768}) {
+                    if (G > maxg) continue;
+                    auto launch = [&]() {
+                        if (big)
+                            hipLaunchKernelGGL(ipo::k_visit_bench<ipo::kTailStepLds>, dim3(G), dim3(ipo::PNT), 0, 0, pv, tv, c0, 0, chunk, same);
+                        else
+                            hipLaunchKernelGGL(ipo::k_visit_bench<sizeof(ipo::SyrkLds)>, dim3(G), dim3(ipo::PNT), 0, 0, pv, tv, c0, 0, chunk, same);
+                    };
+                    launch();
+                    CK(hipDeviceSynchronize());
+                    const int reps = 20;
+                    CK(hipEventRecord(e0, 0));
+                    for (int r = 0; r < reps; r++) launch();
+                    CK(hipEventRecord(e1, 0));
+                    CK(hipEventSynchronize(e1));
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    const double us = 1e3 * ms / reps;
+                    std::printf("  G%d %.1f (%.2f)", G, us, us / chunk);
+                }
+                std::printf("\n");
+            }
+        }
+    return 0;
+}
