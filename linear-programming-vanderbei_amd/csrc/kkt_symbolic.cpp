@@ -243,8 +243,8 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
     constexpr int kBitsNodes = 8192;
     int bw = 0;                                  // words per bit-matrix row (0: lists only)
     std::vector<uint64_t> bits;
-    std::vector<int> cidx(T, -1), gpos, miss;
-    std::vector<uint64_t> gmask;
+    std::vector<int> cidx(T, -1), gpos;
+    std::vector<uint64_t> gmask, pmask;
     while (step < Tfree) {
         const int piv = hp.slot[1];
         const int dg = deg[piv];
@@ -306,9 +306,15 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
         for (size_t a = 0; complete && a < group.size(); a++) complete = deg[group[a]] == nsurv - 1;
         if (complete) {
         } else if (bw > 0) {
-            // word-parallel: the group members after w that w is not adjacent
-            // to are gmask & ~row(w) (gmask: the members not processed yet);
-            // they are taken in group order, as the pairwise loop would
+            // The pairwise loop below adds a missing pair (a, b), a before b
+            // in group order, at a's turn to both lists; whether it is
+            // missing depends only on the adjacency at the step's start.  So
+            // every member w gains exactly the members it was not adjacent
+            // to, in group order (those before it from their turns, those
+            // after it from its own).  Word-parallel here: the missing
+            // members of w are gmask & ~row(w) over the group's words; each
+            // list grows by its own appends only (no scattered pushes), and
+            // the rows take the whole clique afterwards.
             int wlo = bw, whi = -1;
             for (size_t a = 0; a < group.size(); a++) {
                 const int c = cidx[group[a]];
@@ -317,27 +323,42 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
                 wlo = std::min(wlo, c >> 6);
                 whi = std::max(whi, c >> 6);
             }
+            const size_t pw = (group.size() + 63) / 64;
+            if (pmask.size() < pw) pmask.resize(pw, 0ull);
             for (size_t a = 0; a < group.size(); a++) {
                 const int w = group[a], cw = cidx[w];
-                gmask[cw >> 6] &= ~(1ull << (cw & 63));
-                uint64_t* row = bits.data() + static_cast<size_t>(cw) * bw;
-                miss.clear();
+                const uint64_t* row = bits.data() + static_cast<size_t>(cw) * bw;
+                // missing members into a bit set over group positions,
+                // read back in position order (no sort)
+                int nmiss = 0;
                 for (int k = wlo; k <= whi; k++) {
                     uint64_t x = gmask[k] & ~row[k];
+                    if (k == (cw >> 6)) x &= ~(1ull << (cw & 63));
                     while (x) {
-                        const int c2 = (k << 6) + __builtin_ctzll(x);
+                        const int b = gpos[(k << 6) + __builtin_ctzll(x)];
+                        pmask[b >> 6] |= 1ull << (b & 63);
+                        nmiss++;
                         x &= x - 1;
-                        miss.push_back(gpos[c2]);
                     }
                 }
-                if (miss.size() > 1) std::sort(miss.begin(), miss.end());
-                for (int b : miss) {
-                    const int w2 = group[b], c2 = cidx[w2];
-                    nb[w].push_back(w2); nb[w2].push_back(w); deg[w]++; deg[w2]++;
-                    row[c2 >> 6] |= 1ull << (c2 & 63);
-                    bits[static_cast<size_t>(c2) * bw + (cw >> 6)] |= 1ull << (cw & 63);
+                if (nmiss == 0) continue;
+                for (size_t k = 0; k < pw; k++) {
+                    uint64_t x = pmask[k];
+                    pmask[k] = 0;
+                    while (x) {
+                        nb[w].push_back(group[(k << 6) + __builtin_ctzll(x)]);
+                        x &= x - 1;
+                    }
                 }
+                deg[w] += nmiss;
             }
+            for (size_t a = 0; a < group.size(); a++) {
+                const int cw = cidx[group[a]];
+                uint64_t* row = bits.data() + static_cast<size_t>(cw) * bw;
+                for (int k = wlo; k <= whi; k++) row[k] |= gmask[k];
+                row[cw >> 6] &= ~(1ull << (cw & 63));
+            }
+            for (int k = wlo; k <= whi; k++) gmask[k] = 0;
         } else {
             for (size_t a = 0; a < group.size(); a++) {
                 const int w = group[a];
