@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "row_ax.h"
+
 namespace ipo {
 
 constexpr int kRedBlocks = 256;    // fixed partial count -> reproducible sums
@@ -155,14 +157,6 @@ void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t s
 
 // Linking-row products of the sharded solve (exchange.h): out[i - mrow] =
 // sum_k At[k] x[iAt[k]] for rows mrow <= i < m (CSR of A), one wave per row.
-// A x by rows in column blocks of x-slices of kAxSliceBytes (bitwise
-// sparse_dot's sums, see k_rows_ax_pass): nblocks passes into ax[m]
-// (pos[m] scratch); rows_ax_blocks(n) = the passes for n columns
-// (IPO_HIP_AX_BLOCKS overrides; 1 = a single pass)
-constexpr long kAxSliceBytes = 2l << 20;
-int rows_ax_blocks(int n);
-void launch_rows_ax(int m, int n, int nblocks, const int* kAt, const int* iAt, const double* At, const double* x,
-                    int* pos, double* ax, hipStream_t st);
 void launch_link_ax(int mrow, int m, const int* kAt, const int* iAt, const double* At, const double* x, double* out,
                     hipStream_t st);
 

@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
+#include <vector>
 #include "hip_util.h"
 
 namespace ipo {
@@ -185,27 +187,31 @@ void launch_link_ax(int mrow, int m, const int* kAt, const int* iAt, const doubl
     IPO_HIP_CHECK(hipGetLastError());
 }
 
-// Column-blocked row products (A x on CSR, row i summed over its columns in
-// ascending order like sparse_dot): pass b adds the entries of columns
-// [c0, c1) to the carried sum, so each pass gathers from one slice of x
-// that stays in the L2 of every XCD instead of a random line of all of x
-// per entry; the per-row sequence of additions is sparse_dot's, so the
-// result is bitwise the same.  pos[i] = first entry of row i not yet added.
+// Column-sliced row products (A x, row i summed over its columns in
+// ascending order like sparse_dot): pass p adds the entries of the columns
+// of slice p to the carried sum, so each pass gathers from one slice of x
+// that stays in the L2 of every XCD instead of a random line of all of x per
+// entry; the per-row sequence of additions is sparse_dot's, so the result is
+// bitwise the same.  A slice's entries are stored by jagged diagonals (rows
+// of the slice by entry count, longest first; diagonal k = the k-th entry of
+// every row that has one, in that row order): thread r takes the r-th row of
+// the order and its k-th entry at dptr[k] + r, so the 64 lanes of a wave
+// read consecutive addresses (one row per lane on CSR would read 64 lines
+// per load) and run for about the same number of entries.
 __global__ void __launch_bounds__(256)
-k_rows_ax_pass(int m, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
-               const double* __restrict__ x, int c1, int first, int* __restrict__ pos, double* __restrict__ ax) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= m) return;
-    int k = first ? kAt[i] : pos[i];
-    const int ke = kAt[i + 1];
+k_rows_ax_jds(int rows, const int* __restrict__ perm, const int* __restrict__ dptr, const int* __restrict__ dlen,
+              int nd, const int* __restrict__ cols, const double* __restrict__ vals, const double* __restrict__ x,
+              int first, double* __restrict__ ax) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= rows) return;
+    const int i = perm[r];
     double s = first ? 0.0 : ax[i];
-    for (; k < ke; k++) {
-        const int j = iAt[k];
-        if (j >= c1) break;
-        s += At[k] * x[j];
+    for (int k = 0; k < nd; k++) {
+        if (r >= dlen[k]) break;
+        const int q = dptr[k] + r;
+        s += vals[q] * x[cols[q]];
     }
     ax[i] = s;
-    pos[i] = k;
 }
 
 int rows_ax_blocks(int n) {
@@ -214,14 +220,71 @@ int rows_ax_blocks(int n) {
     return static_cast<int>((n + slice - 1) / slice);
 }
 
-void launch_rows_ax(int m, int n, int nblocks, const int* kAt, const int* iAt, const double* At, const double* x,
-                    int* pos, double* ax, hipStream_t st) {
-    if (m <= 0) return;
-    const int per = (n + nblocks - 1) / nblocks;
-    for (int b = 0; b < nblocks; b++) {
-        const int c1 = b + 1 == nblocks ? n : std::min(n, (b + 1) * per);
-        hipLaunchKernelGGL(k_rows_ax_pass, dim3((m + 255) / 256), dim3(256), 0, st, m, kAt, iAt, At, x, c1,
-                           b == 0 ? 1 : 0, pos, ax);
+void RowAxPlan::build(int m, int n, const int* kA, const int* iA, const double* A, int npass, hipStream_t st) {
+    m_ = m;
+    np_ = std::max(1, npass);
+    const int per = (n + np_ - 1) / np_;
+    auto slice = [&](int j) { return per > 0 ? std::min(np_ - 1, j / per) : 0; };
+    // entries per (pass, row), the rows of each pass by count (descending,
+    // row order among equal counts), the diagonals
+    std::vector<int> cnt(static_cast<size_t>(np_) * m, 0);
+    for (int j = 0; j < n; j++)
+        for (int k = kA[j]; k < kA[j + 1]; k++) cnt[static_cast<size_t>(slice(j)) * m + iA[k]]++;
+    std::vector<int> perm(static_cast<size_t>(np_) * m), rank(static_cast<size_t>(np_) * m), dptr, dlen;
+    rows_.assign(np_, 0);
+    nd_.assign(np_, 0);
+    dbase_.assign(np_ + 1, 0);
+    long nz = 0;
+    for (int p = 0; p < np_; p++) {
+        const int* c = cnt.data() + static_cast<size_t>(p) * m;
+        int mx = 0;
+        for (int i = 0; i < m; i++) mx = std::max(mx, c[i]);
+        std::vector<int> bucket(mx + 2, 0);          // rows with count >= v start at bucket[mx - v]
+        for (int i = 0; i < m; i++) bucket[mx - c[i] + 1]++;
+        for (int v = 0; v <= mx; v++) bucket[v + 1] += bucket[v];
+        int* pp = perm.data() + static_cast<size_t>(p) * m;
+        int* rk = rank.data() + static_cast<size_t>(p) * m;
+        for (int i = 0; i < m; i++) { const int r = bucket[mx - c[i]]++; pp[r] = i; rk[i] = r; }
+        // pass 0 writes every row (a row with no entry in it gets 0); later
+        // passes only the rows that have entries in their slice
+        int active = 0;
+        while (active < m && c[pp[active]] > 0) active++;
+        rows_[p] = p == 0 ? m : active;
+        nd_[p] = mx;
+        for (int k = 0, len = active; k < mx; k++) {
+            while (len > 0 && c[pp[len - 1]] <= k) len--;
+            dptr.push_back(static_cast<int>(nz));
+            dlen.push_back(len);
+            nz += len;
+        }
+        dbase_[p + 1] = static_cast<int>(dptr.size());
+    }
+    if (nz > static_cast<long>(INT32_MAX)) throw std::length_error("row products: more than 2^31 entries");
+    std::vector<int> cols(nz), fill(static_cast<size_t>(np_) * m, 0);
+    std::vector<double> vals(nz);
+    for (int j = 0; j < n; j++) {
+        const int p = slice(j);
+        for (int k = kA[j]; k < kA[j + 1]; k++) {
+            const size_t pi = static_cast<size_t>(p) * m + iA[k];
+            const int q = dptr[dbase_[p] + fill[pi]++] + rank[pi];
+            cols[q] = j;
+            vals[q] = A[k];
+        }
+    }
+    perm_.upload(perm, st);
+    dptr_.upload(dptr, st);
+    dlen_.upload(dlen, st);
+    cols_.upload(cols, st);
+    vals_.upload(vals, st);
+    IPO_HIP_CHECK(hipStreamSynchronize(st));     // the host vectors go out of scope
+}
+
+void RowAxPlan::launch(const double* x, double* ax, hipStream_t st) const {
+    for (int p = 0; p < np_; p++) {
+        if (rows_[p] <= 0) continue;
+        hipLaunchKernelGGL(k_rows_ax_jds, dim3((rows_[p] + 255) / 256), dim3(256), 0, st, rows_[p],
+                           perm_.get() + static_cast<size_t>(p) * m_, dptr_.get() + dbase_[p], dlen_.get() + dbase_[p],
+                           nd_[p], cols_.get(), vals_.get(), x, p == 0 ? 1 : 0, ax);
     }
     IPO_HIP_CHECK(hipGetLastError());
 }

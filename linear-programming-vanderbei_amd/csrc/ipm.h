@@ -16,6 +16,7 @@
 #include "exchange.h"
 #include "hip_util.h"
 #include "kkt_device.h"
+#include "row_ax.h"
 
 namespace ipo {
 
@@ -84,12 +85,12 @@ class IpmSolver {
     const double* lax() const { return xch_ ? lax_.get() : axblocks_ > 1 ? ax_.get() : nullptr; }
     int mrow() const { return xch_ ? m_ - nforced_ : axblocks_ > 1 ? 0 : m_; }   // rows below are shard-local
     // A x of every row in column blocks whose x-slice fits one XCD's L2
-    // (launch_rows_ax; bitwise the residual kernels' own sums), when x is
+    // (RowAxPlan, row_ax.h; bitwise the residual kernels' own sums), when x is
     // larger than a slice and the solver is not sharded
     void row_ax(const double* x, hipStream_t st);
     int axblocks_ = 1;
     DevBuf<double> ax_;
-    DevBuf<int> axpos_;
+    RowAxPlan axplan_;
     void print_dims(FILE* tr) const;
 
     int m_, n_;

@@ -364,9 +364,9 @@ IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A
     IPO_HIP_CHECK(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
     lax_.alloc(nforced_ > 0 ? nforced_ : 1);
     axblocks_ = rows_ax_blocks(n_);
-    if (axblocks_ > 1) {
+    if (axblocks_ > 1 && !xch_) {
         ax_.alloc(m_ > 0 ? m_ : 1);
-        axpos_.alloc(m_ > 0 ? m_ : 1);
+        axplan_.build(m, n, kA, iA, A, axblocks_, stream_);
     }
     IPO_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hs_), 16 * sizeof(double), hipHostMallocDefault));
     IPO_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -392,7 +392,7 @@ void IpmSolver::reduce(const RedJobs& j, int nout) {
 
 void IpmSolver::row_ax(const double* x, hipStream_t st) {
     if (xch_ || axblocks_ <= 1) return;
-    launch_rows_ax(m_, n_, axblocks_, kkt_->kAt(), kkt_->iAt(), kkt_->At(), x, axpos_.get(), ax_.get(), st);
+    axplan_.launch(x, ax_.get(), st);
 }
 
 void IpmSolver::link_ax(const double* x) {
@@ -805,13 +805,13 @@ void vector_bench(int m, int n, const int* kA, const int* iA, const double* A, i
     // exceeds one L2 slice (IpmSolver::row_ax), timed together
     const int axb = rows_ax_blocks(n);
     DevBuf<double> axv;
-    DevBuf<int> axpos;
-    if (axb > 1) { axv.alloc(m > 0 ? m : 1); axpos.alloc(m > 0 ? m : 1); }
+    RowAxPlan axplan;
+    if (axb > 1) { axv.alloc(m > 0 ? m : 1); axplan.build(m, n, kA, iA, A, axb, s); }
     for (int kq = 0; kq < 3; kq++) {
         for (int r = -2; r < reps; r++) {                 // two untimed launches first
             if (r == 0) IPO_HIP_CHECK(hipEventRecord(e0, s));
             if (kq == 0) {
-                if (axb > 1) launch_rows_ax(m, n, axb, dkAt.get(), diAt.get(), dAt.get(), col(2), axpos.get(), axv.get(), s);
+                if (axb > 1) axplan.launch(col(2), axv.get(), s);
                 hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, dkAt.get(), diAt.get(),
                                    dAt.get(), dkA.get(), diA.get(), dA.get(), col(0) + n, col(1), col(2), col(3) + n,
                                    col(4) + n, col(5), 1.0, 0.5, 0.1, col(6) + n, col(7), col(8) + n, col(9),

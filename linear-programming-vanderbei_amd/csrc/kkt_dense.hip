@@ -711,7 +711,11 @@ struct PanelLds {
 // goes to wtail.
 __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __restrict__ fu_sup,
                                              const int* __restrict__ fu_j, int f0, const TailView& tv, int kb, int bid,
-                                             PanelLds& S, double* wtail, bool pre = false) {
+                                             PanelLds& S, double* wtail, bool pre = false,
+                                             const int* bailp = nullptr, int bt = 0) {
+    // a bail flag of an earlier step (dense tail, see k_tail_pr): read first,
+    // tested once this workgroup's operand loads are in flight
+    const int bailed = bailp ? *bailp : 0;
     double (*Ct)[CTS] = S.Ct;
     double (*Lr)[PC] = S.Lr;
     double (*Lb)[PC] = S.Lb;
@@ -760,6 +764,7 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
     double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
     double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
+    if (!pre && bailed && bailed - 1 < bt) return;
     if (pre) {
         // dense tail, block column kb > 0: block kb - 1's update of this
         // workgroup's rows, k_tail_syrk's MFMA fragments and order; the
@@ -786,6 +791,7 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
                 vj[u] = okj ? y : 0.0;
                 vw[u] = okd ? x * dk : 0.0;
             }
+            if (bailed && bailed - 1 < bt) return;     // workgroup-uniform
 #pragma unroll
             for (int u = 0; u < NU; u++) {
                 const int k = (tid + u * PNT) / TR;
@@ -954,10 +960,34 @@ k_panel_w(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu
 // + 31, columns 16 (w >> 1) .. + 15.  On a diagonal tile the |terms| go to
 // dscale as k_tail_syrk adds them.
 
+// k-major, row stride SKS = 80 doubles: a wave's MFMA operand read (16
+// consecutive rows x 4 k) puts the four k at bank offsets 0, 32, 0, 32 --
+// two lanes per bank, the minimum for 64 eight-byte reads -- and a store of
+// one k's 64 rows is conflict-free.  ([row][k] with stride 65 had up to four
+// lanes on a bank on the operand reads.)
+constexpr int SKS = PC + 16;
 struct SyrkLds {
-    double As[TR][PC + 1];
-    double Bs[TR][PC + 1];
+    double As[PC][SKS];
+    double Bs[PC][SKS];
 };
+
+// |terms| of a diagonal tile's pivots over one block: as += |L(r, k) W(r, k)|
+// for k = 0 .. nc - 1 in order (lane r = row r).  Sixteen products are read
+// and formed ahead of their adds, so the LDS latency is paid once per
+// sixteen terms instead of once per term (a rolled loop made the diagonal
+// tile the slowest workgroup of every step: ~2.7 us per block).
+__device__ __forceinline__ double diag_terms(const SyrkLds& L, int r, int nc, double as) {
+    int k = 0;
+    for (; k + 16 <= nc; k += 16) {
+        double pr[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) pr[u] = fabs(L.As[k + u][r] * L.Bs[k + u][r]);
+#pragma unroll
+        for (int u = 0; u < 16; u++) as += pr[u];
+    }
+    for (; k < nc; k++) as += fabs(L.As[k][r] * L.Bs[k][r]);
+    return as;
+}
 
 __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& tv, int kb, int bi, int bj,
                                              SyrkLds& L) {
@@ -979,8 +1009,8 @@ __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& 
 #pragma unroll
         for (int u = 0; u < TR * PC / PNT; u++) {
             const int idx = tid + u * PNT;
-            L.As[idx % TR][idx / TR] = va[u];
-            L.Bs[idx % TR][idx / TR] = vb[u];
+            L.As[idx / TR][idx % TR] = va[u];
+            L.Bs[idx / TR][idx % TR] = vb[u];
         }
     }
     __syncthreads();
@@ -994,8 +1024,8 @@ __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& 
     for (int kk = 0; kk < PC; kk += 4) {
         double av[2];
 #pragma unroll
-        for (int a = 0; a < 2; a++) av[a] = L.As[wr + a * 16 + li][kk + lk];
-        const double bv = L.Bs[wc + li][kk + lk];
+        for (int a = 0; a < 2; a++) av[a] = L.As[kk + lk][wr + a * 16 + li];
+        const double bv = L.Bs[kk + lk][wc + li];
 #pragma unroll
         for (int a = 0; a < 2; a++) acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv, acc[a], 0, 0, 0);
     }
@@ -1021,17 +1051,14 @@ __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& 
     if (diag_tile && tid < TR) {
         const int rg = bi * TR + tid;
         if (rg < nt) {
-            double as = 0.0;
-            for (int k = 0; k < nc; k++) as += fabs(L.As[tid][k] * L.Bs[tid][k]);
-            p.dscale[tv.tc + rg] += as;
+            p.dscale[tv.tc + rg] += diag_terms(L, tid, nc, 0.0);
         }
     }
 }
 
-constexpr int kVisitBlocks = 4;      // blocks per deferred trailing update of a tile
 
 // Deferred trailing update of the dense tail ("visit"): tile (bi, bj) of S
-// receives the updates of blocks b0 .. b1 - 1 (at most kVisitBlocks) in one
+// receives the updates of blocks b0 .. b1 - 1 (at most TailView::vk) in one
 // pass, S(bi, bj) -= sum_b L(bi, b) W(bj, b)', W = L D formed on the load
 // (no W array: bitwise the product the panel would store), the products summed
 // in the MFMA accumulators (k ascending inside a block, blocks ascending),
@@ -1040,7 +1067,10 @@ constexpr int kVisitBlocks = 4;      // blocks per deferred trailing update of a
 // blocks in flight measured no faster: tools/ubench_tail, round 4).  On a
 // diagonal tile the |terms| of every block go to dscale (one add).
 __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView& tv, int bi, int bj, int b0, int b1,
-                                              SyrkLds& L) {
+                                              SyrkLds& L, const int* bailp = nullptr, int bt = 0) {
+    // a bail flag of an earlier step (see k_tail_pr), read in the shadow of
+    // the first operand loads
+    const int bailed = bailp ? *bailp : 0;
     const int nt = tv.nt, tid = threadIdx.x;
     constexpr int NU = TR * PC / PNT;
     double va[NU], vb[NU];
@@ -1068,12 +1098,13 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
     for (int a = 0; a < 2; a++) acc[a] = (double4_t){0.0, 0.0, 0.0, 0.0};
     double as = 0.0;
     load(b0);
+    if (bailed && bailed - 1 < bt) return;
     for (int b = b0; b < b1; b++) {
 #pragma unroll
         for (int u = 0; u < NU; u++) {
             const int idx = tid + u * PNT;
-            L.As[idx % TR][idx / TR] = va[u];
-            L.Bs[idx % TR][idx / TR] = vb[u];
+            L.As[idx / TR][idx % TR] = va[u];
+            L.Bs[idx / TR][idx % TR] = vb[u];
         }
         __syncthreads();
         if (b + 1 < b1) load(b + 1);
@@ -1081,14 +1112,13 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
         for (int kk = 0; kk < PC; kk += 4) {
             double av[2];
 #pragma unroll
-            for (int a = 0; a < 2; a++) av[a] = L.As[wr + a * 16 + li][kk + lk];
-            const double bv = L.Bs[wc + li][kk + lk];
+            for (int a = 0; a < 2; a++) av[a] = L.As[kk + lk][wr + a * 16 + li];
+            const double bv = L.Bs[kk + lk][wc + li];
 #pragma unroll
             for (int a = 0; a < 2; a++) acc[a] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv, acc[a], 0, 0, 0);
         }
         if (diag_tile && tid < TR) {
-            const int nc = min(PC, nt - b * PC);
-            for (int k = 0; k < nc; k++) as += fabs(L.As[tid][k] * L.Bs[tid][k]);
+            as = diag_terms(L, tid, min(PC, nt - b * PC), as);
         }
         __syncthreads();
     }
@@ -1117,7 +1147,7 @@ constexpr size_t kTailStepLds0 = sizeof(PanelLds) > sizeof(SyrkLds) ? sizeof(Pan
 constexpr size_t kTailStepLds = kTailStepLds0 > sizeof(PreLds) ? kTailStepLds0 : sizeof(PreLds);
 
 // Visits of launch t (tail_visit_cols): block column c receives the updates
-// of blocks 0 .. c - 2 in chunks of kVisitBlocks, the latest chunk in launch
+// of blocks 0 .. c - 2 in chunks of K = TailView::vk, the latest chunk in launch
 // c - 1, the one before in launch c - 2, ...: launch c - 1 - k applies blocks
 // [c - 1 - 4 (k + 1), c - 1 - 4 k) (clipped at 0) -- every block available
 // (b < t) and every column done before its panel, block c - 1 being the
@@ -1125,7 +1155,7 @@ constexpr size_t kTailStepLds = kTailStepLds0 > sizeof(PreLds) ? kTailStepLds0 :
 // order; the work is spread over the launches (late-as-possible, so the
 // early steps, once 3x the panel's time under the right-looking update, are
 // panel-bound) and a tile is read and written once per chunk, not per block.
-__host__ __device__ __forceinline__ int visit_hi(int t, int c) { return c - 1 - kVisitBlocks * (c - 1 - t); }
+__host__ __device__ __forceinline__ int visit_hi(int t, int c, int K) { return c - 1 - K * (c - 1 - t); }
 
 // Step t of the look-ahead dense-tail factorisation, one launch:
 //   workgroups [0, gp):  panel of block column t (k_panel_w's body);
@@ -1140,16 +1170,15 @@ k_tail_pr(PlanView p, TailView tv, int t, int gp) {
     // a panel of an earlier step bailed (flags[2] = 1 + its block column;
     // not this launch's own, whose visits must complete): the host
     // resumes the look-ahead from there
-    const int bailed = p.flags[2];
-    if (bailed && bailed - 1 < t) return;
     if ((int)blockIdx.x < gp) {
-        panel_w_body(p, nullptr, nullptr, 0, tv, t, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), nullptr, t > 0);
+        panel_w_body(p, nullptr, nullptr, 0, tv, t, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), nullptr, t > 0,
+                     p.flags + 2, t);
         return;
     }
     int tile = blockIdx.x - gp, c = t + 1;
     while (tile >= tv.ntb - c) { tile -= tv.ntb - c; c++; }
-    const int b1 = visit_hi(t, c);
-    visit_tile512(p, tv, c + tile, c, max(0, b1 - kVisitBlocks), b1, *reinterpret_cast<SyrkLds*>(lds));
+    const int b1 = visit_hi(t, c, tv.vk);
+    visit_tile512(p, tv, c + tile, c, max(0, b1 - tv.vk), b1, *reinterpret_cast<SyrkLds*>(lds), p.flags + 2, t);
 }
 
 // Block t's update of block column t + 1 only (tiles (bi, t + 1), bi > t):
@@ -1224,17 +1253,17 @@ k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count) {
 
 }  // namespace
 
-int tail_visit_tiles(int ntb, int t) {
+int tail_visit_tiles(int ntb, int t, int K) {
     int n = 0;
-    for (int c = t + 1; c < ntb && visit_hi(t, c) > 0; c++) n += ntb - c;
+    for (int c = t + 1; c < ntb && visit_hi(t, c, K) > 0; c++) n += ntb - c;
     return t > 0 ? n : 0;
 }
 
-void tail_visit_work(int ntb, int nt, double& flops, double& bytes) {
+void tail_visit_work(int ntb, int nt, int K, double& flops, double& bytes) {
     flops = bytes = 0.0;
     for (int t = 1; t < ntb; t++)
-        for (int c = t + 1; c < ntb && visit_hi(t, c) > 0; c++) {
-            const int b1 = visit_hi(t, c), b0 = std::max(0, b1 - kVisitBlocks);
+        for (int c = t + 1; c < ntb && visit_hi(t, c, K) > 0; c++) {
+            const int b1 = visit_hi(t, c, K), b0 = std::max(0, b1 - K);
             for (int bi = c; bi < ntb; bi++) {
                 const double rows = std::min(TR, nt - bi * TR), cols = std::min(TR, nt - c * TR);
                 for (int b = b0; b < b1; b++) {
@@ -1250,7 +1279,7 @@ void tail_visit_work(int ntb, int nt, double& flops, double& bytes) {
 void launch_tail_step(const PlanView& pv, const TailView& tv, int t, hipStream_t s) {
     const int h = tv.nt - t * PC;
     const int gp = std::max(1, (h + TR - 1) / TR - 1);
-    const int nr = tail_visit_tiles(tv.ntb, t);
+    const int nr = tail_visit_tiles(tv.ntb, t, tv.vk);
     hipLaunchKernelGGL(k_tail_pr, dim3(gp + nr), dim3(PNT), 0, s, pv, tv, t, gp);
 }
 

@@ -21,12 +21,16 @@
 namespace ipo {
 
 // Device view of the dense tail (see kkt_plan.h): S = nt x nt column-major.
+// Blocks per visit of the look-ahead dense tail (kkt_dense.hip, visit_hi):
+// IPO_HIP_VISIT_BLOCKS overrides.
+constexpr int kTailVisitBlocks = 4;
 struct TailView {
     double* S;
     int nt, ntb, tc;
     const int* task_ptr;
     const TailTask* tasks;
     double* W;        // nt x 64 workspace: L21 * D of the current block column
+    int vk = kTailVisitBlocks;   // blocks per deferred trailing update (visit) of a tile
 };
 
 // Device-time phases of the KKT core (timing mode), with the algorithmic
@@ -242,6 +246,7 @@ class KktDevice {
     DevBuf<SlotRec> dslot_rec_, dtail_slot_rec_;   // per gather k-slot record (sparse units, dense tail)
     DevBuf<unsigned long long> dChainGran_;   // dense-tail sweep chains: z of every block as epoch-tagged granules
     int chain_epoch_ = 0;      // the chains' launch epoch (one per launch, never reused)
+    int visit_blocks_ = kTailVisitBlocks;   // TailView::vk (IPO_HIP_VISIT_BLOCKS)
     bool chain_pairs_ = false; // dense-tail chains with two blocks per workgroup (k_tail_fwd_pair / _bwd_pair)
     DevBuf<int> dtail_task_ptr_, dtail_kslot_, dtail_kslot_ptr_;
     DevBuf<uint64_t> dtail_tasks_, dutasks_;

@@ -3027,6 +3027,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             chain_pairs_ = cp && std::atoi(cp) != 0;
         }
     }
+    if (const char* vb = std::getenv("IPO_HIP_VISIT_BLOCKS")) visit_blocks_ = std::max(1, std::atoi(vb));
 
     mark("dLx_.alloc(plan_.lx_size > 0");
     dLx_.alloc(plan_.lx_size > 0 ? plan_.lx_size : 1);
@@ -3278,6 +3279,7 @@ TailView KktDevice::tail_view() const {
     t.task_ptr = dtail_task_ptr_.get();
     t.tasks = reinterpret_cast<const TailTask*>(dtail_tasks_.get());
     t.W = dW_.get();
+    t.vk = visit_blocks_;
     return t;
 }
 

@@ -65,10 +65,10 @@ void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0
 // the deferred trailing updates ("visits") scheduled for launch t -- one
 // launch per block column.  W = L21 D is formed from L and D where used.
 void launch_tail_step(const PlanView& pv, const TailView& tv, int t, hipStream_t s);
-// visit tiles of launch t (tail of ntb block columns)
-int tail_visit_tiles(int ntb, int t);
+// visit tiles of launch t (tail of ntb block columns, chunks of K blocks)
+int tail_visit_tiles(int ntb, int t, int K);
 // algorithmic flops / bytes of every visit of one factorisation
-void tail_visit_work(int ntb, int nt, double& flops, double& bytes);
+void tail_visit_work(int ntb, int nt, int K, double& flops, double& bytes);
 // Repair path, block column kb of the dense tail with the dependent-pivot
 // rule: one round (k_tail_dep); sti = two copies of {k0, 1 + pending column,
 // done, ndep}, both zeroed before round 0; round r reads copy r & 1 and

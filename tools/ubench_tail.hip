@@ -44,6 +44,7 @@ int main(int argc, char** argv) {
     pv.dg = ddg; pv.live = dlive; pv.flags = dflags; pv.sign = dsign; pv.dscale = ddsc; pv.tau = 1e-17;
     ipo::TailView tv{};
     tv.S = dS; tv.nt = nt; tv.ntb = ntb; tv.tc = 0; tv.W = dW;
+    if (const char* vb = std::getenv("IPO_HIP_VISIT_BLOCKS")) tv.vk = std::atoi(vb);
     std::vector<hipEvent_t> ev(ntb + 1);
     for (auto& e : ev) CK(hipEventCreate(&e));
     std::vector<double> step_us(ntb, 0.0);
@@ -72,6 +73,7 @@ int main(int argc, char** argv) {
     int fl[4];
     CK(hipMemcpy(fl, dflags, 16, hipMemcpyDeviceToHost));
     const double flops = (double)nt * nt * nt / 3.0;
+    std::printf("visit chunk %d; ", tv.vk);
     std::printf("nt %d (%d block columns): %.3f ms per factor, %.2f TFLOP/s of nt^3/3, bail flags %d %d %d\n", nt, ntb,
                 total / reps, flops / (total / reps * 1e-3) / 1e12, fl[0], fl[1], fl[2]);
     std::printf("per step (us):");

@@ -17,17 +17,19 @@
 
 namespace ipo {
 
-// workgroup g -> tile g of the lower triangle of block columns >= c0 (or tile (c0, c0) for all: same)
+// workgroup g -> tile g of the lower triangle of block columns >= c0 (or
+// tile (c0 + 1, c0) for all: same); offd: strictly below the diagonal only
 template <size_t LDSB>
-__global__ void __launch_bounds__(PNT) k_visit_bench(PlanView p, TailView tv, int c0, int b0, int b1, int same) {
+__global__ void __launch_bounds__(PNT) k_visit_bench(PlanView p, TailView tv, int c0, int b0, int b1, int same,
+                                                     int offd) {
     __shared__ __attribute__((aligned(16))) char lds[LDSB];
     int tile = blockIdx.x, c = c0;
     if (!same)
-        while (tile >= tv.ntb - c) { tile -= tv.ntb - c; c++; }
+        while (tile >= tv.ntb - c - offd) { tile -= tv.ntb - c - offd; c++; }
     else
         tile = 0;
     if (c >= tv.ntb) return;
-    visit_tile512(p, tv, c + tile, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
+    visit_tile512(p, tv, c + offd + tile, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
 }
 
 }  // namespace ipo
@@ -53,33 +55,39 @@ int main(int argc, char** argv) {
     const int c0 = 20;        // columns 20.. : 50 + 49 + ... tiles available, blocks 0..19 as operands
     const int maxg = (ntb - c0) * (ntb - c0 + 1) / 2;
     std::printf("nt %d; visit of G tiles, chunk blocks each; us per launch (us per block)\n", nt);
-    for (int same = 0; same < 2; same++)
-        for (int big = 1; big >= 0; big--) {
-            std::printf("%s operands, LDS %s:\n", same ? "one tile's" : "own", big ? "of the step kernel (1 WG/CU)" : "of the visit (2 WG/CU)");
-            for (int chunk : {1, 2, 4, 8}) {
-                std::printf("  chunk %d:", chunk);
-                for (int G : {1, 16, 64, 128, 256, 384, 512, 768}) {
-                    if (G > maxg) continue;
-                    auto launch = [&]() {
-                        if (big)
-                            hipLaunchKernelGGL(ipo::k_visit_bench<ipo::kTailStepLds>, dim3(G), dim3(ipo::PNT), 0, 0, pv, tv, c0, 0, chunk, same);
-                        else
-                            hipLaunchKernelGGL(ipo::k_visit_bench<sizeof(ipo::SyrkLds)>, dim3(G), dim3(ipo::PNT), 0, 0, pv, tv, c0, 0, chunk, same);
-                    };
-                    launch();
-                    CK(hipDeviceSynchronize());
-                    const int reps = 20;
-                    CK(hipEventRecord(e0, 0));
-                    for (int r = 0; r < reps; r++) launch();
-                    CK(hipEventRecord(e1, 0));
-                    CK(hipEventSynchronize(e1));
-                    float ms = 0;
-                    CK(hipEventElapsedTime(&ms, e0, e1));
-                    const double us = 1e3 * ms / reps;
-                    std::printf("  G%d %.1f (%.2f)", G, us, us / chunk);
-                }
-                std::printf("\n");
+    struct Mode { int same, big, offd; const char* what; };
+    const Mode modes[] = {{0, 1, 0, "own operands, diagonal tiles included"},
+                          {0, 1, 1, "own operands, below the diagonal only"},
+                          {1, 1, 1, "one off-diagonal tile's operands (cache-resident)"},
+                          {0, 0, 1, "own operands, below the diagonal, LDS of the visit alone"}};
+    for (const Mode& md : modes) {
+        std::printf("%s:\n", md.what);
+        for (int chunk : {1, 4, 8}) {
+            std::printf("  chunk %d:", chunk);
+            for (int G : {1, 64, 256, 384, 512}) {
+                if (G > maxg) continue;
+                auto launch = [&]() {
+                    if (md.big)
+                        hipLaunchKernelGGL(ipo::k_visit_bench<ipo::kTailStepLds>, dim3(G), dim3(ipo::PNT), 0, 0, pv, tv, c0, 0,
+                                           chunk, md.same, md.offd);
+                    else
+                        hipLaunchKernelGGL(ipo::k_visit_bench<sizeof(ipo::SyrkLds)>, dim3(G), dim3(ipo::PNT), 0, 0, pv, tv, c0,
+                                           0, chunk, md.same, md.offd);
+                };
+                launch();
+                CK(hipDeviceSynchronize());
+                const int reps = 20;
+                CK(hipEventRecord(e0, 0));
+                for (int r = 0; r < reps; r++) launch();
+                CK(hipEventRecord(e1, 0));
+                CK(hipEventSynchronize(e1));
+                float ms = 0;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                const double us = 1e3 * ms / reps;
+                std::printf("  G%d %.1f (%.2f)", G, us, us / chunk);
             }
+            std::printf("\n");
         }
+    }
     return 0;
 }
