@@ -66,7 +66,23 @@ __device__ __forceinline__ double sparse_dot(int kb, int ke, const double* __res
 #pragma unroll
         for (int u = 0; u < 16; u++) s += a[u] * b[u];
     }
-    for (; k < ke; k++) s += v[k] * x[idx[k]];
+    // the rest (< 16 entries: every column of a typical LP) the same way,
+    // masked, so its loads are in flight together too (one dependent pair
+    // of loads per entry made short rows latency-bound)
+    const int rem = ke - k;
+    if (rem > 0) {
+        int ix[16];
+        double a[16], b[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (u < rem) { ix[u] = idx[k + u]; a[u] = v[k + u]; }
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (u < rem) b[u] = x[ix[u]];
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+            if (u < rem) s += a[u] * b[u];
+    }
     return s;
 }
 

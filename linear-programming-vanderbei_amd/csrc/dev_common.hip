@@ -206,10 +206,29 @@ k_rows_ax_jds(int rows, const int* __restrict__ perm, const int* __restrict__ dp
     if (r >= rows) return;
     const int i = perm[r];
     double s = first ? 0.0 : ax[i];
-    for (int k = 0; k < nd; k++) {
+    // eight diagonals at a time, their loads in flight together (the row's
+    // entries still added in order); a row has entry k iff r < dlen[k], and
+    // dlen does not increase with k
+    for (int k = 0; k < nd; k += 8) {
         if (r >= dlen[k]) break;
-        const int q = dptr[k] + r;
-        s += vals[q] * x[cols[q]];
+        int c[8];
+        double a[8], b[8];
+        bool ok[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            ok[u] = k + u < nd && r < dlen[k + u];
+            if (ok[u]) {
+                const int q = dptr[k + u] + r;
+                c[u] = cols[q];
+                a[u] = vals[q];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (ok[u]) b[u] = x[c[u]];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (ok[u]) s += a[u] * b[u];
     }
     ax[i] = s;
 }
@@ -218,6 +237,11 @@ int rows_ax_blocks(int n) {
     if (const char* e = std::getenv("IPO_HIP_AX_BLOCKS")) return std::max(1, std::atoi(e));
     const long slice = kAxSliceBytes / static_cast<long>(sizeof(double));
     return static_cast<int>((n + slice - 1) / slice);
+}
+
+bool rows_ax_sliced(int n) {
+    if (const char* e = std::getenv("IPO_HIP_AX_JDS")) return std::atoi(e) != 0;
+    return rows_ax_blocks(n) > 1;
 }
 
 void RowAxPlan::build(int m, int n, const int* kA, const int* iA, const double* A, int npass, hipStream_t st) {

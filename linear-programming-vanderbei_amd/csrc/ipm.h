@@ -82,13 +82,14 @@ class IpmSolver {
     void xsum(double* d, size_t n, RedOp op) { if (xch_) xch_->allreduce(d, n, op, stream_); }
     // rows >= mrow() take A x from lax(): the summed linking rows of a shard,
     // or every row when A x is formed column-blocked (row_ax) beforehand
-    const double* lax() const { return xch_ ? lax_.get() : axblocks_ > 1 ? ax_.get() : nullptr; }
-    int mrow() const { return xch_ ? m_ - nforced_ : axblocks_ > 1 ? 0 : m_; }   // rows below are shard-local
+    const double* lax() const { return xch_ ? lax_.get() : axsliced_ ? ax_.get() : nullptr; }
+    int mrow() const { return xch_ ? m_ - nforced_ : axsliced_ ? 0 : m_; }   // rows below are shard-local
     // A x of every row in column blocks whose x-slice fits one XCD's L2
     // (RowAxPlan, row_ax.h; bitwise the residual kernels' own sums), when x is
     // larger than a slice and the solver is not sharded
     void row_ax(const double* x, hipStream_t st);
     int axblocks_ = 1;
+    bool axsliced_ = false;   // A x by RowAxPlan (x over one L2 slice, or IPO_HIP_AX_JDS=1)
     DevBuf<double> ax_;
     RowAxPlan axplan_;
     void print_dims(FILE* tr) const;

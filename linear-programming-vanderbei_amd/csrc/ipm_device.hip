@@ -364,7 +364,8 @@ IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A
     IPO_HIP_CHECK(hipEventCreateWithFlags(&ev_side_, hipEventDisableTiming));
     lax_.alloc(nforced_ > 0 ? nforced_ : 1);
     axblocks_ = rows_ax_blocks(n_);
-    if (axblocks_ > 1 && !xch_) {
+    axsliced_ = rows_ax_sliced(n_) && !xch_;
+    if (axsliced_) {
         ax_.alloc(m_ > 0 ? m_ : 1);
         axplan_.build(m, n, kA, iA, A, axblocks_, stream_);
     }
@@ -391,7 +392,7 @@ void IpmSolver::reduce(const RedJobs& j, int nout) {
 }
 
 void IpmSolver::row_ax(const double* x, hipStream_t st) {
-    if (xch_ || axblocks_ <= 1) return;
+    if (!axsliced_) return;
     axplan_.launch(x, ax_.get(), st);
 }
 
@@ -804,19 +805,20 @@ void vector_bench(int m, int n, const int* kA, const int* iA, const double* A, i
     // the residuals as run_hsd forms them: A x column-blocked first when x
     // exceeds one L2 slice (IpmSolver::row_ax), timed together
     const int axb = rows_ax_blocks(n);
+    const bool sliced = rows_ax_sliced(n);
     DevBuf<double> axv;
     RowAxPlan axplan;
-    if (axb > 1) { axv.alloc(m > 0 ? m : 1); axplan.build(m, n, kA, iA, A, axb, s); }
+    if (sliced) { axv.alloc(m > 0 ? m : 1); axplan.build(m, n, kA, iA, A, axb, s); }
     for (int kq = 0; kq < 3; kq++) {
         for (int r = -2; r < reps; r++) {                 // two untimed launches first
             if (r == 0) IPO_HIP_CHECK(hipEventRecord(e0, s));
             if (kq == 0) {
-                if (axb > 1) axplan.launch(col(2), axv.get(), s);
+                if (sliced) axplan.launch(col(2), axv.get(), s);
                 hipLaunchKernelGGL(k_hsd_residuals, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, dkAt.get(), diAt.get(),
                                    dAt.get(), dkA.get(), diA.get(), dA.get(), col(0) + n, col(1), col(2), col(3) + n,
                                    col(4) + n, col(5), 1.0, 0.5, 0.1, col(6) + n, col(7), col(8) + n, col(9),
-                                   col(10) + n, col(11), part, axb > 1 ? 0 : m, m,
-                                   axb > 1 ? static_cast<const double*>(axv.get()) : static_cast<const double*>(nullptr),
+                                   col(10) + n, col(11), part, sliced ? 0 : m, m,
+                                   sliced ? static_cast<const double*>(axv.get()) : static_cast<const double*>(nullptr),
                                    static_cast<const double*>(nullptr));
             }
             else if (kq == 1)

@@ -16,6 +16,9 @@ namespace ipo {
 // the CSC of A); launch() writes ax[m], one kernel per pass.
 constexpr long kAxSliceBytes = 2l << 20;
 int rows_ax_blocks(int n);
+// whether A x goes through a RowAxPlan: more than one slice, or
+// IPO_HIP_AX_JDS=1 (jagged diagonals over a single slice)
+bool rows_ax_sliced(int n);
 class RowAxPlan {
   public:
     void build(int m, int n, const int* kA, const int* iA, const double* A, int npass, hipStream_t st);

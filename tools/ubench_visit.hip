@@ -6,7 +6,8 @@
 // the operands of one tile (cache-resident: the compute + LDS bound).
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off \
 //         -I linear-programming-vanderbei_amd/csrc tools/ubench_visit.hip -o tools/ubench_visit
-//   tools/ubench_visit [nt]
+//   tools/ubench_visit [nt]                 (the table below)
+//   tools/ubench_visit nt mode chunk G reps (one configuration: for counter passes)
 #include "../linear-programming-vanderbei_amd/csrc/kkt_dense.hip"
 
 #include <cstdio>
@@ -19,7 +20,8 @@ namespace ipo {
 
 // workgroup g -> tile g of the lower triangle of block columns >= c0 (or
 // tile (c0 + 1, c0) for all: same); offd: strictly below the diagonal only
-template <size_t LDSB>
+// NPF 0: the double-buffered visit (visit_tile512_db)
+template <size_t LDSB, int NPF>
 __global__ void __launch_bounds__(PNT) k_visit_bench(PlanView p, TailView tv, int c0, int b0, int b1, int same,
                                                      int offd) {
     __shared__ __attribute__((aligned(16))) char lds[LDSB];
@@ -29,7 +31,10 @@ __global__ void __launch_bounds__(PNT) k_visit_bench(PlanView p, TailView tv, in
     else
         tile = 0;
     if (c >= tv.ntb) return;
-    visit_tile512(p, tv, c + offd + tile, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
+    if constexpr (NPF == 0)
+        visit_tile512_db(p, tv, c + offd + tile, c, b0, b1, *reinterpret_cast<VisitLds*>(lds));
+    else
+        visit_tile512<NPF>(p, tv, c + offd + tile, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
 }
 
 }  // namespace ipo
@@ -55,28 +60,37 @@ int main(int argc, char** argv) {
     const int c0 = 20;        // columns 20.. : 50 + 49 + ... tiles available, blocks 0..19 as operands
     const int maxg = (ntb - c0) * (ntb - c0 + 1) / 2;
     std::printf("nt %d; visit of G tiles, chunk blocks each; us per launch (us per block)\n", nt);
-    struct Mode { int same, big, offd; const char* what; };
-    const Mode modes[] = {{0, 1, 0, "own operands, diagonal tiles included"},
-                          {0, 1, 1, "own operands, below the diagonal only"},
-                          {1, 1, 1, "one off-diagonal tile's operands (cache-resident)"},
-                          {0, 0, 1, "own operands, below the diagonal, LDS of the visit alone"}};
+    struct Mode { int same, big, offd, npf; const char* what; };
+    const Mode modes[] = {{0, 1, 0, 1, "own operands, diagonal tiles included"},
+                          {0, 1, 1, 1, "own operands, below the diagonal only"},
+                          {0, 1, 1, 0, "own operands, below the diagonal only, double-buffered LDS"},
+                          {0, 0, 1, 1, "own operands, below the diagonal, LDS of the visit alone"}};
+    const bool one = argc > 5;
+    const int one_mode = one ? std::atoi(argv[2]) : 0, one_chunk = one ? std::atoi(argv[3]) : 0,
+              one_g = one ? std::atoi(argv[4]) : 0, one_reps = one ? std::atoi(argv[5]) : 20;
     for (const Mode& md : modes) {
+        if (one && &md != &modes[one_mode]) continue;
         std::printf("%s:\n", md.what);
         for (int chunk : {1, 4, 8}) {
+            if (one) chunk = one_chunk;
             std::printf("  chunk %d:", chunk);
             for (int G : {1, 64, 256, 384, 512}) {
+                if (one) G = one_g;
                 if (G > maxg) continue;
                 auto launch = [&]() {
-                    if (md.big)
-                        hipLaunchKernelGGL(ipo::k_visit_bench<ipo::kTailStepLds>, dim3(G), dim3(ipo::PNT), 0, 0, pv, tv, c0, 0,
-                                           chunk, md.same, md.offd);
+                    if (md.npf == 0)
+                        hipLaunchKernelGGL((ipo::k_visit_bench<sizeof(ipo::VisitLds), 0>), dim3(G), dim3(ipo::PNT), 0, 0, pv,
+                                           tv, c0, 0, chunk, md.same, md.offd);
+                    else if (md.big)
+                        hipLaunchKernelGGL((ipo::k_visit_bench<ipo::kTailStepLds, 1>), dim3(G), dim3(ipo::PNT), 0, 0, pv, tv,
+                                           c0, 0, chunk, md.same, md.offd);
                     else
-                        hipLaunchKernelGGL(ipo::k_visit_bench<sizeof(ipo::SyrkLds)>, dim3(G), dim3(ipo::PNT), 0, 0, pv, tv, c0,
-                                           0, chunk, md.same, md.offd);
+                        hipLaunchKernelGGL((ipo::k_visit_bench<sizeof(ipo::SyrkLds), 1>), dim3(G), dim3(ipo::PNT), 0, 0, pv,
+                                           tv, c0, 0, chunk, md.same, md.offd);
                 };
                 launch();
                 CK(hipDeviceSynchronize());
-                const int reps = 20;
+                const int reps = one ? one_reps : 20;
                 CK(hipEventRecord(e0, 0));
                 for (int r = 0; r < reps; r++) launch();
                 CK(hipEventRecord(e1, 0));
@@ -85,9 +99,28 @@ int main(int argc, char** argv) {
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 const double us = 1e3 * ms / reps;
                 std::printf("  G%d %.1f (%.2f)", G, us, us / chunk);
+                if (one) break;
             }
             std::printf("\n");
+            if (one) break;
         }
     }
+#ifdef IPO_VISIT_STAMPS
+    {
+        long long st[8][16][6];
+        CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(ipo::g_vstamps), sizeof(st)));
+        std::printf("workgroup 0 of the last launch, cycles from wave 0's first block start; slots per block: "
+                    "0 start, 1 staged, 2 barrier, 3 next loads issued, 4 MFMA issued, 5 end barrier\n");
+        const long long b0 = st[0][0][0];
+        for (int w = 0; w < 8; w += 3) {
+            std::printf("wave %d:\n", w);
+            for (int b = 0; b < 8; b++) {
+                std::printf("  block %d:", b);
+                for (int sl = 0; sl < 6; sl++) std::printf(" %7lld", st[w][b][sl] - b0);
+                std::printf("\n");
+            }
+        }
+    }
+#endif
     return 0;
 }
