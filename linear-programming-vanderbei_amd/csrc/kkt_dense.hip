@@ -1091,153 +1091,8 @@ __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& 
 // are loaded into registers while block b's are multiplied from LDS (two
 // blocks in flight measured no faster: tools/ubench_tail, round 4).  On a
 // diagonal tile the |terms| of every block go to dscale (one add).
-// Double-buffered visit (the step kernel's): k-major operand tiles with row
-// stride SKD = 72 (the four k of an MFMA operand read at bank offsets 0, 16,
-// 32, 48: two lanes per bank, the minimum; a store of one k's 64 rows
-// conflict-free), two of each, so block b + 1 is staged into the other
-// buffer and block b + 2's loads are issued while block b's MFMA steps run:
-// one barrier per block, and the MFMA pipes do not wait out the staging
-// and the loads (measured with one buffer: ~8,700 cycles per block, of
-// which the MFMA steps are 4,096 per SIMD).
-constexpr int SKD = PC + 8;
-struct VisitLds {
-    double As[2][PC][SKD];
-    double Bs[2][PC][SKD];
-};
-
-template <int NS>
-__device__ __forceinline__ void mfma_steps(const double (*As)[SKD], const double (*Bs)[SKD], int k0, int wr, int wc,
-                                           int li, int lk, double4_t (&acc)[2]) {
-    // NS k-steps from k0; each step's operands are read one step ahead of
-    // its MFMAs (the scheduling groups below), so an LDS round trip hides
-    // under the previous step's MFMAs instead of stalling the wave
-    double av[NS][2], bv[NS];
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        const int kk = k0 + 4 * s;
-        av[s][0] = As[kk + lk][wr + li];
-        av[s][1] = As[kk + lk][wr + 16 + li];
-        bv[s] = Bs[kk + lk][wc + li];
-    }
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s][0], bv[s], acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s][1], bv[s], acc[1], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);          // step 0's reads
-#pragma unroll
-    for (int s = 0; s < NS; s++) {
-        if (s + 1 < NS) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // step s + 1's reads
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);      // step s's MFMAs
-    }
-}
-
-__device__ __forceinline__ void visit_tile512_db(const PlanView& p, const TailView& tv, int bi, int bj, int b0, int b1,
-                                                 VisitLds& L, const int* bailp = nullptr, int bt = 0) {
-    const int bailed = bailp ? *bailp : 0;
-    const int nt = tv.nt, tid = threadIdx.x;
-    constexpr int NU = TR * PC / PNT;
-    double rx[NU], ry[NU], rd[NU];
-    int offa[NU], offb[NU];
-#pragma unroll
-    for (int u = 0; u < NU; u++) {
-        const int idx = tid + u * PNT, rr = idx % TR, k = idx / TR;
-        offa[u] = min(bi * TR + rr, nt - 1) + k * nt;
-        offb[u] = min(bj * TR + rr, nt - 1) + k * nt;
-    }
-    auto load = [&](int b) {
-        const int k0 = b * PC;
-        const double* __restrict__ Lcol = tv.S + (size_t)k0 * nt;
-        const double* __restrict__ dgb = p.dg + tv.tc + k0;
-        if (k0 + PC <= nt) {
-#pragma unroll
-            for (int u = 0; u < NU; u++) {
-                rx[u] = Lcol[offa[u]];
-                ry[u] = Lcol[offb[u]];
-                rd[u] = dgb[(tid + u * PNT) / TR];
-            }
-        } else {
-            const int kmax = nt - 1 - k0;
-#pragma unroll
-            for (int u = 0; u < NU; u++) {
-                const int k = (tid + u * PNT) / TR, kc = min(k, kmax);
-                rx[u] = Lcol[offa[u] - (k - kc) * nt];
-                ry[u] = Lcol[offb[u] - (k - kc) * nt];
-                rd[u] = dgb[kc];
-            }
-        }
-    };
-    auto stage = [&](int b, int buf) {
-        const int nc = min(PC, nt - b * PC);
-#pragma unroll
-        for (int u = 0; u < NU; u++) {
-            const int idx = tid + u * PNT, rr = idx % TR, k = idx / TR;
-            const bool oka = k < nc && bi * TR + rr < nt, okb = k < nc && bj * TR + rr < nt;
-            L.As[buf][k][rr] = oka ? rx[u] : 0.0;
-            L.Bs[buf][k][rr] = okb ? ry[u] * rd[u] : 0.0;   // W = L21 D of block b, formed as its panel forms it (bitwise)
-        }
-    };
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int wr = (wv & 1) * 32, wc = (wv >> 1) * 16;
-    const int li = lane & 15, lk = lane >> 4;
-    const bool diag_tile = bi == bj;
-    double4_t acc[2];
-#pragma unroll
-    for (int a = 0; a < 2; a++) acc[a] = (double4_t){0.0, 0.0, 0.0, 0.0};
-    double as = 0.0;
-    load(b0);
-    double old[2][4];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int rr = wr + a * 16 + (lane >> 4) + 4 * i, cc = wc + (lane & 15);
-            const int rg = bi * TR + rr, cg = bj * TR + cc;
-            const bool ok = rg < nt && cg < nt && !(diag_tile && cc > rr);
-            old[a][i] = tv.S[ok ? rg + (size_t)cg * nt : 0];
-        }
-    if (bailed && bailed - 1 < bt) return;
-    stage(b0, 0);
-    if (b0 + 1 < b1) load(b0 + 1);
-    __syncthreads();
-    for (int b = b0; b < b1; b++) {
-        const int buf = (b - b0) & 1;
-        VISIT_STAMP(b - b0, 0);
-        mfma_steps<PC / 8>(L.As[buf], L.Bs[buf], 0, wr, wc, li, lk, acc);
-        VISIT_STAMP(b - b0, 1);
-        if (b + 1 < b1) {
-            stage(b + 1, buf ^ 1);      // the other buffer: read by nobody since the last barrier
-            VISIT_STAMP(b - b0, 2);
-            if (b + 2 < b1) load(b + 2);
-        }
-        VISIT_STAMP(b - b0, 3);
-        mfma_steps<PC / 8>(L.As[buf], L.Bs[buf], PC / 2, wr, wc, li, lk, acc);
-        VISIT_STAMP(b - b0, 4);
-        if (diag_tile && tid < TR) as = diag_terms<SKD>(L.As[buf], L.Bs[buf], tid, min(PC, nt - b * PC), as);
-        __syncthreads();
-        VISIT_STAMP(b - b0, 5);
-    }
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int rr = wr + a * 16 + (lane >> 4) + 4 * i, cc = wc + (lane & 15);
-            const int rg = bi * TR + rr, cg = bj * TR + cc;
-            if (rg < nt && cg < nt && !(diag_tile && cc > rr)) tv.S[rg + (size_t)cg * nt] = old[a][i] - acc[a][i];
-        }
-    if (diag_tile && tid < TR && bi * TR + tid < nt) p.dscale[tv.tc + bi * TR + tid] += as;
-}
-
-#ifndef IPO_VISIT_NPF
-#define IPO_VISIT_NPF 1          // operand blocks in flight in the step kernel's visits
-#endif
-#ifndef IPO_VISIT_DB
-#define IPO_VISIT_DB 0           // 1: the step kernel's visits double-buffered (visit_tile512_db)
-#endif
-template <int NPF = 1>
 __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView& tv, int bi, int bj, int b0, int b1,
                                               SyrkLds& L, const int* bailp = nullptr, int bt = 0) {
-    static_assert(NPF == 1 || NPF == 2, "operand blocks in flight");
     // a bail flag of an earlier step (see k_tail_pr), read in the shadow of
     // the first operand loads
     const int bailed = bailp ? *bailp : 0;
@@ -1248,7 +1103,7 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
     // staged into LDS -- arithmetic on a load right after it is issued
     // makes the wave wait for it there, before the previous block's MFMA
     // steps, and the load latency is then paid once per block
-    double rx[NPF][NU], ry[NPF][NU], rd[NPF][NU];
+    double rx[NU], ry[NU], rd[NU];
     // element offsets of this thread's operands inside a block column,
     // the same for every block (rows clamped into the tail): a block's loads
     // are a uniform base plus these, no per-block address arithmetic (the
@@ -1290,8 +1145,7 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
 #pragma unroll
     for (int a = 0; a < 2; a++) acc[a] = (double4_t){0.0, 0.0, 0.0, 0.0};
     double as = 0.0;
-    load(b0, rx[0], ry[0], rd[0]);
-    if (NPF == 2 && b0 + 1 < b1) load(b0 + 1, rx[NPF - 1], ry[NPF - 1], rd[NPF - 1]);
+    load(b0, rx, ry, rd);
     // the tile's own entries (no other workgroup of the launch touches
     // them), read now so their latency hides under the products
     double old[2][4];
@@ -1305,7 +1159,7 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
             old[a][i] = tv.S[ok ? rg + (size_t)cg * nt : 0];
         }
     if (bailed && bailed - 1 < bt) return;
-    // block b: operands from registers into LDS, block b + NPF's loads into
+    // block b: operands from registers into LDS, block b + 1's loads into
     // the freed registers, then block b's MFMA steps
     auto step = [&](int b, double (&xx)[NU], double (&yy)[NU], double (&dd)[NU]) {
         VISIT_STAMP(b - b0, 0);
@@ -1320,7 +1174,7 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
         VISIT_STAMP(b - b0, 1);
         __syncthreads();
         VISIT_STAMP(b - b0, 2);
-        if (b + NPF < b1) load(b + NPF, xx, yy, dd);
+        if (b + 1 < b1) load(b + 1, xx, yy, dd);
         VISIT_STAMP(b - b0, 3);
         mfma_32x16(L, wr, wc, li, lk, acc);
         VISIT_STAMP(b - b0, 4);
@@ -1328,10 +1182,7 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
         __syncthreads();
         VISIT_STAMP(b - b0, 5);
     };
-    for (int b = b0; b < b1; b += NPF) {
-        step(b, rx[0], ry[0], rd[0]);
-        if (NPF == 2 && b + 1 < b1) step(b + 1, rx[NPF - 1], ry[NPF - 1], rd[NPF - 1]);
-    }
+    for (int b = b0; b < b1; b++) step(b, rx, ry, rd);
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -1344,8 +1195,7 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
 }
 
 constexpr size_t kTailStepLds0 = sizeof(PanelLds) > sizeof(SyrkLds) ? sizeof(PanelLds) : sizeof(SyrkLds);
-constexpr size_t kTailStepLds1 = kTailStepLds0 > sizeof(PreLds) ? kTailStepLds0 : sizeof(PreLds);
-constexpr size_t kTailStepLds = IPO_VISIT_DB && sizeof(VisitLds) > kTailStepLds1 ? sizeof(VisitLds) : kTailStepLds1;
+constexpr size_t kTailStepLds = kTailStepLds0 > sizeof(PreLds) ? kTailStepLds0 : sizeof(PreLds);
 
 // Visits of launch t (tail_visit_cols): block column c receives the updates
 // of blocks 0 .. c - 2 in chunks of K = TailView::vk, the latest chunk in launch
@@ -1379,12 +1229,7 @@ k_tail_pr(PlanView p, TailView tv, int t, int gp) {
     int tile = blockIdx.x - gp, c = t + 1;
     while (tile >= tv.ntb - c) { tile -= tv.ntb - c; c++; }
     const int b1 = visit_hi(t, c, tv.vk);
-#if IPO_VISIT_DB
-    visit_tile512_db(p, tv, c + tile, c, max(0, b1 - tv.vk), b1, *reinterpret_cast<VisitLds*>(lds), p.flags + 2, t);
-#else
-    visit_tile512<IPO_VISIT_NPF>(p, tv, c + tile, c, max(0, b1 - tv.vk), b1, *reinterpret_cast<SyrkLds*>(lds),
-                                 p.flags + 2, t);
-#endif
+    visit_tile512(p, tv, c + tile, c, max(0, b1 - tv.vk), b1, *reinterpret_cast<SyrkLds*>(lds), p.flags + 2, t);
 }
 
 // Block t's update of block column t + 1 only (tiles (bi, t + 1), bi > t):

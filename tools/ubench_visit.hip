@@ -20,8 +20,7 @@ namespace ipo {
 
 // workgroup g -> tile g of the lower triangle of block columns >= c0 (or
 // tile (c0 + 1, c0) for all: same); offd: strictly below the diagonal only
-// NPF 0: the double-buffered visit (visit_tile512_db)
-template <size_t LDSB, int NPF>
+template <size_t LDSB>
 __global__ void __launch_bounds__(PNT) k_visit_bench(PlanView p, TailView tv, int c0, int b0, int b1, int same,
                                                      int offd) {
     __shared__ __attribute__((aligned(16))) char lds[LDSB];
@@ -31,10 +30,7 @@ __global__ void __launch_bounds__(PNT) k_visit_bench(PlanView p, TailView tv, in
     else
         tile = 0;
     if (c >= tv.ntb) return;
-    if constexpr (NPF == 0)
-        visit_tile512_db(p, tv, c + offd + tile, c, b0, b1, *reinterpret_cast<VisitLds*>(lds));
-    else
-        visit_tile512<NPF>(p, tv, c + offd + tile, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
+    visit_tile512(p, tv, c + offd + tile, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
 }
 
 }  // namespace ipo
@@ -60,11 +56,11 @@ int main(int argc, char** argv) {
     const int c0 = 20;        // columns 20.. : 50 + 49 + ... tiles available, blocks 0..19 as operands
     const int maxg = (ntb - c0) * (ntb - c0 + 1) / 2;
     std::printf("nt %d; visit of G tiles, chunk blocks each; us per launch (us per block)\n", nt);
-    struct Mode { int same, big, offd, npf; const char* what; };
-    const Mode modes[] = {{0, 1, 0, 1, "own operands, diagonal tiles included"},
-                          {0, 1, 1, 1, "own operands, below the diagonal only"},
-                          {0, 1, 1, 0, "own operands, below the diagonal only, double-buffered LDS"},
-                          {0, 0, 1, 1, "own operands, below the diagonal, LDS of the visit alone"}};
+    struct Mode { int same, big, offd; const char* what; };
+    const Mode modes[] = {{0, 1, 0, "own operands, diagonal tiles included"},
+                          {0, 1, 1, "own operands, below the diagonal only"},
+                          {1, 1, 1, "every workgroup one off-diagonal tile's operands"},
+                          {0, 0, 1, "own operands, below the diagonal, LDS of the visit alone"}};
     const bool one = argc > 5;
     const int one_mode = one ? std::atoi(argv[2]) : 0, one_chunk = one ? std::atoi(argv[3]) : 0,
               one_g = one ? std::atoi(argv[4]) : 0, one_reps = one ? std::atoi(argv[5]) : 20;
@@ -78,14 +74,11 @@ int main(int argc, char** argv) {
                 if (one) G = one_g;
                 if (G > maxg) continue;
                 auto launch = [&]() {
-                    if (md.npf == 0)
-                        hipLaunchKernelGGL((ipo::k_visit_bench<sizeof(ipo::VisitLds), 0>), dim3(G), dim3(ipo::PNT), 0, 0, pv,
-                                           tv, c0, 0, chunk, md.same, md.offd);
-                    else if (md.big)
-                        hipLaunchKernelGGL((ipo::k_visit_bench<ipo::kTailStepLds, 1>), dim3(G), dim3(ipo::PNT), 0, 0, pv, tv,
+                    if (md.big)
+                        hipLaunchKernelGGL((ipo::k_visit_bench<ipo::kTailStepLds>), dim3(G), dim3(ipo::PNT), 0, 0, pv, tv,
                                            c0, 0, chunk, md.same, md.offd);
                     else
-                        hipLaunchKernelGGL((ipo::k_visit_bench<sizeof(ipo::SyrkLds), 1>), dim3(G), dim3(ipo::PNT), 0, 0, pv,
+                        hipLaunchKernelGGL((ipo::k_visit_bench<sizeof(ipo::SyrkLds)>), dim3(G), dim3(ipo::PNT), 0, 0, pv,
                                            tv, c0, 0, chunk, md.same, md.offd);
                 };
                 launch();
