@@ -11,12 +11,16 @@ interior-point trajectory (hsd.c starts from all ones), other KKT scalings
 and other dependent-pivot events.  For each, the oracle (the reference's
 algorithm, oracle/) is run under its three summation orders (lltnum's,
 reversed, sorted: orc_set_perturb) and the envelope recorded: statuses,
-iterations, final objectives.  tests/test_gpu_heldout.py holds the GPU to
+iterations, final objectives -- and a fourth order, the oracle built with
+-ffp-contract=fast -mfma (contracted multiply-adds, the FMA order of
+tools/rounding_stability.py).  tests/test_gpu_heldout.py holds the GPU to
 that envelope with the rule as shipped.
 
 usage: python tools/heldout_scaled.py [maxdim]"""
+import ctypes as C
 import json
 import os
+import subprocess
 import sys
 
 import numpy as np
@@ -41,10 +45,20 @@ def scaled(name):
     return p
 
 
+def fma_lib(out="/tmp/orcfma_lib"):
+    """The oracle library with contracted multiply-adds (built outside the tree)."""
+    flags = "-O2 -std=gnu99 -fPIC -ffp-contract=fast -mfma -Wall -Wno-unused-result"
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), f"OUT={out}", f"CFLAGS={flags}",
+                    f"{out}/liborc.so"], check=True)
+    return C.CDLL(os.path.join(out, "liborc.so"))
+
+
 def main():
     maxdim = int(sys.argv[1]) if len(sys.argv) > 1 else 12000
     L = oracle_lib.lib()
-    out = {"seed": SEED, "scaling": "row i of A and b times 2^k, k uniform in {-3..3}", "problems": {}}
+    Lf = fma_lib()
+    out = {"seed": SEED, "scaling": "row i of A and b times 2^k, k uniform in {-3..3}",
+           "orders": ["lltnum (the reference's)", "reversed", "sorted", "fma"], "problems": {}}
     for name in available_problems():
         try:
             dims = ipo_amd.mps_dims(mps_path(name))
@@ -62,6 +76,14 @@ def main():
                              "pobj": r["final_pobj"], "dobj": r["final_dobj"]})
         finally:
             L.orc_set_perturb(0)
+        saved = oracle_lib._lib
+        try:
+            oracle_lib._lib = Lf
+            r = oracle_lib.solve_arrays(p, "hsd")
+        finally:
+            oracle_lib._lib = saved
+        runs.append({"status": ipo_amd.STATUS_TEXT[r["status"]], "iters": r["iters"], "pobj": r["final_pobj"],
+                     "dobj": r["final_dobj"], "order": "fma"})
         its = [r["iters"] for r in runs]
         stable = len({r["status"] for r in runs}) == 1 and max(its) - min(its) <= 2
         out["problems"][name] = {"orders": runs, "stable": stable}
