@@ -1625,17 +1625,12 @@ k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
     double acc[R];
 #pragma unroll
     for (int r = 0; r < R; r++) acc[r] = 0.0;
-    // The L(i, j) tiles do not depend on z: each is loaded two blocks ahead
-    // of its use, so a block of the loop costs its products and barriers,
-    // not a memory round trip (with the load one block ahead every
-    // workgroup paid one round trip per earlier block and trailed the
-    // chain by that much: ~3.5 us per block)
-    auto tile = [&](int j, double (&t)[16]) {
+    for (int j = 0; j < i; j++) {
+        // the L(i, j) tile does not depend on z: load it before waiting
         const double* __restrict__ col = tv.S + row + (size_t)(j * PC + wv * 16) * nt;
+        double t[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) t[q] = col[(size_t)q * nt];
-    };
-    auto use = [&](int j, const double (&t)[16]) {
         if (wv == 0) {
             double zj[R];
             gran_wait<R>(gran + (size_t)j * R * 128, epoch, lane, PC, zj);
@@ -1649,17 +1644,6 @@ k_tail_fwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
             for (int r = 0; r < R; r++) acc[r] += t[q] * zb[r][wv * 16 + q];
         }
         __syncthreads();
-    };
-    double ta[16], tb[16];
-    if (0 < i) tile(0, ta);
-    if (1 < i) tile(1, tb);
-    for (int j = 0; j < i; j += 2) {
-        use(j, ta);
-        if (j + 2 < i) tile(j + 2, ta);
-        if (j + 1 < i) {
-            use(j + 1, tb);
-            if (j + 3 < i) tile(j + 3, tb);
-        }
     }
 #pragma unroll
     for (int r = 0; r < R; r++) red[r][wv][lane] = acc[r];
@@ -1715,16 +1699,13 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
     for (int r = 0; r < R; r++)
 #pragma unroll
         for (int q = 0; q < 16; q++) acc[r][q] = 0.0;
-    // L(j, i) tiles two blocks ahead of their use, as in k_tail_fwd_chain
-    auto tile = [&](int j, double (&t)[16]) {
+    for (int j = ntb - 1; j > i; j--) {
         const int r0 = j * PC, nr = min(PC, nt - r0);
         const int rr = r0 + (lane < nr ? lane : 0);
         const double* __restrict__ col = tv.S + rr + (size_t)(k0 + (nq > 0 ? kq : 0)) * nt;
+        double t[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, max(nq, 1) - 1) * nt];
-    };
-    auto use = [&](int j, const double (&t)[16]) {
-        const int nr = min(PC, nt - j * PC);
         if (wv == 0) {
             double zj[R];
             gran_wait<R>(gran + (size_t)j * R * 128, epoch, lane, nr, zj);
@@ -1739,17 +1720,6 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
             for (int q = 0; q < 16; q++) acc[r][q] += t[q] * zr;
         }
         __syncthreads();
-    };
-    double ta[16], tb[16];
-    if (ntb - 1 > i) tile(ntb - 1, ta);
-    if (ntb - 2 > i) tile(ntb - 2, tb);
-    for (int j = ntb - 1; j > i; j -= 2) {
-        use(j, ta);
-        if (j - 2 > i) tile(j - 2, ta);
-        if (j - 1 > i) {
-            use(j - 1, tb);
-            if (j - 3 > i) tile(j - 3, tb);
-        }
     }
     double* red = lds_pad;   // colsum scratch
     if (nq > 0) colsum_put<R>(red, acc, kq, nq, lane);
