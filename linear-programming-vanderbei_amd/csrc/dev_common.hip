@@ -233,15 +233,19 @@ k_rows_ax_jds(int rows, const int* __restrict__ perm, const int* __restrict__ dp
     ax[i] = s;
 }
 
+// Measured on BASELINE configs[3]'s uniform LP (x 8 MB): one pass 72.6 us
+// per residual launch, 2 / 3 / 4 / 8 column slices 77.5 / 79.1 / 85 / 123 us
+// (the jagged-diagonal entry loads made the slices' locality worth less than
+// their extra passes), so large problems take one pass by default.
 int rows_ax_blocks(int n) {
     if (const char* e = std::getenv("IPO_HIP_AX_BLOCKS")) return std::max(1, std::atoi(e));
-    const long slice = kAxSliceBytes / static_cast<long>(sizeof(double));
-    return static_cast<int>((n + slice - 1) / slice);
+    (void)n;
+    return 1;
 }
 
 bool rows_ax_sliced(int n) {
     if (const char* e = std::getenv("IPO_HIP_AX_JDS")) return std::atoi(e) != 0;
-    return rows_ax_blocks(n) > 1;
+    return rows_ax_blocks(n) > 1 || static_cast<long>(n) * static_cast<long>(sizeof(double)) > kAxSliceBytes;
 }
 
 void RowAxPlan::build(int m, int n, const int* kA, const int* iA, const double* A, int npass, hipStream_t st) {

@@ -753,33 +753,18 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     const bool rok = h1 ? row < h : row < h0;
     const bool tile = TR * (j + 1) < h;             // workgroup has tile rows
     const int nwin = (nc + WIN - 1) / WIN;
-    // this wave's entries of the panel (masked when they are used: a select
-    // right after a load makes the wave wait for it there); a dense-tail
-    // panel with a pre-update issues them after the pre-update's operands,
-    // which are needed first
     double a[WIN];
-    auto load_a = [&]() {
 #pragma unroll
-        for (int q = 0; q < WIN; q++) {
-            const int c = cw0 + q;
-            const bool ok = rok && c < nc && (h1 || c <= row);
-            a[q] = panel[ok ? row + (size_t)c * ld : 0];
-        }
-    };
-    auto mask_a = [&]() {
-#pragma unroll
-        for (int q = 0; q < WIN; q++) {
-            const int c = cw0 + q;
-            const bool ok = rok && c < nc && (h1 || c <= row);
-            a[q] = ok ? a[q] : 0.0;
-        }
-    };
-    if (!pre) load_a();
+    for (int q = 0; q < WIN; q++) {
+        const int c = cw0 + q;
+        const bool ok = rok && c < nc && (h1 || c <= row);
+        const double t = panel[ok ? row + (size_t)c * ld : 0];
+        a[q] = ok ? t : 0.0;
+    }
     // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
     double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
     double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
     if (!pre && bailed && bailed - 1 < bt) return;
-    if (!pre) mask_a();
     if (pre) {
         // dense tail, block column kb > 0: block kb - 1's update of this
         // workgroup's rows, k_tail_syrk's MFMA fragments and order; the
@@ -791,26 +776,22 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
         constexpr int NU = TR * PC / PNT;
         {
             // all 3 NU loads in flight, then into LDS
-            double vd[NU], vj[NU], vw[NU], dk[NU];
+            double vd[NU], vj[NU], vw[NU];
             const int rr = tid % TR, rd = kb * TR + rr, rj = (kb + j + 1) * TR + rr;
             const bool okd = rd < nt, okj = rj < nt;
 #pragma unroll
             for (int u = 0; u < NU; u++) {
                 const int k = (tid + u * PNT) / TR;
-                vd[u] = Lcol[okd ? rd + (size_t)k * nt : 0];
-                vj[u] = Lcol[okj ? rj + (size_t)k * nt : 0];
-                dk[u] = p.dg[tv.tc + kp + k];
-            }
-            load_a();
-            if (bailed && bailed - 1 < bt) return;     // workgroup-uniform
-#pragma unroll
-            for (int u = 0; u < NU; u++) {
+                const double x = Lcol[okd ? rd + (size_t)k * nt : 0];
+                const double y = Lcol[okj ? rj + (size_t)k * nt : 0];
                 // W = L21 D of block t - 1 formed here, the product its panel
                 // would have stored (l * d, the same operands: bitwise)
-                vw[u] = okd ? vd[u] * dk[u] : 0.0;
-                vd[u] = okd ? vd[u] : 0.0;
-                vj[u] = okj ? vj[u] : 0.0;
+                const double dk = p.dg[tv.tc + kp + k];
+                vd[u] = okd ? x : 0.0;
+                vj[u] = okj ? y : 0.0;
+                vw[u] = okd ? x * dk : 0.0;
             }
+            if (bailed && bailed - 1 < bt) return;     // workgroup-uniform
 #pragma unroll
             for (int u = 0; u < NU; u++) {
                 const int k = (tid + u * PNT) / TR;
@@ -859,7 +840,6 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
                 for (int i = 0; i < 4; i++)
                     Am[wc + y * 16 + (lane & 15)][wr + x * 16 + (lane >> 4) + 4 * i] = acc[x][y][i];
         __syncthreads();
-        mask_a();
 #pragma unroll
         for (int q = 0; q < WIN; q++) {
             const int c = cw0 + q;

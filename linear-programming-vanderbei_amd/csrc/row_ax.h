@@ -9,9 +9,9 @@
 
 namespace ipo {
 
-// A x by rows in column slices of x of kAxSliceBytes (bitwise sparse_dot's
-// sums, see k_rows_ax_jds): rows_ax_blocks(n) = the passes for n columns
-// (IPO_HIP_AX_BLOCKS overrides; 1 = a single pass).  RowAxPlan holds A's
+// A x by rows through jagged diagonals (bitwise sparse_dot's sums, see
+// k_rows_ax_jds) when x exceeds kAxSliceBytes: rows_ax_blocks(n) = the
+// column slices, one pass each (default 1; IPO_HIP_AX_BLOCKS overrides).  RowAxPlan holds A's
 // entries by slice in jagged-diagonal order (built once, on the host, from
 // the CSC of A); launch() writes ax[m], one kernel per pass.
 constexpr long kAxSliceBytes = 2l << 20;
