@@ -3400,11 +3400,12 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
         xsum(tv.S, static_cast<size_t>(plan_.nt) * plan_.nt, RedOp::Sum);
         xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
         if (tail_fused) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
-            for (int t = 0; t < plan_.ntb; t++) {
-                ph_begin(s);
-                launch_tail_step(pv, tv, t, s);
-                ph_end(kPhTail, 1, s);
-            }
+            // one event pair around the steps (a pair per launch added its
+            // own ~2.5 us to every launch's time: the phase's average launch
+            // would not be the kernel's)
+            ph_begin(s);
+            for (int t = 0; t < plan_.ntb; t++) launch_tail_step(pv, tv, t, s);
+            ph_end(kPhTail, plan_.ntb, s);
         } else
         for (int kb = 0; kb < plan_.ntb; kb++) {
             const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
@@ -3520,11 +3521,9 @@ void KktDevice::repair_tail() {
             tm_.tail_dep_rounds += kDepBatch;
             if (hFlags_[6]) break;
         }
-        for (int t = tb + 1; t < plan_.ntb; t++) {
-            ph_begin(s);
-            launch_tail_step(pv, tail_view(), t, s);
-            ph_end(kPhTail, 1, s);
-        }
+        ph_begin(s);
+        for (int t = tb + 1; t < plan_.ntb; t++) launch_tail_step(pv, tail_view(), t, s);
+        ph_end(kPhTail, plan_.ntb - tb - 1, s);
         if (finish_pass(true)) break;
         if (hFlags_[1] != 4 || hFlags_[4] - 1 <= tb)   // cannot happen: a later tail column or nothing
             throw std::runtime_error("kkt: dense-tail repair did not advance");
