@@ -260,7 +260,10 @@ def hbm_roofline_leg(reps):
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_hbm.json")))
     hk = json.load(open(files[-1]))["kernels"] if files else {}
     for k in kernels:
-        kernels[k]["traffic"] = hk.get(k, {}).get("hbm_bytes_per_launch")
+        e = hk.get(k, {})
+        # the residual leg's time includes the jagged-diagonal A x passes
+        # (vector_bench times them together): so does its traffic
+        kernels[k]["traffic"] = e.get("hbm_bytes_per_launch_with_row_products", e.get("hbm_bytes_per_launch"))
         kernels[k]["traffic_source"] = os.path.basename(files[-1]) if k in hk else None
     top = max(kernels, key=lambda k: kernels[k]["ms_per_launch"])
     t = kernels[top]

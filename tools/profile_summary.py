@@ -148,13 +148,19 @@ def dfl001_part():
         hk = {}
         for k in sorted(set(hfetch) | set(hwrite)):
             kb = base(k)
-            if kb not in ("k_hsd_residuals", "k_hsd_directions", "k_step"):
+            if kb not in ("k_hsd_residuals", "k_rows_ax_jds", "k_hsd_directions", "k_step"):
                 continue
             fs, fn = hfetch.get(k, (0.0, 0))
             ws, wn = hwrite.get(k, (0.0, 0))
             hk[kb] = {"launches": max(fn, wn), "fetch_bytes_per_launch": 2 * 1024 * fs / max(fn, 1),
                       "write_bytes_per_launch": 1024 * ws / max(wn, 1)}
             hk[kb]["hbm_bytes_per_launch"] = hk[kb]["fetch_bytes_per_launch"] + hk[kb]["write_bytes_per_launch"]
+        # the residual leg is A x by jagged diagonals (large x) + the residual
+        # kernel: its traffic per residual launch is the sum of both
+        if "k_rows_ax_jds" in hk and "k_hsd_residuals" in hk:
+            r, j = hk["k_hsd_residuals"], hk["k_rows_ax_jds"]
+            per = j["launches"] / max(r["launches"], 1)
+            r["hbm_bytes_per_launch_with_row_products"] = r["hbm_bytes_per_launch"] + per * j["hbm_bytes_per_launch"]
         with open(os.path.join(dst, f"{tag}_pmc_hbm.json"), "w") as fh:
             json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, tools/hbm_probe.py 5 (bench.py's "
                                  "hbm_roofline kernels, BASELINE configs[3] uniform LP); FETCH_SIZE doubled (gfx950)",
