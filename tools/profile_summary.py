@@ -188,7 +188,7 @@ for leg, probe in (("banded", "tools/banded_probe.py"), ("blockang", "tools/bloc
             w.writerow([short(n), calls, f"{tot:.1f}", f"{avg:.2f}", f"{pct:.2f}"])
     out = {"source": f"rocprofv3 --kernel-trace --stats / --pmc passes, python3 {probe} {iters} 0; FETCH_SIZE "
                      f"doubled (gfx950); per IPM iteration = run total / {iters}",
-           "iterations": iters, "kernel_us_per_iteration": sum(r[2] for r in krows) / 1000.0 / iters}
+           "iterations": iters, "kernel_ms_per_iteration": sum(r[2] for r in krows) / 1000.0 / iters}
     f_ = os.path.join(src, f"{tag}_{leg}_pmc_fetch", "run_results.db")
     w_ = os.path.join(src, f"{tag}_{leg}_pmc_write", "run_results.db")
     if os.path.exists(f_) and os.path.exists(w_):
