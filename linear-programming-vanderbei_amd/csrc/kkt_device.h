@@ -248,6 +248,7 @@ class KktDevice {
     int chain_epoch_ = 0;      // the chains' launch epoch (one per launch, never reused)
     int visit_blocks_ = kTailVisitBlocks;   // TailView::vk (IPO_HIP_VISIT_BLOCKS)
     bool chain_pairs_ = false; // dense-tail chains with two blocks per workgroup (k_tail_fwd_pair / _bwd_pair)
+    bool chain_lead_ = false;  // forward dense-tail sweep by one lead workgroup + helpers (k_tail_fwd_lead)
     DevBuf<int> dtail_task_ptr_, dtail_kslot_, dtail_kslot_ptr_;
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;

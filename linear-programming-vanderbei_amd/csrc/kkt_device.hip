@@ -769,9 +769,17 @@ k_tail_syrk(PlanView p, TailView tv, int kb) {
 // subtracts L(r, j) z_j = 0 * 0 and changes nothing), so the chain is one
 // basic block the compiler can schedule; the same mul-then-subtract per
 // entry as the general form (bitwise the same result).
+// The lane index, opaque to the optimiser: a solve inside a loop would
+// otherwise have its 64 per-step lane masks hoisted out of the loop (128
+// scalar registers, spilled).
+__device__ __forceinline__ int opaque_lane() {
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
 template <int R, int NS>
 __device__ __forceinline__ void tri_lower_live(double (&zr)[R], const double (*Ls)[PC + 1]) {
-    const int lane = threadIdx.x & 63;
+    const int lane = opaque_lane();
     double lr[NS];
 #pragma unroll
     for (int j = 0; j < NS; j++) lr[j] = Ls[lane][j];
@@ -787,7 +795,7 @@ __device__ __forceinline__ void tri_lower_live(double (&zr)[R], const double (*L
 }
 template <int R, int NS>
 __device__ __forceinline__ void tri_upper_live(double (&zr)[R], const double (*Ls)[PC + 1]) {
-    const int lane = threadIdx.x & 63;
+    const int lane = opaque_lane();
     double lc[NS];
 #pragma unroll
     for (int j = 0; j < NS; j++) lc[j] = Ls[j][lane];
@@ -805,7 +813,7 @@ __device__ __forceinline__ void tri_upper_live(double (&zr)[R], const double (*L
 template <int R>
 __device__ __forceinline__ void tri_lower(double (&zr)[R], const double (*Ls)[PC + 1], const int* lv, int nc,
                                           const double (&eps)[R], int (&bad)[R]) {
-    const int lane = threadIdx.x & 63;
+    const int lane = opaque_lane();
     const uint64_t lm = __ballot(lane < nc && lv[lane]);
     if (lm == (nc >= 64 ? ~0ull : (1ull << nc) - 1ull)) {     // every column live (wave-uniform)
         if (nc <= 16) tri_lower_live<R, 16>(zr, Ls);
@@ -837,7 +845,7 @@ __device__ __forceinline__ void tri_lower(double (&zr)[R], const double (*Ls)[PC
 template <int R>
 __device__ __forceinline__ void tri_upper(double (&zr)[R], const double (*Ls)[PC + 1], const int* lv, int nc,
                                           const double (&eps)[R], int (&bad)[R]) {
-    const int lane = threadIdx.x & 63;
+    const int lane = opaque_lane();
     const uint64_t lm = __ballot(lane < nc && lv[lane]);
     if (lm == (nc >= 64 ? ~0ull : (1ull << nc) - 1ull)) {     // every column live (wave-uniform)
         if (nc <= 16) tri_upper_live<R, 16>(zr, Ls);
@@ -916,8 +924,10 @@ __device__ __forceinline__ double dscale_rule(const PlanView& p, int v, double z
 // Stage L11 of a panel (ld = h) from the upper-triangle slot image:
 // Ls[r][j] = L(r, j) for j < r, 0 elsewhere.  Each wave issues all its
 // loads before the first LDS store (addresses clamped in bounds).
-__device__ __forceinline__ void stage_l11(const double* panel, size_t ld, int nc, double (*Ls)[PC + 1]) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+// Waves wv of nw (default: the whole workgroup) share the loads.
+__device__ __forceinline__ void stage_l11(const double* panel, size_t ld, int nc, double (*Ls)[PC + 1], int wv,
+                                          int nw) {
+    const int lane = threadIdx.x & 63;
     for (int r0 = wv; r0 < PC; r0 += 16 * nw) {
         double t[16];
 #pragma unroll
@@ -933,6 +943,9 @@ __device__ __forceinline__ void stage_l11(const double* panel, size_t ld, int nc
             if (r < PC) Ls[r][lane] = t[q];
         }
     }
+}
+__device__ __forceinline__ void stage_l11(const double* panel, size_t ld, int nc, double (*Ls)[PC + 1]) {
+    stage_l11(panel, ld, nc, Ls, threadIdx.x >> 6, blockDim.x >> 6);
 }
 
 // Vector families of a sweep: z (K entries each) and the forward update
@@ -1988,6 +2001,272 @@ k_tail_bwd_pair(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
     }
 }
 
+// ------------------------------------ forward tail sweep: a lead workgroup
+// The chain above hands every block's z across CUs (a granule round trip per
+// block on the critical path).  Here ONE lead workgroup solves all blocks in
+// order, z_{i-1} reaching block i through LDS.  Of block i's products
+// L(i, j) z_j the lead forms only the last K = kLeadBlocks (j = i-K .. i-1);
+// helper workgroup i - K (one per block i > K) sums j = 0 .. i-K-1 from the
+// granules of z the lead publishes and hands its per-lane partials to the
+// lead as granules.  Each lane's sum is k_tail_fwd_chain's wave partial --
+// the same terms in the same order, continued by the lead -- and the column
+// reduction and L11 solve are the same: bitwise the same sweep.
+// Lead: wave 0 solves; waves 1-4 ("product waves", wave g + 1 owns columns
+// 16g .. 16g+15 of every block) form the partials and, while wave 0 solves
+// block i, already sum block i+1's partial up to j = i-1, issue the loads of
+// step i+2 and stage L11 of block i+1.  Step i, barriers A_i and B_i:
+//   products: acc = pre_i + L(i, i-1) z_{i-1} -> red  |A_i|  pre_{i+1} =
+//             helper partial + L(i+1, j) z_j for j = i+1-K .. i-1; loads
+//             for step i+2; L11(i+1) staged  |B_i|
+//   solver:   |A_i|  z_i = L11 \ (z_i - sum of red), published  |B_i|
+// Residency: a helper waits only on z the lead publishes, the lead only on
+// helpers' partials over earlier z -- acyclic while the grid (<= ntb
+// workgroups, one per CU by the dynamic LDS) is resident.
+constexpr int kLeadBlocks = 2;
+// raw buffer over the tail S (nt <= kChainMaxBlocks * PC: byte offsets fit an int)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tail_rsrc(const double* S) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(S), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t rs, int voff, int soff) {
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+    return __builtin_bit_cast(double, v);
+}
+constexpr int kLeadNT = 320;
+constexpr int kHelpBatch = 4;
+// helper partials: block i, right-hand side r, column group g, lane l ->
+// granules ((((i R + r) 4 + g) 64 + l) 2 + {0, 1}
+__device__ __forceinline__ gran_t* part_slot(gran_t* pg, int i, int R, int r, int g, int lane) {
+    return pg + (((((size_t)i * R + r) * 4 + g) * 64) + lane) * 2;
+}
+__device__ __forceinline__ void lds_sync() {     // LDS-only barrier: global stores need not drain
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int R>
+__global__ void __launch_bounds__(kLeadNT)
+k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, gran_t* __restrict__ gran,
+                gran_t* __restrict__ pgran, unsigned epoch) {
+    extern __shared__ double lds[];
+    constexpr int K = kLeadBlocks;
+    const int nt = tv.nt, tc = tv.tc, ntb = tv.ntb;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = wv - 1;
+    if (blockIdx.x > 0) {        // helper of block i
+        const int i = blockIdx.x + K, k0 = i * PC, nc = min(PC, nt - k0), jend = i - K;
+        double* zb = lds;        // zb[(b R + r) PC + c]
+        const __amdgpu_buffer_rsrc_t rs = tail_rsrc(tv.S);
+        const int nt8 = nt * 8, g16 = __builtin_amdgcn_readfirstlane(g * 16);
+        const int voff = (k0 + (lane < nc ? lane : 0)) * 8;
+        double acc[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = 0.0;
+        for (int j0 = 0; j0 < jend; j0 += kHelpBatch) {
+            double t[kHelpBatch][16];
+            if (wv > 0) {
+#pragma unroll
+                for (int b = 0; b < kHelpBatch; b++) {
+                    const int s0 = (min(j0 + b, jend - 1) * PC + g16) * nt8;
+#pragma unroll
+                    for (int q = 0; q < 16; q++) t[b][q] = buf_ld(rs, voff, s0 + q * nt8);
+                }
+            } else {
+#pragma unroll
+                for (int b = 0; b < kHelpBatch; b++) {
+                    if (j0 + b < jend) {
+                        double zj[R];
+                        gran_wait<R>(gran + (size_t)(j0 + b) * R * 128, epoch, lane, PC, zj);
+#pragma unroll
+                        for (int r = 0; r < R; r++) zb[(b * R + r) * PC + lane] = zj[r];
+                    }
+                }
+            }
+            lds_sync();
+            if (wv > 0) {
+#pragma unroll
+                for (int b = 0; b < kHelpBatch; b++) {
+                    if (j0 + b < jend) {
+#pragma unroll
+                        for (int q = 0; q < 16; q++) {
+#pragma unroll
+                            for (int r = 0; r < R; r++) acc[r] += t[b][q] * zb[(b * R + r) * PC + g * 16 + q];
+                        }
+                    }
+                }
+            }
+            lds_sync();
+        }
+        if (wv > 0) {
+#pragma unroll
+            for (int r = 0; r < R; r++) gran_put(part_slot(pgran, i, R, r, g, lane), epoch, acc[r]);
+        }
+        return;
+    }
+    double(*Ls)[PC][PC + 1] = reinterpret_cast<double(*)[PC][PC + 1]>(lds);     // two buffers
+    double* zh = lds + 2 * PC * (PC + 1);     // z of the last K blocks: zh[((j % K) R + r) PC + c]
+    double* red = zh + K * R * PC;            // red[(r 4 + g) 64 + lane]
+    int* lv = reinterpret_cast<int*>(red + R * 4 * 64);    // lv[buf PC + c]
+    if (wv == 0) {
+        // ---- solver wave
+        double eps[R], zown[R];
+        int bad[R] = {};
+        load_eps<R>(epsp, eps);
+#pragma unroll
+        for (int r = 0; r < R; r++) zown[r] = lane < min(PC, nt) ? V.z[r * V.zs + tc + lane] : 0.0;
+        lds_sync();                                                      // B_{-1}
+        for (int i = 0; i < ntb; i++) {
+            const int k0 = i * PC, nc = min(PC, nt - k0);
+            double znext[R];
+            const int k1 = k0 + PC, nc1 = i + 1 < ntb ? min(PC, nt - k1) : 0;
+#pragma unroll
+            for (int r = 0; r < R; r++) znext[r] = lane < nc1 ? V.z[r * V.zs + tc + k1 + lane] : 0.0;
+            lds_sync();                                                  // A_i
+            double zr[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const double* rd = red + r * 4 * 64 + lane;
+                zr[r] = lane < nc ? zown[r] - (((rd[0] + rd[64]) + rd[128]) + rd[192]) : 0.0;
+            }
+            tri_lower<R>(zr, Ls[i & 1], lv + (i & 1) * PC, nc, eps, bad);
+            if (lane < nc) {
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    gran_put(gran + (((size_t)i * R + r) * 64 + lane) * 2, epoch, zr[r]);
+                    V.z[r * V.zs + tc + k0 + lane] = zr[r];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                zh[((i % K) * R + r) * PC + lane] = lane < nc ? zr[r] : 0.0;
+                zown[r] = znext[r];
+            }
+            lds_sync();                                                  // B_i
+        }
+        flag_bad<R>(p, bad);
+        return;
+    }
+    // ---- product waves
+    // buffer loads: the per-column offsets are scalars, only the row offset
+    // is a per-lane register (64 global loads would each hold a 64-bit address)
+    const __amdgpu_buffer_rsrc_t rs = tail_rsrc(tv.S);
+    const int nt8 = nt * 8, g16 = __builtin_amdgcn_readfirstlane(g * 16);
+    auto load_tiles = [&](int i, double(&t)[K][16]) {     // L(i, j), j = i-K .. i-1 (j >= 0)
+        const int k0 = i * PC, nc = min(PC, nt - k0);
+        const int voff = (k0 + (lane < nc ? lane : 0)) * 8;
+#pragma unroll
+        for (int b = 0; b < K; b++) {
+            const int s0 = (max(i - K + b, 0) * PC + g16) * nt8;
+#pragma unroll
+            for (int q = 0; q < 16; q++) t[b][q] = buf_ld(rs, voff, s0 + q * nt8);
+        }
+    };
+    // L11 of block i (stage_l11's rows r = g + 4q of Ls[r][c] = L(r, c), c < r)
+    // and its live marks, loaded into registers a step before they are stored
+    auto l11_load = [&](int i, double(&t)[16], int& lvv) {
+        const int k0 = i * PC, nc = min(PC, nt - k0);
+        const int voff = (k0 + lane) * 8;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int r = g + 4 * q;
+            const bool ok = r < nc && lane < r;
+            const double v = buf_ld(rs, ok ? voff : 0, min(k0 + r, nt - 1) * nt8);
+            t[q] = ok ? v : 0.0;
+        }
+        lvv = tid - 64 < nc ? p.live[tc + k0 + tid - 64] : 0;
+    };
+    auto l11_store = [&](int i, const double(&t)[16], int lvv) {
+        const int nc = min(PC, nt - i * PC);
+#pragma unroll
+        for (int q = 0; q < 16; q++) Ls[i & 1][g + 4 * q][lane] = t[q];
+        if (tid - 64 < nc) lv[(i & 1) * PC + tid - 64] = lvv;
+    };
+    unsigned long long praw[R][2];
+    auto part_load = [&](int i) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const gran_t* q = part_slot(pgran, i, R, r, g, lane);
+            praw[r][0] = __hip_atomic_load(const_cast<gran_t*>(q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            praw[r][1] = __hip_atomic_load(const_cast<gran_t*>(q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
+    double pre[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) pre[r] = 0.0;
+    double tA[K][16], tB[K][16], lA[16], lB[16];
+    int vA, vB;
+    l11_load(0, lA, vA);
+    l11_store(0, lA, vA);
+    load_tiles(min(1, ntb - 1), tB);
+    l11_load(min(1, ntb - 1), lB, vB);
+    part_load(min(1, ntb - 1));
+    lds_sync();                                                          // B_{-1}
+    // cur / lcur: step i's tiles (and the L11 slot to refill), nxt / lnxt: step i+1's
+    auto step = [&](int i, double(&cur)[K][16], double(&nxt)[K][16], double(&lcur)[16], int& vcur,
+                    double(&lnxt)[16], int& vnxt) {
+        double acc[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = pre[r];
+        if (i >= 1) {                                  // the last term: z_{i-1}
+            const double* z = zh + ((i - 1) % K) * R * PC + g * 16;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+#pragma unroll
+                for (int r = 0; r < R; r++) acc[r] += cur[K - 1][q] * z[r * PC + q];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) red[(r * 4 + g) * 64 + lane] = acc[r];
+        lds_sync();                                                      // A_i
+        if (i + 1 < ntb) {
+            l11_store(i + 1, lnxt, vnxt);
+            if (i + 1 > K) {                           // helper i+1-K's partial (j <= i-K)
+                for (;;) {
+                    bool ok = true;
+#pragma unroll
+                    for (int r = 0; r < R; r++) ok &= (praw[r][0] >> 32) == epoch && (praw[r][1] >> 32) == epoch;
+                    if (__all(ok)) break;
+                    __builtin_amdgcn_s_sleep(IPO_POLL_SLEEP);
+                    part_load(i + 1);
+                }
+#pragma unroll
+                for (int r = 0; r < R; r++)
+                    pre[r] = __longlong_as_double(static_cast<long long>(((praw[r][1] & 0xffffffffull) << 32) |
+                                                                         (praw[r][0] & 0xffffffffull)));
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; r++) pre[r] = 0.0;
+            }
+#pragma unroll
+            for (int b = 0; b < K - 1; b++) {          // j = i+1-K .. i-1, in order
+                const int j = i + 1 - K + b;
+                if (j >= 0) {
+                    const double* z = zh + (j % K) * R * PC + g * 16;
+#pragma unroll
+                    for (int q = 0; q < 16; q++) {
+#pragma unroll
+                        for (int r = 0; r < R; r++) pre[r] += nxt[b][q] * z[r * PC + q];
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);     // z reads one tile at a time (registers)
+            }
+        }
+        // step i+2's loads, unconditional (clamped in range: a conditional
+        // load would keep the old registers live across the branch)
+        const int i2 = min(i + 2, ntb - 1);
+        load_tiles(i2, cur);
+        l11_load(i2, lcur, vcur);
+        part_load(i2);
+        lds_sync();                                                      // B_i
+    };
+    int i = 0;
+    for (; i + 1 < ntb; i += 2) {      // two steps per trip, unconditionally (no register merges)
+        step(i, tA, tB, lA, vA, lB, vB);
+        step(i + 1, tB, tA, lB, vB, lA, vA);
+    }
+    if (i < ntb) step(i, tA, tB, lA, vA, lB, vB);
+}
+
 // ------------------------------------------- sync-free sweeps, top levels
 // The narrow top of the elimination tree (levels >= sf_level_, a few
 // supernodes each) in one persistent launch per direction instead of one or
@@ -3008,7 +3287,8 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dW_.alloc(static_cast<size_t>(plan_.nt) * kPanelCols);   // W = L21 D of one block column (per-phase path)
         dDepSt_.alloc(tail_dep_state_doubles(plan_.ntb));
         dDepI_.alloc(8);
-        dChainGran_.alloc(static_cast<size_t>(plan_.ntb) * 2 * 128);     // R <= 2 right-hand sides
+        // R <= 2 right-hand sides: z of every block, then k_tail_fwd_lead's helper partials
+        dChainGran_.alloc(static_cast<size_t>(plan_.ntb) * (2 * 128 + 2 * 4 * 64 * 2));
         IPO_HIP_CHECK(hipMemsetAsync(dChainGran_.get(), 0, dChainGran_.bytes(), s));
         if (plan_.ntb <= kChainMaxBlocks) {
             for (const void* f : {reinterpret_cast<const void*>(&k_tail_fwd_chain<1>),
@@ -3025,6 +3305,12 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             // two 64-row blocks per chain workgroup (IPO_HIP_CHAIN_PAIRS=1; default: one)
             const char* cp = std::getenv("IPO_HIP_CHAIN_PAIRS");
             chain_pairs_ = cp && std::atoi(cp) != 0;
+            for (const void* f : {reinterpret_cast<const void*>(&k_tail_fwd_lead<1>),
+                                  reinterpret_cast<const void*>(&k_tail_fwd_lead<2>)})
+                IPO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
+            // the forward sweep by a lead workgroup (IPO_HIP_CHAIN_LEAD=1; default: the per-block chain)
+            const char* cl = std::getenv("IPO_HIP_CHAIN_LEAD");
+            chain_lead_ = cl && std::atoi(cl) != 0;
         }
     }
     if (const char* vb = std::getenv("IPO_HIP_VISIT_BLOCKS")) visit_blocks_ = std::max(1, std::atoi(vb));
@@ -3652,7 +3938,11 @@ void KktDevice::sweep(double* dz, const double* epsp) {
         hipLaunchKernelGGL(k_tail_gather<R>, dim3(ceil_div(plan_.nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(),
                            dyrow_idx_.get(), V);
         tail_rhs_end(dz, R);
-        if (chain_pairs_)
+        if (chain_lead_)
+            hipLaunchKernelGGL(k_tail_fwd_lead<R>, dim3(1 + std::max(0, plan_.ntb - 1 - kLeadBlocks)), dim3(kLeadNT),
+                               kChainLds, s, pv, tv, V, epsp, dChainGran_.get(),
+                               dChainGran_.get() + static_cast<size_t>(plan_.ntb) * 2 * 128, ++chain_epoch_);
+        else if (chain_pairs_)
             hipLaunchKernelGGL(k_tail_fwd_pair<R>, dim3((plan_.ntb + 1) / 2), dim3(NT), kPairFwdLds, s, pv, tv, V, epsp,
                                dChainGran_.get(), ++chain_epoch_);
         else
