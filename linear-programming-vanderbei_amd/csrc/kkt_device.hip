@@ -2011,10 +2011,15 @@ k_tail_bwd_pair(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
 // lead as granules.  Each lane's sum is k_tail_fwd_chain's wave partial --
 // the same terms in the same order, continued by the lead -- and the column
 // reduction and L11 solve are the same: bitwise the same sweep.
-// Lead: wave 0 solves; waves 1-4 ("product waves", wave g + 1 owns columns
-// 16g .. 16g+15 of every block) form the partials and, while wave 0 solves
-// block i, already sum block i+1's partial up to j = i-1, issue the loads of
-// step i+2 and stage L11 of block i+1.  Step i, barriers A_i and B_i:
+// Lead: wave 0 solves; four "product waves" (column group g owns columns
+// 16g .. 16g+15 of every block; waves 1, 2, 3, 5 -- wave 4, which would share
+// the solver's SIMD, leaves at once) form the partials and, while wave 0
+// solves block i, already sum block i+1's partial up to j = i-1, store the
+// L11 of block i+1 (loaded a step earlier) and issue the loads of step i+2
+// (tiles, L11, the helper partial).  Measured on dfl001 (70 blocks, R = 2,
+// IPO_LEAD_STAMPS): 2.8 us per step -- solve 2.0, waits 0.8 -- against
+// ~3.5 us per block of the per-block chain, whose cross-CU hand-off this
+// removes.  Step i, barriers A_i and B_i:
 //   products: acc = pre_i + L(i, i-1) z_{i-1} -> red  |A_i|  pre_{i+1} =
 //             helper partial + L(i+1, j) z_j for j = i+1-K .. i-1; loads
 //             for step i+2; L11(i+1) staged  |B_i|
@@ -2023,6 +2028,14 @@ k_tail_bwd_pair(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
 // helpers' partials over earlier z -- acyclic while the grid (<= ntb
 // workgroups, one per CU by the dynamic LDS) is resident.
 constexpr int kLeadBlocks = 2;
+// developer stamps (-DIPO_LEAD_STAMPS; compiled out otherwise): one launch's
+// per-step split printed from the device
+#ifdef IPO_LEAD_STAMPS
+__device__ double g_lead_stats[8][4];
+#define LEAD_T(v) const long long v = wall_clock64()
+#else
+#define LEAD_T(v) do {} while (0)
+#endif
 // raw buffer over the tail S (nt <= kChainMaxBlocks * PC: byte offsets fit an int)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t tail_rsrc(const double* S) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(S), 0, 0x7fffffff, 0x00020000);
@@ -2032,7 +2045,7 @@ __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t rs, int voff, in
     const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
     return __builtin_bit_cast(double, v);
 }
-constexpr int kLeadNT = 320;
+constexpr int kLeadNT = 384;
 constexpr int kHelpBatch = 4;
 // helper partials: block i, right-hand side r, column group g, lane l ->
 // granules ((((i R + r) 4 + g) 64 + l) 2 + {0, 1}
@@ -2052,7 +2065,12 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
     extern __shared__ double lds[];
     constexpr int K = kLeadBlocks;
     const int nt = tv.nt, tc = tv.tc, ntb = tv.ntb;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, g = wv - 1;
+    // waves: 0 solves; 1, 2, 3 and 5 are column groups 0-3; 4 (which would
+    // share the solver's SIMD) leaves at once
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = wv <= 3 ? wv - 1 : wv - 2;     // wave-uniform (scalar buffer offsets)
+    const int pl = g * 64 + lane;
+    if (wv == 4) return;
     if (blockIdx.x > 0) {        // helper of block i
         const int i = blockIdx.x + K, k0 = i * PC, nc = min(PC, nt - k0), jend = i - K;
         double* zb = lds;        // zb[(b R + r) PC + c]
@@ -2114,14 +2132,19 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
         load_eps<R>(epsp, eps);
 #pragma unroll
         for (int r = 0; r < R; r++) zown[r] = lane < min(PC, nt) ? V.z[r * V.zs + tc + lane] : 0.0;
+#ifdef IPO_LEAD_STAMPS
+        long long sa = 0, st = 0, sb = 0;
+#endif
         lds_sync();                                                      // B_{-1}
         for (int i = 0; i < ntb; i++) {
+            LEAD_T(t0);
             const int k0 = i * PC, nc = min(PC, nt - k0);
             double znext[R];
             const int k1 = k0 + PC, nc1 = i + 1 < ntb ? min(PC, nt - k1) : 0;
 #pragma unroll
             for (int r = 0; r < R; r++) znext[r] = lane < nc1 ? V.z[r * V.zs + tc + k1 + lane] : 0.0;
             lds_sync();                                                  // A_i
+            LEAD_T(t1);
             double zr[R];
 #pragma unroll
             for (int r = 0; r < R; r++) {
@@ -2129,6 +2152,7 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
                 zr[r] = lane < nc ? zown[r] - (((rd[0] + rd[64]) + rd[128]) + rd[192]) : 0.0;
             }
             tri_lower<R>(zr, Ls[i & 1], lv + (i & 1) * PC, nc, eps, bad);
+            LEAD_T(t2);
             if (lane < nc) {
 #pragma unroll
                 for (int r = 0; r < R; r++) {
@@ -2142,7 +2166,17 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
                 zown[r] = znext[r];
             }
             lds_sync();                                                  // B_i
+#ifdef IPO_LEAD_STAMPS
+            LEAD_T(t3);
+            sa += t1 - t0; st += t2 - t1; sb += t3 - t2;
+#endif
         }
+#ifdef IPO_LEAD_STAMPS
+        if (lane == 0) {
+            g_lead_stats[0][0] = sa * 0.01 / ntb; g_lead_stats[0][1] = st * 0.01 / ntb;
+            g_lead_stats[0][2] = sb * 0.01 / ntb;
+        }
+#endif
         flag_bad<R>(p, bad);
         return;
     }
@@ -2170,16 +2204,18 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
         for (int q = 0; q < 16; q++) {
             const int r = g + 4 * q;
             const bool ok = r < nc && lane < r;
-            const double v = buf_ld(rs, ok ? voff : 0, min(k0 + r, nt - 1) * nt8);
-            t[q] = ok ? v : 0.0;
+            t[q] = buf_ld(rs, ok ? voff : 0, min(k0 + r, nt - 1) * nt8);   // masked when stored
         }
-        lvv = tid - 64 < nc ? p.live[tc + k0 + tid - 64] : 0;
+        lvv = p.live[tc + k0 + min(pl, nc - 1)];
     };
     auto l11_store = [&](int i, const double(&t)[16], int lvv) {
         const int nc = min(PC, nt - i * PC);
 #pragma unroll
-        for (int q = 0; q < 16; q++) Ls[i & 1][g + 4 * q][lane] = t[q];
-        if (tid - 64 < nc) lv[(i & 1) * PC + tid - 64] = lvv;
+        for (int q = 0; q < 16; q++) {
+            const int r = g + 4 * q;
+            Ls[i & 1][r][lane] = r < nc && lane < r ? t[q] : 0.0;
+        }
+        if (pl < nc) lv[(i & 1) * PC + pl] = lvv;
     };
     unsigned long long praw[R][2];
     auto part_load = [&](int i) {
@@ -2195,6 +2231,10 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
     for (int r = 0; r < R; r++) pre[r] = 0.0;
     double tA[K][16], tB[K][16], lA[16], lB[16];
     int vA, vB;
+#ifdef IPO_LEAD_STAMPS
+    long long pw = 0, p3 = 0, p4 = 0;
+    int polls = 0;
+#endif
     l11_load(0, lA, vA);
     l11_store(0, lA, vA);
     load_tiles(min(1, ntb - 1), tB);
@@ -2218,6 +2258,7 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
 #pragma unroll
         for (int r = 0; r < R; r++) red[(r * 4 + g) * 64 + lane] = acc[r];
         lds_sync();                                                      // A_i
+        LEAD_T(u0);
         if (i + 1 < ntb) {
             l11_store(i + 1, lnxt, vnxt);
             if (i + 1 > K) {                           // helper i+1-K's partial (j <= i-K)
@@ -2226,9 +2267,16 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
 #pragma unroll
                     for (int r = 0; r < R; r++) ok &= (praw[r][0] >> 32) == epoch && (praw[r][1] >> 32) == epoch;
                     if (__all(ok)) break;
+#ifdef IPO_LEAD_STAMPS
+                    polls++;
+#endif
                     __builtin_amdgcn_s_sleep(IPO_POLL_SLEEP);
                     part_load(i + 1);
                 }
+                LEAD_T(u1);
+#ifdef IPO_LEAD_STAMPS
+                pw += u1 - u0;
+#endif
 #pragma unroll
                 for (int r = 0; r < R; r++)
                     pre[r] = __longlong_as_double(static_cast<long long>(((praw[r][1] & 0xffffffffull) << 32) |
@@ -2251,12 +2299,17 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
                 __builtin_amdgcn_sched_barrier(0);     // z reads one tile at a time (registers)
             }
         }
+        LEAD_T(u2);
         // step i+2's loads, unconditional (clamped in range: a conditional
         // load would keep the old registers live across the branch)
         const int i2 = min(i + 2, ntb - 1);
         load_tiles(i2, cur);
         l11_load(i2, lcur, vcur);
         part_load(i2);
+        LEAD_T(u3);
+#ifdef IPO_LEAD_STAMPS
+        p3 += u2 - u0; p4 += u3 - u2;
+#endif
         lds_sync();                                                      // B_i
     };
     int i = 0;
@@ -2265,6 +2318,12 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
         step(i + 1, tB, tA, lB, vB, lA, vA);
     }
     if (i < ntb) step(i, tA, tB, lA, vA, lB, vB);
+#ifdef IPO_LEAD_STAMPS
+    if (lane == 0) {
+        g_lead_stats[wv][0] = pw * 0.01 / ntb; g_lead_stats[wv][1] = polls;
+        g_lead_stats[wv][2] = p3 * 0.01 / ntb; g_lead_stats[wv][3] = p4 * 0.01 / ntb;
+    }
+#endif
 }
 
 // ------------------------------------------- sync-free sweeps, top levels
@@ -3308,9 +3367,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             for (const void* f : {reinterpret_cast<const void*>(&k_tail_fwd_lead<1>),
                                   reinterpret_cast<const void*>(&k_tail_fwd_lead<2>)})
                 IPO_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kChainLds));
-            // the forward sweep by a lead workgroup (IPO_HIP_CHAIN_LEAD=1; default: the per-block chain)
+            // the forward sweep by a lead workgroup (default; IPO_HIP_CHAIN_LEAD=0: the per-block chain)
             const char* cl = std::getenv("IPO_HIP_CHAIN_LEAD");
-            chain_lead_ = cl && std::atoi(cl) != 0;
+            chain_lead_ = !(cl && std::atoi(cl) == 0);
         }
     }
     if (const char* vb = std::getenv("IPO_HIP_VISIT_BLOCKS")) visit_blocks_ = std::max(1, std::atoi(vb));
@@ -3948,6 +4007,18 @@ void KktDevice::sweep(double* dz, const double* epsp) {
         else
             hipLaunchKernelGGL(k_tail_fwd_chain<R>, dim3(plan_.ntb), dim3(NT), kChainLds, s, pv, tv, V, epsp,
                                dChainGran_.get(), ++chain_epoch_);
+#ifdef IPO_LEAD_STAMPS
+        if (chain_lead_ && chain_epoch_ % 64 == 41) {
+            double st[8][4];
+            IPO_HIP_CHECK(hipStreamSynchronize(s));
+            IPO_HIP_CHECK(hipMemcpyFromSymbol(st, HIP_SYMBOL(g_lead_stats), sizeof(st)));
+            std::fprintf(stderr, "lead R %d ntb %d per step us: solver wait-A %.3f tri %.3f wait-B %.3f\n", R, plan_.ntb,
+                         st[0][0], st[0][1], st[0][2]);
+            for (int w = 1; w <= 4; w++)
+                std::fprintf(stderr, "  wave %d: partial wait %.3f (%g polls) phase3 %.3f loads %.3f\n", w, st[w][0],
+                             st[w][1], st[w][2], st[w][3]);
+        }
+#endif
     }
     ph_end(kPhForward, fwd_launches_, s);
     ph_begin(s);

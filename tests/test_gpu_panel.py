@@ -119,7 +119,7 @@ def test_tail_chain_pairs_bitwise():
 
 def test_tail_chain_lead_bitwise():
     """The forward dense-tail sweep by one lead workgroup with helper
-    workgroups (k_tail_fwd_lead, IPO_HIP_CHAIN_LEAD=1) against one workgroup
-    per block (default): every lane's partial is the same terms in the
+    workgroups (k_tail_fwd_lead, default) against one workgroup per block
+    (IPO_HIP_CHAIN_LEAD=0): every lane's partial is the same terms in the
     same order -- identical dfl001 HSD solves (trace and final values)."""
     assert _solve_env("IPO_HIP_CHAIN_LEAD", "0") == _solve_env("IPO_HIP_CHAIN_LEAD", "1")
