@@ -769,17 +769,18 @@ k_tail_syrk(PlanView p, TailView tv, int kb) {
 // subtracts L(r, j) z_j = 0 * 0 and changes nothing), so the chain is one
 // basic block the compiler can schedule; the same mul-then-subtract per
 // entry as the general form (bitwise the same result).
-// The lane index, opaque to the optimiser: a solve inside a loop would
-// otherwise have its 64 per-step lane masks hoisted out of the loop (128
-// scalar registers, spilled).
+// The lane index, opaque to the optimiser (OPQ solves): a solve inside a
+// loop would otherwise have its 64 per-step lane masks hoisted out of the
+// loop (128 scalar registers, spilled: the sync-free sweeps, the lead
+// sweep).  Outside loops the hoisted masks are cheaper (OPQ = false).
 __device__ __forceinline__ int opaque_lane() {
     int lane = threadIdx.x & 63;
     asm volatile("" : "+v"(lane));
     return lane;
 }
-template <int R, int NS>
+template <int R, int NS, bool OPQ>
 __device__ __forceinline__ void tri_lower_live(double (&zr)[R], const double (*Ls)[PC + 1]) {
-    const int lane = opaque_lane();
+    const int lane = OPQ ? opaque_lane() : (int)(threadIdx.x & 63);
     double lr[NS];
 #pragma unroll
     for (int j = 0; j < NS; j++) lr[j] = Ls[lane][j];
@@ -793,9 +794,9 @@ __device__ __forceinline__ void tri_lower_live(double (&zr)[R], const double (*L
         }
     }
 }
-template <int R, int NS>
+template <int R, int NS, bool OPQ>
 __device__ __forceinline__ void tri_upper_live(double (&zr)[R], const double (*Ls)[PC + 1]) {
-    const int lane = opaque_lane();
+    const int lane = OPQ ? opaque_lane() : (int)(threadIdx.x & 63);
     double lc[NS];
 #pragma unroll
     for (int j = 0; j < NS; j++) lc[j] = Ls[j][lane];
@@ -810,15 +811,15 @@ __device__ __forceinline__ void tri_upper_live(double (&zr)[R], const double (*L
     }
 }
 
-template <int R>
+template <int R, bool OPQ = false>
 __device__ __forceinline__ void tri_lower(double (&zr)[R], const double (*Ls)[PC + 1], const int* lv, int nc,
                                           const double (&eps)[R], int (&bad)[R]) {
-    const int lane = opaque_lane();
+    const int lane = OPQ ? opaque_lane() : (int)(threadIdx.x & 63);
     const uint64_t lm = __ballot(lane < nc && lv[lane]);
     if (lm == (nc >= 64 ? ~0ull : (1ull << nc) - 1ull)) {     // every column live (wave-uniform)
-        if (nc <= 16) tri_lower_live<R, 16>(zr, Ls);
-        else if (nc <= 32) tri_lower_live<R, 32>(zr, Ls);
-        else tri_lower_live<R, 64>(zr, Ls);
+        if (nc <= 16) tri_lower_live<R, 16, OPQ>(zr, Ls);
+        else if (nc <= 32) tri_lower_live<R, 32, OPQ>(zr, Ls);
+        else tri_lower_live<R, 64, OPQ>(zr, Ls);
         return;
     }
     double lr[PC];
@@ -842,15 +843,15 @@ __device__ __forceinline__ void tri_lower(double (&zr)[R], const double (*Ls)[PC
 }
 
 // unit-upper (L11') counterpart; Ls[j][r] = L(j, r) (zero for r >= j)
-template <int R>
+template <int R, bool OPQ = false>
 __device__ __forceinline__ void tri_upper(double (&zr)[R], const double (*Ls)[PC + 1], const int* lv, int nc,
                                           const double (&eps)[R], int (&bad)[R]) {
-    const int lane = opaque_lane();
+    const int lane = OPQ ? opaque_lane() : (int)(threadIdx.x & 63);
     const uint64_t lm = __ballot(lane < nc && lv[lane]);
     if (lm == (nc >= 64 ? ~0ull : (1ull << nc) - 1ull)) {     // every column live (wave-uniform)
-        if (nc <= 16) tri_upper_live<R, 16>(zr, Ls);
-        else if (nc <= 32) tri_upper_live<R, 32>(zr, Ls);
-        else tri_upper_live<R, 64>(zr, Ls);
+        if (nc <= 16) tri_upper_live<R, 16, OPQ>(zr, Ls);
+        else if (nc <= 32) tri_upper_live<R, 32, OPQ>(zr, Ls);
+        else tri_upper_live<R, 64, OPQ>(zr, Ls);
         return;
     }
     double lc[PC];
@@ -1079,7 +1080,7 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
         double zr[R];
 #pragma unroll
         for (int r = 0; r < R; r++) zr[r] = lane < nc ? zl[r][lane] : 0.0;
-        tri_lower<R>(zr, Ls, lv, nc, eps, bad);
+        tri_lower<R, true>(zr, Ls, lv, nc, eps, bad);
         if (lane < nc) {
             // zout: z_s goes to a mirror instead (the chunk items of one
             // supernode each solve it and must all read its right-hand side)
@@ -2151,7 +2152,7 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
                 const double* rd = red + r * 4 * 64 + lane;
                 zr[r] = lane < nc ? zown[r] - (((rd[0] + rd[64]) + rd[128]) + rd[192]) : 0.0;
             }
-            tri_lower<R>(zr, Ls[i & 1], lv + (i & 1) * PC, nc, eps, bad);
+            tri_lower<R, true>(zr, Ls[i & 1], lv + (i & 1) * PC, nc, eps, bad);
             LEAD_T(t2);
             if (lane < nc) {
 #pragma unroll
@@ -2604,7 +2605,7 @@ __device__ __forceinline__ void bwd_sf_solve(const PlanView& p, const SfView& sf
         }
         zr[r] = lane < nc ? zd - sub : 0.0;
     }
-    tri_upper<R>(zr, Ls, lv, nc, eps, bad);
+    tri_upper<R, true>(zr, Ls, lv, nc, eps, bad);
     if (lane < nc) {
 #pragma unroll
         for (int r = 0; r < R; r++) {
