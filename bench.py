@@ -236,6 +236,83 @@ def banded_leg(args):
             "round1_reference_value": 1.8}
 
 
+INTPT_WORKLOAD = "netlib 25fv47 by the path-following method (intpt.c:133-238), fp64, BASELINE configs[1], one GPU"
+
+
+def oracle_run(mps, method, iters=200):
+    """The CPU oracle (oracle/, single-threaded C restatement of ipo) on one
+    solve of `mps`: (status, iterations, loop seconds, setup seconds)."""
+    import oracle_lib
+
+    class Run(C.Structure):
+        _fields_ = [("trace", C.c_void_p), ("max_iter", C.c_int), ("iters", C.c_int), ("t_setup", C.c_double),
+                    ("t_total", C.c_double), ("final_mu", C.c_double), ("final_pobj", C.c_double),
+                    ("final_dobj", C.c_double), ("final_pinf", C.c_double), ("final_dinf", C.c_double)]
+    oracle_lib.build()
+    L = oracle_lib.lib()
+    L.orc_ipo_run.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.POINTER(Run)]
+    L.orc_ipo_run.restype = C.c_int
+    r = Run()
+    r.max_iter = iters
+    st = L.orc_ipo_run(mps.encode(), {"hsd": 0, "intpt": 1, "hsdls": 2}[method], None, C.byref(r))
+    return st, r.iters, r.t_total - r.t_setup, r.t_setup
+
+
+def intpt_leg(args, sync):
+    """BASELINE configs[1]: netlib 25fv47 by intpt (intpt.c:133-238; one KKT
+    factorisation and one refined solve per iteration) on one GPU, problem
+    resident in HBM; a step is one complete solve to intpt's own stop
+    (intpt.c:171).  Beside it the CPU oracle's intpt on the same file (one
+    thread, whole solves repeated for ~10 s) and SURVEY.md 8(d)'s per-iteration
+    roofline (s = 1 solve per iteration)."""
+    import ipo_amd
+    from conftest import mps_path
+    path = mps_path("25fv47")
+    p = ipo_amd.load_mps(path)
+    ctx = ipo_amd.Context(p)
+    try:
+        for _ in range(max(1, args.warmup)):
+            ctx.run("intpt")
+        sync()
+        t0 = time.perf_counter()
+        runs = [ctx.run("intpt") for _ in range(args.intpt_steps)]
+        sync()
+        el = time.perf_counter() - t0
+        _, stt, _ = ctx.run("intpt", timing=True)
+    finally:
+        ctx.close()
+    status, st, _ = runs[-1]
+    iters = sum(r[1]["iters"] for r in runs)
+    ok = all(r[0] == 0 for r in runs)
+    flops, byts = survey_work(st, p.m, p.n, p.nz, solves=1)
+    roof = roofline_of(flops, byts, el / max(iters, 1))
+    roof["per"] = "IPM iteration (SURVEY.md 8(d) algorithmic work, s = 1), timed region"
+    ph = {name: {"ms_per_solve": stt["phase_ms"][i], "launches_per_solve": stt["phase_launches"][i]}
+          for i, name in enumerate(ipo_amd.PHASES) if stt["phase_launches"][i]}
+    out = {"workload": INTPT_WORKLOAD, "value": iters / el if ok else None, "unit": "iterations/s", "n_gpus": 1,
+           "steps": args.intpt_steps, "ms_per_step": 1e3 * el / max(args.intpt_steps, 1),
+           "ms_per_iteration": 1e3 * el / max(iters, 1), "iterations_per_solve": [r[1]["iters"] for r in runs],
+           "status": ipo_amd.STATUS_TEXT.get(status, status), "final_pobj": st["final_pobj"],
+           "final_dobj": st["final_dobj"], "m": p.m, "n": p.n, "nz": p.nz, "lnz": st["lnz"],
+           "setup_s": ctx.setup_seconds, "roofline": roof, "phases_one_solve": ph,
+           "published_optimum": 5.5018458883e3}
+    if args.cpu_iters > 0:
+        try:
+            t_loop, n_it, n_solves = 0.0, 0, 0
+            while t_loop < 10.0 and n_solves < 40:
+                cst, ci, cl, _ = oracle_run(path, "intpt")
+                t_loop, n_it, n_solves = t_loop + cl, n_it + ci, n_solves + 1
+            out["cpu_baseline"] = {"value": n_it / t_loop, "unit": "iterations/s", "cores": 1, "kind": "port",
+                                   "sample": f"{n_solves} complete 25fv47 intpt solves of {ci} iterations (status "
+                                             f"{cst}), oracle/ C restatement, single thread, symbolic setup excluded, "
+                                             f"{t_loop:.1f}s timed", "oracle_iterations": ci}
+            if out["value"] is not None:
+                out["speedup_vs_cpu_baseline"] = out["value"] / out["cpu_baseline"]["value"]
+        except Exception as e:  # noqa: BLE001 -- the GPU number stands on its own
+            out["cpu_baseline"] = {"error": repr(e)}
+    return out
+
+
 HBM_WORKLOAD = ("synthetic random sparse LP, BASELINE configs[3] uniform variant: m=200,000, n=1,000,000, "
                 "4 nnz/column (4.0e6, density 0.002%), seed 20251121")
 
@@ -322,23 +399,10 @@ def pmc_mfma():
 
 def cpu_baseline(mps, iters):
     """Oracle (single-threaded C restatement of ipo) on `iters` HSD iterations of dfl001."""
-    import oracle_lib
-
-    class Run(C.Structure):
-        _fields_ = [("trace", C.c_void_p), ("max_iter", C.c_int), ("iters", C.c_int), ("t_setup", C.c_double),
-                    ("t_total", C.c_double), ("final_mu", C.c_double), ("final_pobj", C.c_double),
-                    ("final_dobj", C.c_double), ("final_pinf", C.c_double), ("final_dinf", C.c_double)]
-    oracle_lib.build()
-    L = oracle_lib.lib()
-    L.orc_ipo_run.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.POINTER(Run)]
-    L.orc_ipo_run.restype = C.c_int
-    r = Run()
-    r.max_iter = iters
-    L.orc_ipo_run(mps.encode(), 0, None, C.byref(r))
-    loop = r.t_total - r.t_setup
-    return {"value": r.iters / loop, "unit": "iterations/s", "cores": 1, "kind": "port",
-            "sample": f"dfl001 hsd iterations 0..{r.iters - 1} ({r.iters} of 117), oracle/ C restatement, "
-                      f"single thread, symbolic setup {r.t_setup:.2f}s excluded, {loop:.1f}s timed",
+    _, it, loop, setup = oracle_run(mps, "hsd", iters)
+    return {"value": it / loop, "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": f"dfl001 hsd iterations 0..{it - 1} ({it} of 117), oracle/ C restatement, "
+                      f"single thread, symbolic setup {setup:.2f}s excluded, {loop:.1f}s timed",
             "host_cpus": os.cpu_count()}
 
 
@@ -375,6 +439,9 @@ def main():
     ap.add_argument("--ba-timeout", type=float, default=300.0, help="watchdog for the block-angular leg (s)")
     ap.add_argument("--banded", choices=["on", "off"], default="on",
                     help="also solve BASELINE configs[3] banded (factor + solve throughput, reported under banded)")
+    ap.add_argument("--intpt", choices=["on", "off"], default="on",
+                    help="also time BASELINE configs[1] (25fv47 by intpt, reported under intpt_25fv47)")
+    ap.add_argument("--intpt-steps", type=int, default=20, help="timed complete 25fv47 intpt solves")
     ap.add_argument("--hbm", choices=["on", "off"], default="on",
                     help="also time the HBM-bound vector kernels on BASELINE configs[3] (reported under hbm_roofline)")
     args = ap.parse_args()
@@ -426,10 +493,12 @@ def main():
                             "gflop_per_s": flops / secs / 1e9, "gbyte_per_s": byts / secs / 1e9,
                             "flops_per_occurrence": st_t["phase_flops"][i], "bytes_per_occurrence": st_t["phase_bytes"][i],
                             "occurrences": cnt}
-        # the dominant kernel: the phase with the most device time; its work
-        # is priced once per factorisation (a dense-tail repair's relaunches
-        # add launches and time, not work): the dense tail at SURVEY.md 8(d)'s
-        # nt^3 / 3 flops of a dense factor
+        # the dominant kernel: the phase with the most device time.  Its work
+        # is SURVEY.md 8(d)'s unit: the phase's share of the reference's narth
+        # (ldlt.c:1243-1248; the dense tail = its columns' sum c_j^2 + 3 c_j +
+        # 1), once per factorisation (a dense-tail repair's relaunches add
+        # launches and time, not work); what the kernels execute (explicit
+        # zeros of the widened tail, padding) is reported beside it
         top = max(phases, key=lambda k: phases[k]["ms_total"])
         ph = phases[top]
         i = ipo_amd.PHASES.index(top)
@@ -456,7 +525,28 @@ def main():
                      "algorithmic_flops_per_occurrence": st_t["phase_flops"][i],
                      "algorithmic_flops_per_launch": flops_l,
                      "algorithmic_bytes_per_launch": bytes_l, "share_of_timed_region": ph["share_of_timed_region"],
+                     "work_unit": "SURVEY.md 8(d): the phase's share of narth (ldlt.c:1243-1248) per factorisation",
                      "tail_repairs": st_t["tail_repairs"], "tail_dep_rounds": st_t["tail_dep_rounds"]})
+        # executed / algorithmic per phase: f64 MFMA flops and HBM bytes from the
+        # committed counter passes (profiles/<round>_pmc_{mfma,traffic}.json)
+        # over the phase's algorithmic flops and bytes per launch
+        for name, phd in phases.items():
+            j = ipo_amd.PHASES.index(name)
+            fl = st_t["phase_flops"][j] * st_t["phase_count"][j] / phd["launches"]
+            by = st_t["phase_bytes"][j] * st_t["phase_count"][j] / phd["launches"]
+            phd["algorithmic_flops_per_launch"], phd["algorithmic_bytes_per_launch"] = fl, by
+            if mf is not None and name in mf["phases"] and fl > 0:
+                phd["executed_over_algorithmic_mfma"] = mf["phases"][name]["f64_mfma_flops_per_launch"] / fl
+            trn = pmc_traffic(name)
+            if trn is not None and by > 0:
+                phd["traffic_over_algorithmic_bytes"] = trn[0] / by
+        if "executed_over_algorithmic_mfma" in ph:
+            roof["executed_over_algorithmic_mfma"] = ph["executed_over_algorithmic_mfma"]
+        if "traffic_over_algorithmic_bytes" in ph:
+            roof["traffic_over_algorithmic_bytes"] = ph["traffic_over_algorithmic_bytes"]
+        # the factor phases' algorithmic flops sum to narth (one factorisation)
+        fac = sum(st_t["phase_flops"][ipo_amd.PHASES.index(k)] for k in ("gather", "diag", "trsm", "tail_syrk", "tail"))
+        roof["factor_phases_sum_over_narth"] = fac / st_t["narth"] if st_t["narth"] else None
 
     out = {
         "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": d.world, "steps": args.steps,
@@ -498,6 +588,11 @@ def main():
             out["end_to_end"] = end_to_end(p, golden, sync)
         except Exception as e:  # noqa: BLE001 -- the headline number stands on its own
             out["end_to_end"] = {"error": repr(e)}
+    if args.intpt == "on" and d.world == 1:
+        try:
+            out["intpt_25fv47"] = intpt_leg(args, sync)
+        except Exception as e:  # noqa: BLE001 -- the headline number stands on its own
+            out["intpt_25fv47"] = {"workload": INTPT_WORKLOAD, "error": repr(e)}
     if args.banded == "on" and d.world == 1:
         try:
             out["banded"] = banded_leg(args)

@@ -3,10 +3,12 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -149,6 +151,34 @@ struct LuQ {
     int qmax = 1;
 };
 std::unique_ptr<LuQ> g_lu_q;
+
+// What the header promises of a caller's Q (ipo_hip.h): kQ[0] = 0 and
+// nondecreasing, rows 0 <= iQ < n strictly ascending in every column (so no
+// duplicate entries: ldlt.c:253-256 subtracts each entry once), and Q
+// symmetric in pattern and value (iolp.c:733-793 leaves QUADS that way).
+// Anything else indexes the ordering's arrays out of range on the host or
+// factors another matrix than the reference would: refused.
+void validate_q(int n, const int* kQ, const int* iQ, const double* Q) {
+    if (n < 0) throw std::invalid_argument("Q: negative dimension");
+    if (kQ[0] != 0) throw std::invalid_argument("Q: kQ[0] != 0");
+    for (int j = 0; j < n; j++) {
+        if (kQ[j + 1] < kQ[j]) throw std::invalid_argument("Q: kQ decreasing at column " + std::to_string(j));
+        for (int k = kQ[j]; k < kQ[j + 1]; k++) {
+            if (iQ[k] < 0 || iQ[k] >= n) throw std::invalid_argument("Q: row index out of range in column " + std::to_string(j));
+            if (k > kQ[j] && iQ[k] <= iQ[k - 1])
+                throw std::invalid_argument("Q: rows not strictly ascending in column " + std::to_string(j));
+        }
+    }
+    for (int j = 0; j < n; j++)
+        for (int k = kQ[j]; k < kQ[j + 1]; k++) {
+            const int i = iQ[k];
+            const int* b = iQ + kQ[i];
+            const int* e = iQ + kQ[i + 1];
+            const int* f = std::lower_bound(b, e, j);
+            if (f == e || *f != j || Q[f - iQ] != Q[k])
+                throw std::invalid_argument("Q: not symmetric at (" + std::to_string(i) + ", " + std::to_string(j) + ")");
+        }
+}
 
 }  // namespace
 
@@ -477,6 +507,12 @@ void forwardbackward(double* Dn, double* Dm, double* dx, double* dy) {
 int ipo_hip_ldlt_set_q(int n, const int* kQ, const int* iQ, const double* Q, int max) {
     if (g_lu) { set_err("ipo_hip_ldlt_set_q after ldltfac (call inv_clo first)"); return -1; }
     if (!kQ || n < 0) { g_lu_q.reset(); return 0; }
+    try {
+        validate_q(n, kQ, iQ, Q);
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
     auto q = std::make_unique<LuQ>();
     q->kQ.assign(kQ, kQ + n + 1);
     q->iQ.assign(iQ, iQ + kQ[n]);
@@ -503,6 +539,7 @@ ipo_hip_kkt* ipo_hip_kkt_create(int m, int n, const int* kA, const int* iA, cons
 ipo_hip_kkt* ipo_hip_kkt_create_q(int m, int n, const int* kA, const int* iA, const double* A, const int* kQ,
                                   const int* iQ, const double* Q, int qmax) {
     try {
+        if (kQ) validate_q(m, kQ, iQ, Q);
         auto* k = new ipo_hip_kkt();
         IPO_HIP_CHECK(hipStreamCreateWithFlags(&k->stream, hipStreamNonBlocking));
         k->m = m;

@@ -3278,24 +3278,35 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         work_flops[kPhDiag] = df; work_bytes[kPhDiag] = db;
         work_flops[kPhTrsm] = tf; work_bytes[kPhTrsm] = tb;
         work_flops[kPhSyrk] = sf; work_bytes[kPhSyrk] = sb;
+        // Algorithmic flops per factorisation in SURVEY.md 8(d)'s unit: the
+        // reference's narth (ldlt.c:1243-1248), split by the phase doing each
+        // column's work (kkt_plan.h: narth_tail / narth_gather / narth_panel,
+        // which sum to narth).  What the kernels execute (plan flops above,
+        // the dense tail's explicit zeros) is not the work.  Bytes: each
+        // phase's entries of L read and written once (+ the gather's source
+        // reads from the plan).
+        (void)sdf; (void)stf; (void)df; (void)tf; (void)sf; (void)lxs;
+        work_flops[kPhGather] = P.narth_gather;
         if (use_panel_) {   // k_panel_w does both: the diag phase carries the sparse trsm work;
             // the dense tail is its own phase (k_tail_pr: panels + deferred
-            // trailing updates), priced as SURVEY.md 8(d) prices a dense
-            // factor: nt^3 / 3 flops, its lower triangle read and written once
-            work_flops[kPhDiag] = sdf + stf; work_bytes[kPhDiag] = sdb + stb;
+            // trailing updates; its repair launches)
+            work_flops[kPhDiag] = P.narth_panel; work_bytes[kPhDiag] = sdb + stb;
             work_flops[kPhTrsm] = work_bytes[kPhTrsm] = 0;
             work_flops[kPhSyrk] = work_bytes[kPhSyrk] = 0;
-            const double nt = P.nt;
-            work_flops[kPhTail] = nt * nt * nt / 3.0;
-            work_bytes[kPhTail] = 16.0 * 0.5 * nt * (nt + 1.0);
+            work_flops[kPhTail] = P.narth_tail;
+            work_bytes[kPhTail] = 16.0 * (static_cast<double>(P.lnz_tail) + P.nt);
+        } else {            // per-phase path: the tail's work goes with its trailing updates
+            work_flops[kPhDiag] = P.narth_panel;
+            work_flops[kPhTrsm] = 0;
+            work_flops[kPhSyrk] = P.narth_tail;
         }
-        // a sweep reads every factor entry once (sparse panels + the tail's
-        // lower triangle) and the vector / update values it touches
-        const double tail_tri = 0.5 * P.nt * (P.nt + 1.0);
-        const double nrowsR = P.rowptr.empty() ? 0 : P.rowptr.back();
+        // a sweep (s (4 nnz(L) + N) per iteration, a solve
+        // being one forward and one backward sweep): 2 nnz(L) + N / 2 flops,
+        // every entry of L read once (12 B with its index) and the vector
+        // values in and out
         for (int ph : {kPhForward, kPhBackward}) {
-            work_flops[ph] = 2.0 * (lxs + tail_tri);
-            work_bytes[ph] = 8.0 * (lxs + tail_tri) + 8.0 * 2 * T_ + (ph == kPhForward ? 12.0 : 12.0) * nrowsR;
+            work_flops[ph] = 2.0 * static_cast<double>(P.lnz) + 0.5 * T_;
+            work_bytes[ph] = 12.0 * static_cast<double>(P.lnz) + 16.0 * T_;
         }
     }
     mark("per-task source descriptors ");

@@ -26,6 +26,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
+#include <exception>
 #include <mutex>
 #include <stdexcept>
 #include <thread>
@@ -126,7 +127,12 @@ std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* 
     }
     constexpr size_t kSharedMin = 16384;      // pieces at least this large go to the shared list
 
-    auto worker = [&]() {
+    // a worker that throws (bad_alloc on its per-thread arrays, ...) stores
+    // the first exception and stops the pool; it is rethrown after the join,
+    // so the C API's try / catch sees it instead of std::terminate
+    std::exception_ptr failure;
+    std::atomic<bool> failed{false};
+    auto work = [&]() {
         std::vector<int> inset(T, -1), dist(T, -1), order;
         auto inset_of = [&](int w) { return inset[w]; };
         auto set_inset = [&](int w, int st) { inset[w] = st; };
@@ -279,14 +285,14 @@ std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* 
             Job J;
             {
                 std::unique_lock<std::mutex> g(mu);
-                cv.wait(g, [&] { return !shared.empty() || busy == 0; });
-                if (shared.empty()) return;            // nothing queued and nobody working: done
+                cv.wait(g, [&] { return failed || !shared.empty() || busy == 0; });
+                if (failed || shared.empty()) return;  // nothing queued and nobody working: done
                 J = std::move(shared.back());
                 shared.pop_back();
                 busy++;
             }
             split(std::move(J));
-            while (!local.empty()) {
+            while (!local.empty() && !failed) {
                 Job c = std::move(local.back());
                 local.pop_back();
                 split(std::move(c));
@@ -298,11 +304,22 @@ std::vector<int> nested_dissection_perm(int m, int n, const int* kA, const int* 
             }
         }
     };
+    auto worker = [&]() {
+        try {
+            work();
+        } catch (...) {
+            std::lock_guard<std::mutex> g(mu);
+            if (!failed) failure = std::current_exception();
+            failed = true;
+            cv.notify_all();
+        }
+    };
     const int nth = setup_threads();
     std::vector<std::thread> pool;
     for (int i = 1; i < nth; i++) pool.emplace_back(worker);
     worker();
     for (auto& th : pool) th.join();
+    if (failure) std::rethrow_exception(failure);
     for (int v = 0; v < T; v++)
         if (perm[v] < 0) throw std::logic_error("nested dissection: incomplete permutation");
     return perm;

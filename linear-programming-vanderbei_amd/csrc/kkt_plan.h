@@ -197,6 +197,11 @@ struct KktPlan {
     // reference statistics
     int64_t lnz = 0;                // nnz strict lower L (reference pattern)
     double narth = 0.0;
+    // narth by the phase doing each column's work (build_kkt_plan): the dense
+    // tail's columns, the sparse columns' products beyond their supernode
+    // (gather) and the rest (panels); they sum to narth
+    double narth_tail = 0.0, narth_gather = 0.0, narth_panel = 0.0;
+    int64_t lnz_tail = 0;           // entries of L's pattern in the dense tail's columns
     int pdf = 0, denwin = 0;
     int max_h = 0, max_nc = 0;
     double flops_factor = 0.0;      // sum over updates of 2*ra*rc*nc (approx)

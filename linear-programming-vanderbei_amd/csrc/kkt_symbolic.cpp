@@ -515,6 +515,29 @@ KktPlan build_kkt_plan(int m, int n, const int* kA, const int* iA, const int* kA
 
     auto panel_h = [&](int s) { return P.col0[s + 1] - P.col0[s] + (P.rowptr[s + 1] - P.rowptr[s]); };
 
+    // ---- narth (ldlt.c:1243-1248: sum_j c_j^2 + 3 nnz(L) + N) split by the
+    //      phase whose kernels do each column's work (SURVEY.md 8(d)'s unit
+    //      per phase): a tail column's c_j^2 + 3 c_j + 1 is the dense tail's;
+    //      a sparse column's outer product over the rows beyond its supernode,
+    //      min(c_j, |R_s|)^2, the gather's; the rest (the products inside the
+    //      panel, the scaling, the pivot) the panels'.  The three sum to narth.
+    {
+        double tail = 0.0, gath = 0.0;
+        for (int j = tc; j < T; j++) {
+            const double c = cnt[j];
+            tail += c * c + 3.0 * c + 1.0;
+            P.lnz_tail += cnt[j];
+        }
+        for (int j = 0; j < tc; j++) {
+            const int s = P.sup_of[j];
+            const double r = std::min(cnt[j], P.rowptr[s + 1] - P.rowptr[s]);
+            gath += r * r;
+        }
+        P.narth_tail = std::min(tail, P.narth);
+        P.narth_gather = std::min(gath, P.narth - P.narth_tail);
+        P.narth_panel = P.narth - P.narth_tail - P.narth_gather;
+    }
+
     // ---- sparse supernodal tree + levels (children have smaller indices)
     P.parent.assign(ns, -1);
     P.level.assign(ns, 0);

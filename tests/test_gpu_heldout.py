@@ -67,18 +67,40 @@ def test_heldout_scaled_within_envelope(name):
         bits = [base[f"{k}_iters"] for k in ("golden", "fma", "reverse", "sorted")]
         slack = max(1, max(bits) - min(bits))
     assert it <= max(its) + slack, (it, its, slack)
-    # an optimum is claimed where the reference's own order (order 0) ends
-    # optimal, as test_gpu_ipm claims it where the golden run does: scaled
-    # forplan ends "optimal" by HSD's mu test alone under the FMA order and on
-    # the GPU (objective 285 against the published 664), as unscaled forplan
-    # does on the GPU, while the reference's own order stalls to the limit
-    if st == "optimal solution" and v[0]["status"] == "optimal solution":
+    # an "optimal solution" is held to an optimum: where the reference's own
+    # order (order 0) ends optimal, as test_gpu_ipm holds it where the golden
+    # run does; where it does not, to the published optimum, or else to the
+    # objectives of an order that ends optimal (a GPU "optimal"
+    # is never passed unchecked).  The one exception is listed with its reason.
+    if st == "optimal solution":
+        rows, _ = parse(r["trace"])          # the printed last line, as check_optimum reads it
+        got = (rows[-1][1], rows[-1][3])
+        opt_orders = [o for o in v if o["status"] == "optimal solution"]
         if name in OPT:
             target = -OPT[name]["sense"] * OPT[name]["optimum"]
             tol = WIDE.get(("hsd", name), (1e-5, ""))[0]
-            targets = (target, target)
+            targets = [(target, target)]
+        elif opt_orders:
+            targets, tol = [(o["pobj"], o["dobj"]) for o in opt_orders], 1e-5
         else:
-            targets, tol = (v[0]["pobj"], v[0]["dobj"]), 1e-5
-        rows, _ = parse(r["trace"])          # the printed last line, as check_optimum reads it
-        for k, g, t in zip(("pobj", "dobj"), (rows[-1][1], rows[-1][3]), targets):
-            assert abs(g - t) <= tol * max(1.0, abs(t)), (k, g, t)
+            targets, tol = [], 0.0
+        if v[0]["status"] != "optimal solution" and name in FALSE_OPTIMAL:
+            # documented: HSD's mu test ends the solve away from feasibility
+            assert r["stats"]["final_pinf"] > 1e-6 or r["stats"]["final_dinf"] > 1e-6, (name, FALSE_OPTIMAL[name])
+            return
+        assert targets, f"{name}: GPU 'optimal solution' with no optimum to hold it to"
+        ok = [all(abs(g - t) <= tol * max(1.0, abs(t)) for g, t in zip(got, tg)) for tg in targets]
+        assert any(ok), (name, got, targets, tol)
+
+
+# Problems whose GPU run may end "optimal solution" by HSD's mu < 1e-12 test
+# alone (hsd.c:155) while the iterate is still far from feasible: the
+# reference's own order stalls to the iteration limit there, one of the other
+# orders stops "optimal" the same way at another objective.  Such an
+# "optimal" certifies nothing, so no objective is claimed; the test asserts
+# instead that the run is indeed infeasible at its stop.
+FALSE_OPTIMAL = {
+    "forplan": "scaled forplan: orders 0-2 stop at the iteration limit at objectives 321 / 298 / 165, the FMA order "
+               "'optimal' at 522 / 557 with large infeasibilities; the published optimum (-664.2) is reached by none "
+               "(the unscaled problem ends the same way on the GPU and under the FMA order, DESIGN.md section 3)",
+}

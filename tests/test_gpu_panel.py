@@ -95,8 +95,13 @@ def test_tail_repair():
         check_hsd("dfl001", _with_env("IPO_HIP_TAIL_REPAIR", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))[1])
 
 
-def _solve_env(var, val):
-    status, text, st = _with_env(var, val, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))
+def _solve_env(var, val, name="dfl001", extra=()):
+    def run():
+        return ipo_amd.run_mps(mps_path(name), "hsd")
+    fn = run
+    for v2, x2 in extra:
+        fn = (lambda f, v2=v2, x2=x2: (lambda: _with_env(v2, x2, f)))(fn)
+    status, text, st = _with_env(var, val, fn)
     return status, text, {k: st[k] for k in sorted(st) if k.startswith("final") or k == "iters"}
 
 
@@ -110,16 +115,23 @@ def test_hsd_overlap_bitwise():
 
 def test_tail_chain_pairs_bitwise():
     """Dense-tail substitution chains with two 64-row blocks per workgroup
-    (k_tail_fwd_pair / k_tail_bwd_pair, default) against one block per
-    workgroup (IPO_HIP_CHAIN_PAIRS=0): the same arithmetic in the same order,
-    the first block's z handed on inside the workgroup -- identical dfl001
-    HSD solves (trace and final values)."""
-    assert _solve_env("IPO_HIP_CHAIN_PAIRS", "0") == _solve_env("IPO_HIP_CHAIN_PAIRS", "1")
+    (k_tail_fwd_pair / k_tail_bwd_pair, IPO_HIP_CHAIN_PAIRS=1; off by default)
+    against one block per workgroup (IPO_HIP_CHAIN_PAIRS=0): the same
+    arithmetic in the same order, the first block's z handed on inside the
+    workgroup -- identical dfl001 HSD solves (trace and final values).  The
+    lead forward sweep is off on both sides (IPO_HIP_CHAIN_LEAD=0), since it
+    takes precedence over the forward pair kernel."""
+    off = (("IPO_HIP_CHAIN_LEAD", "0"),)
+    assert _solve_env("IPO_HIP_CHAIN_PAIRS", "0", extra=off) == _solve_env("IPO_HIP_CHAIN_PAIRS", "1", extra=off)
 
 
-def test_tail_chain_lead_bitwise():
+@pytest.mark.parametrize("name", ["dfl001", "25fv47", "bnl2", "greenbea", "brandy"])
+def test_tail_chain_lead_bitwise(name):
     """The forward dense-tail sweep by one lead workgroup with helper
     workgroups (k_tail_fwd_lead, default) against one workgroup per block
     (IPO_HIP_CHAIN_LEAD=0): every lane's partial is the same terms in the
-    same order -- identical dfl001 HSD solves (trace and final values)."""
-    assert _solve_env("IPO_HIP_CHAIN_LEAD", "0") == _solve_env("IPO_HIP_CHAIN_LEAD", "1")
+    same order -- identical HSD solves (trace and final values).  Tails of 70
+    blocks (dfl001), 7 and 9 (25fv47 nt 396, bnl2 559: odd counts, partial
+    last blocks: the extra step after the two-step loop), 12 (greenbea 732,
+    partial) and 3 (brandy 155: no helper workgroups)."""
+    assert _solve_env("IPO_HIP_CHAIN_LEAD", "0", name) == _solve_env("IPO_HIP_CHAIN_LEAD", "1", name)

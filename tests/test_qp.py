@@ -182,3 +182,41 @@ def test_oracle_factor_with_q_solves_the_qp_system():
         ry = fy - (A @ dx - E * dy - qmax * (Qm @ dy))
         rx = fx - (A.T @ dy + D * dx)
         assert max(np.abs(ry).max(), np.abs(rx).max()) <= 1e-9 * (1 + max(np.abs(fy).max(), np.abs(fx).max()))
+
+
+def test_set_q_validates_input():
+    """ipo_hip_ldlt_set_q (host only: no device until ldltfac) refuses a Q
+    the header's contract excludes -- rows out of range, unsorted or
+    duplicated rows in a column, an asymmetric pattern or value -- with -1
+    and a message, and accepts a valid one."""
+    import ctypes as C
+    L = ipo_amd.lib()
+    L.ipo_hip_ldlt_set_q.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    L.ipo_hip_ldlt_set_q.restype = C.c_int
+    L.inv_clo.restype = None
+
+    def setq(kQ, iQ, Q, n=None):
+        kQ, iQ, Q = (np.ascontiguousarray(kQ, np.int32), np.ascontiguousarray(iQ, np.int32),
+                     np.ascontiguousarray(Q, np.float64))
+        n = len(kQ) - 1 if n is None else n
+        rc = L.ipo_hip_ldlt_set_q(n, kQ.ctypes.data, iQ.ctypes.data, Q.ctypes.data, 1)
+        L.inv_clo()
+        return rc, ipo_amd.last_error()
+
+    kQ, iQ, Q = random_q(12, 3)
+    assert setq(kQ, iQ, Q)[0] == 0
+    bad_row = iQ.copy(); bad_row[2] = 12
+    rc, msg = setq(kQ, bad_row, Q)
+    assert rc == -1 and "out of range" in msg
+    j = next(j for j in range(12) if kQ[j + 1] - kQ[j] >= 2)
+    unsorted = iQ.copy(); unsorted[kQ[j]], unsorted[kQ[j] + 1] = unsorted[kQ[j] + 1], unsorted[kQ[j]]
+    rc, msg = setq(kQ, unsorted, Q)
+    assert rc == -1 and "ascending" in msg
+    asym = Q.copy()
+    k = next(k for k in range(kQ[j], kQ[j + 1]) if iQ[k] != j)
+    asym[k] += 1.0
+    rc, msg = setq(kQ, iQ, asym)
+    assert rc == -1 and "symmetric" in msg
+    # diagonal only, one column without its twin: (1, 0) present, (0, 1) absent
+    rc, msg = setq([0, 2, 3], [0, 1, 1], [1.0, 0.5, 1.0])
+    assert rc == -1 and "symmetric" in msg
