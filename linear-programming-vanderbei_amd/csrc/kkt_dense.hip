@@ -581,13 +581,42 @@ __device__ __forceinline__ void df_wait(const int* prog, int v, int& seen) {
 // Software-pipelined: step i forms pivot i + 1 (its column updated first,
 // by v_readlane) before the rest of its updates, so the division of the next
 // pivot issues interleaved with them instead of after them.
-template <bool FULL>
+// DEP (the dense tail's second pass after a pivot failed the zero test, see
+// panel_w_body): such a pivot takes the dependent-pivot rule of ldlt.c:600-614
+// in the chain -- +-1e-8 by node class when some entry of the column below it
+// reaches 1e-2, else the column is dropped (l = 0, d kept, live 0).  The
+// block's own rows decide "keep" for certain; "drop" also needs the rows
+// below the block, which other workgroups hold: each workgroup checks its
+// tile against the decision (win_solve) and the panel bails if one fails.
+struct DepState {
+    const int* sign;       // node class of the block's columns (c0-relative)
+    int* lv;               // LDS: live mark per column, published with dv
+    int* spec;             // LDS: the speculation failed (or met a NaN)
+    int ndep;              // dependent pivots of this wave's window
+};
+
+__device__ __forceinline__ void dep_pivot(double col, int k, int lane, int h0, double& dk, int& alive, DepState& ds) {
+    const bool in = lane > k && lane < h0;
+    const bool big = __ballot(in && !(fabs(col) < 1.0e+6 * 1.0e-8)) != 0;   // includes NaN
+    const bool nan = __ballot(in && col != col) != 0;
+    if (nan && lane == 0) *ds.spec = 1;     // the host repair decides it (the reference's NaN-order max)
+    if (big) dk = (ds.sign[k] < 0 ? -1.0 : 1.0) * 1.0e-8;   // y-nodes -, x-nodes +
+    else alive = 0;                                        // dropped, d keeps its value
+    ds.ndep++;
+}
+
+template <bool FULL, bool DEP>
 __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& tz_any, int cw0, int nc, int lane,
                                            int h0, double tau, double (*Ct)[CTS], double (*Lr)[PC], double* dv,
-                                           int* prog) {
+                                           int* prog, DepState& ds) {
     double dk = lane_bcast(a[0], cw0);
-    tz_any |= fabs(dk) <= tau * lane_bcast(dsc, cw0);   // no short-circuit: no branch
-    double l = lane > cw0 && lane < h0 ? a[0] / dk : 0.0;
+    int alive = 1;
+    if (DEP) {
+        if (fabs(dk) <= tau * lane_bcast(dsc, cw0)) dep_pivot(a[0], cw0, lane, h0, dk, alive, ds);
+    } else {
+        tz_any |= fabs(dk) <= tau * lane_bcast(dsc, cw0);   // no short-circuit: no branch
+    }
+    double l = alive && lane > cw0 && lane < h0 ? a[0] / dk : 0.0;
 #pragma unroll
     for (int i = 0; i < WIN; i++) {
         const int k = cw0 + i;
@@ -598,6 +627,7 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
             Ct[k][lane] = c;
             Lr[k][lane] = l;
             dv[k] = dk;                   // every lane stores the same value: no EXEC branch
+            if (DEP) ds.lv[k] = alive;
             // the wavefront fence orders the reads of the row just written
             // (and the published count) after the writes for the compiler;
             // the LDS runs one wave's operations in issue order
@@ -611,8 +641,13 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
                 // pivot k + 1: its column by v_readlane, then l of the next step
                 a[i + 1] = a[i + 1] - lk * lane_bcast(c, k + 1);
                 dk = lane_bcast(a[i + 1], k + 1);
-                tz_any |= fabs(dk) <= tau * lane_bcast(dsc, k + 1);
-                l = lane > k + 1 && lane < h0 ? a[i + 1] / dk : 0.0;
+                if (DEP) {
+                    alive = 1;
+                    if (fabs(dk) <= tau * lane_bcast(dsc, k + 1)) dep_pivot(a[i + 1], k + 1, lane, h0, dk, alive, ds);
+                } else {
+                    tz_any |= fabs(dk) <= tau * lane_bcast(dsc, k + 1);
+                }
+                l = alive && lane > k + 1 && lane < h0 ? a[i + 1] / dk : 0.0;
             }
 #pragma unroll
             for (int q = i + 2; q < WIN; q++) a[q] = a[q] - lk * cc[q];
@@ -659,16 +694,25 @@ __device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw,
 
 // Window solve of the tile rows (half 1, wave w): solve_rows' form, step i
 // once half 0 has published pivot i of the window (wprog); publishes Lb.
-template <bool FULL>
+// DEP: a dropped column (lv 0) gives l = 0, and this tile's entries of it
+// must stay below 1e-2 (the speculation of dep_pivot), else the panel bails.
+template <bool FULL, bool DEP>
 __device__ __forceinline__ void win_solve(double (&a)[WIN], int cw0, int nc, bool rok, int lane, double (*Ct)[CTS],
-                                          double (*Lb)[PC], const double* dv, const int* wprog, int* prog) {
+                                          double (*Lb)[PC], const double* dv, const int* wprog, int* prog,
+                                          DepState& ds) {
     int seen = 0;
 #pragma unroll
     for (int i = 0; i < WIN; i++) {
         const int k = cw0 + i;
         if (FULL || k < nc) {
             df_wait(wprog, i + 1, seen);
-            const double l = rok ? a[i] / dv[k] : 0.0;
+            double l;
+            if (DEP && !ds.lv[k]) {
+                if (__ballot(rok && !(fabs(a[i]) < 1.0e+6 * 1.0e-8)) != 0 && lane == 0) *ds.spec = 1;
+                l = 0.0;
+            } else {
+                l = rok ? a[i] / dv[k] : 0.0;
+            }
             a[i] = l;
             Lb[k][lane] = l;
             df_publish(prog, i + 1);
@@ -702,17 +746,40 @@ struct PanelLds {
     double Lr[PC][PC];
     double Lb[PC][PC];
     double dv[PC];
+    int lv[PC];                           // DEP pass: live mark per column
     int prog[8];                          // published columns: windows of half 0, then of half 1
     int tiny;
+    int spec;                             // DEP pass: a tile (or a NaN) contradicts a dropped column
+    int ndep;                             // DEP pass: dependent pivots of the block
 };
 
 // Workgroup `bid` of a windowed panel: fused unit f0 + bid of a sparse level
 // (fu_sup != nullptr) or block column kb of the dense tail, whose W = L21 D
 // goes to wtail.
-__device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __restrict__ fu_sup,
+// Dependent pivots in the dense tail (dep != 0, k_tail_pr): the first pass
+// (DEP false) ends unwritten as soon as the diagonal block has a pivot that
+// fails the zero test -- every workgroup of the panel sees it, the block is
+// factored identically in each -- and returns true; the caller reruns the
+// panel with DEP true, which applies ldlt.c:600-614 in the chain (dep_pivot):
+// a column "kept" with +-1e-8 is certain from the block's rows alone; a
+// dropped one is checked by every workgroup on its own tile (win_solve).  A
+// workgroup whose tile contradicts a drop (or meets a NaN) bails as the first
+// pass would have (flags[1] bit 4 | 16, flags[2]), and the host resumes the
+// look-ahead from this block column (KktDevice::repair_tail) after putting
+// back what the other workgroups wrote: the DEP pass saves its tile rows and
+// workgroup 0 the block's |terms| into tv.W (unused by the look-ahead) before
+// anything is written, and workgroup 0 leaves the dependent pivots it added
+// to flags[0] in flags[3] (k_tail_restore).  Where the speculation holds (122
+// of the 124 dependent pivots of the oracle's dfl001_100/110/114 factors that
+// fall in the GPU's dense tail), the block costs one more panel pass instead
+// of the host round trips and relaunches of a repair; the factor is bitwise
+// the repair path's (tests/test_gpu_panel.py).  dep == 2 (IPO_HIP_TAIL_SPEC=2,
+// tests only) treats every drop as contradicted, which exercises the restore.
+template <bool DEP = false>
+__device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __restrict__ fu_sup,
                                              const int* __restrict__ fu_j, int f0, const TailView& tv, int kb, int bid,
                                              PanelLds& S, double* wtail, bool pre = false,
-                                             const int* bailp = nullptr, int bt = 0) {
+                                             const int* bailp = nullptr, int bt = 0, int dep = 0) {
     // a bail flag of an earlier step (dense tail, see k_tail_pr): read first,
     // tested once this workgroup's operand loads are in flight
     const int bailed = bailp ? *bailp : 0;
@@ -764,7 +831,20 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
     double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
     double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
-    if (!pre && bailed && bailed - 1 < bt) return;
+    if (!pre && bailed && bailed - 1 < bt) return false;
+    if (DEP) {
+        // what this pass may overwrite, saved for k_tail_restore: the tile
+        // rows (rows >= 64 of the block column, as in S) and workgroup 0's
+        // |terms| of the block's pivots (rows 0..nc-1 of W's column 0)
+        if (h1 && rok && tile) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) {
+                const int c = cw0 + q;
+                if (c < nc) tv.W[row + (size_t)c * tv.nt] = a[q];
+            }
+        }
+        if (j == 0 && !h1 && lane < nc && (lane >> 4) == w) tv.W[lane] = dsc;
+    }
     if (pre) {
         // dense tail, block column kb > 0: block kb - 1's update of this
         // workgroup's rows, k_tail_syrk's MFMA fragments and order; the
@@ -791,7 +871,7 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
                 vj[u] = okj ? y : 0.0;
                 vw[u] = okd ? x * dk : 0.0;
             }
-            if (bailed && bailed - 1 < bt) return;     // workgroup-uniform
+            if (bailed && bailed - 1 < bt) return false;     // workgroup-uniform
 #pragma unroll
             for (int u = 0; u < NU; u++) {
                 const int k = (tid + u * PNT) / TR;
@@ -851,8 +931,9 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
         PANEL_STAMP(14);
     }
     if (tid < 8) S.prog[tid] = 0;
-    if (tid == 0) tiny_sh = 0;
+    if (tid == 0) { tiny_sh = 0; S.spec = dep == 2 ? -1 : 0; S.ndep = 0; }
     __syncthreads();
+    DepState ds{p.sign + c0, S.lv, &S.spec, 0};
     PANEL_STAMP(0);
     // half 0, wave w: updates of windows 0 .. w - 1, then factor window w;
     // half 1, wave w: the same updates on the tile rows, then solve window w.
@@ -880,13 +961,14 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
         if (!h1) {
             bool tz_any = false;
             __builtin_amdgcn_s_setprio(3);
-            if (cw0 + WIN <= nc) win_factor<true>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv, prog + w);
-            else win_factor<false>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv, prog + w);
+            if (cw0 + WIN <= nc) win_factor<true, DEP>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv, prog + w, ds);
+            else win_factor<false, DEP>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv, prog + w, ds);
             if (tz_any && lane == 0) tiny_sh = 1;
+            if (DEP && ds.ndep && lane == 0) atomicAdd(&S.ndep, ds.ndep);
         } else {
             __builtin_amdgcn_s_setprio(3);
-            if (cw0 + WIN <= nc) win_solve<true>(a, cw0, nc, rok, lane, Ct, Lb, dv, S.prog + w, prog + w);
-            else win_solve<false>(a, cw0, nc, rok, lane, Ct, Lb, dv, S.prog + w, prog + w);
+            if (cw0 + WIN <= nc) win_solve<true, DEP>(a, cw0, nc, rok, lane, Ct, Lb, dv, S.prog + w, prog + w, ds);
+            else win_solve<false, DEP>(a, cw0, nc, rok, lane, Ct, Lb, dv, S.prog + w, prog + w, ds);
         }
         __builtin_amdgcn_s_setprio(0);
         PANEL_STAMP(2);
@@ -915,12 +997,21 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     PANEL_STAMP(12);
-    if (tiny_sh) {
+    if (!DEP && tiny_sh && dep) return true;      // every workgroup of the panel: rerun with DEP
+    // DEP: spec < 0 (dep == 2) with a dropped column in the block counts as contradicted
+    const bool fail = DEP ? (S.spec > 0 || (S.spec < 0 && S.ndep > 0 && [&] {
+                                 for (int k = 0; k < nc; k++)
+                                     if (!S.lv[k]) return true;
+                                 return false;
+                             }()))
+                          : tiny_sh != 0;
+    if (fail) {
         if (tid == 0) {
-            atomicOr(&p.flags[1], fu_sup ? 2 : 4);   // bit: where it bailed
+            atomicOr(&p.flags[1], fu_sup ? 2 : DEP ? 4 | 16 : 4);   // bit: where it bailed (16: restore first)
             if (!fu_sup) atomicMax(&p.flags[2], kb + 1);   // the dense-tail block column
+            if (DEP && j == 0) p.flags[3] = 0;            // workgroup 0 added no dependent pivots
         }
-        return;
+        return false;
     }
     if (!fu_sup) {
         if (w < nwin && (h1 ? rok && tile : (j == 0 && lane >= nc && lane < h0))) {
@@ -932,7 +1023,7 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
         }
         if (pre && j == 0 && !h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc_pre;
     }
-    if (j != 0) return;
+    if (j != 0) return false;
     // workgroup 0: L11' into the upper slot through an LDS transpose (Ct is
     // free again), D, mark
     if (!h1) {
@@ -942,8 +1033,13 @@ __device__ __forceinline__ void panel_w_body(const PlanView& p, const int* __res
     __syncthreads();
     for (int rr = 1 + wv; rr < nc; rr += PNT / 64)
         if (lane < rr) panel[lane + (size_t)rr * ld] = Ct[rr][lane];
-    if (tid < nc) { p.dg[c0 + tid] = dv[tid]; p.live[c0 + tid] = 1; }
+    if (tid < nc) { p.dg[c0 + tid] = dv[tid]; p.live[c0 + tid] = DEP ? S.lv[tid] : 1; }
+    if (DEP && tid == 0) {
+        if (S.ndep) atomicAdd(&p.flags[0], S.ndep);
+        p.flags[3] = S.ndep;                       // taken back by k_tail_restore if a later check fails
+    }
     PANEL_STAMP(13);
+    return false;
 }
 
 __global__ void __launch_bounds__(PNT)
@@ -1222,14 +1318,36 @@ k_tail_pr(PlanView p, TailView tv, int t, int gp) {
     // not this launch's own, whose visits must complete): the host
     // resumes the look-ahead from there
     if ((int)blockIdx.x < gp) {
-        panel_w_body(p, nullptr, nullptr, 0, tv, t, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), nullptr, t > 0,
-                     p.flags + 2, t);
+        PanelLds& S = *reinterpret_cast<PanelLds*>(lds);
+        if (panel_w_body<false>(p, nullptr, nullptr, 0, tv, t, blockIdx.x, S, nullptr, t > 0, p.flags + 2, t, tv.dep)) {
+            __syncthreads();           // every wave has read the first pass's verdict
+            panel_w_body<true>(p, nullptr, nullptr, 0, tv, t, blockIdx.x, S, nullptr, t > 0, p.flags + 2, t, tv.dep);
+        }
         return;
     }
     int tile = blockIdx.x - gp, c = t + 1;
     while (tile >= tv.ntb - c) { tile -= tv.ntb - c; c++; }
     const int b1 = visit_hi(t, c, tv.vk);
     visit_tile512(p, tv, c + tile, c, max(0, b1 - tv.vk), b1, *reinterpret_cast<SyrkLds*>(lds), p.flags + 2, t);
+}
+
+// A DEP pass of block column kb failed its check in some workgroup (flags[1]
+// bit 16) after others had written: put back the tile rows and the block's
+// |terms| it saved in tv.W and the dependent pivots workgroup 0 added, so the
+// host repair starts from the column as the look-ahead left it.
+__global__ void __launch_bounds__(256)
+k_tail_restore(PlanView p, TailView tv, int kb) {
+    const int nt = tv.nt, k0 = kb * PC, nc = min(PC, nt - k0), h = nt - k0, c = blockIdx.y;
+    double* panel = tv.S + k0 + (size_t)k0 * nt;
+    for (int row = nc + blockIdx.x * 256 + threadIdx.x; row < h; row += gridDim.x * 256)
+        panel[row + (size_t)c * nt] = tv.W[row + (size_t)c * nt];
+    if (blockIdx.x == 0 && c == 0) {
+        if ((int)threadIdx.x < nc) p.dscale[tv.tc + k0 + threadIdx.x] = tv.W[threadIdx.x];
+        if (threadIdx.x == 0) {
+            p.flags[0] -= p.flags[3];
+            p.flags[3] = 0;
+        }
+    }
 }
 
 // Block t's update of block column t + 1 only (tiles (bi, t + 1), bi > t):
@@ -1332,6 +1450,12 @@ void launch_tail_step(const PlanView& pv, const TailView& tv, int t, hipStream_t
     const int gp = std::max(1, (h + TR - 1) / TR - 1);
     const int nr = tail_visit_tiles(tv.ntb, t, tv.vk);
     hipLaunchKernelGGL(k_tail_pr, dim3(gp + nr), dim3(PNT), 0, s, pv, tv, t, gp);
+}
+
+void launch_tail_restore(const PlanView& pv, const TailView& tv, int kb, hipStream_t s) {
+    const int nc = std::min(PC, tv.nt - kb * PC), rows = tv.nt - kb * PC - nc;
+    hipLaunchKernelGGL(k_tail_restore, dim3(std::max(1, std::min(64, (rows + 255) / 256)), nc), dim3(256), 0, s, pv, tv,
+                       kb);
 }
 
 void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, hipStream_t s) {

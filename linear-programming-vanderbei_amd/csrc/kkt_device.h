@@ -31,6 +31,7 @@ struct TailView {
     const TailTask* tasks;
     double* W;        // nt x 64 workspace: L21 * D of the current block column
     int vk = kTailVisitBlocks;   // blocks per deferred trailing update (visit) of a tile
+    int dep = 1;      // dependent pivots inside the look-ahead panel (kkt_dense.hip panel_w_body; 0: bail to the host)
 };
 
 // Device-time phases of the KKT core (timing mode), with the algorithmic
@@ -247,6 +248,8 @@ class KktDevice {
     DevBuf<unsigned long long> dChainGran_;   // dense-tail sweep chains: z of every block as epoch-tagged granules
     int chain_epoch_ = 0;      // the chains' launch epoch (one per launch, never reused)
     int visit_blocks_ = kTailVisitBlocks;   // TailView::vk (IPO_HIP_VISIT_BLOCKS)
+    double epsdiag_cap_ = 0.0;     // IPO_HIP_EPSDIAG_MAX (diagnostics; 0: the reference's unbounded growth)
+    int tail_spec_ = 1;            // TailView::dep when the host repair backs it (IPO_HIP_TAIL_SPEC: 0 off, 2 tests)
     bool chain_pairs_ = false; // dense-tail chains with two blocks per workgroup (k_tail_fwd_pair / _bwd_pair)
     bool chain_lead_ = false;  // forward dense-tail sweep by one lead workgroup + helpers (k_tail_fwd_lead)
     DevBuf<int> dtail_task_ptr_, dtail_kslot_, dtail_kslot_ptr_;

@@ -86,7 +86,7 @@ k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __rest
                 double* __restrict__ Lx, int* __restrict__ live, double* __restrict__ dscale, int tail_from,
                 int* __restrict__ flags, const double* __restrict__ qdiag, double qmax) {
     const int v = blockIdx.x * NT + threadIdx.x;
-    if (v < 3) flags[v] = 0;      // the factorisation's flags (no fill launch of their own)
+    if (v < 4) flags[v] = 0;      // the factorisation's flags (no fill launch of their own)
     if (v >= T) return;
     const int old = perm[v];
     // columns >= tail_from: replicated linking rows of a non-leading shard,
@@ -3385,6 +3385,8 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         }
     }
     if (const char* vb = std::getenv("IPO_HIP_VISIT_BLOCKS")) visit_blocks_ = std::max(1, std::atoi(vb));
+    if (const char* ts = std::getenv("IPO_HIP_TAIL_SPEC")) tail_spec_ = std::atoi(ts);
+    if (const char* em = std::getenv("IPO_HIP_EPSDIAG_MAX")) epsdiag_cap_ = std::atof(em);
 
     mark("dLx_.alloc(plan_.lx_size > 0");
     dLx_.alloc(plan_.lx_size > 0 ? plan_.lx_size : 1);
@@ -3637,6 +3639,10 @@ TailView KktDevice::tail_view() const {
     t.tasks = reinterpret_cast<const TailTask*>(dtail_tasks_.get());
     t.W = dW_.get();
     t.vk = visit_blocks_;
+    // dependent pivots in the look-ahead panel: its failed checks fall back on
+    // the host repair, which the sharded solve does not use
+    const char* rp = std::getenv("IPO_HIP_TAIL_REPAIR");
+    t.dep = use_panel_ && !xch_ && (!rp || std::atoi(rp) != 0) ? tail_spec_ : 0;
     return t;
 }
 
@@ -3694,9 +3700,11 @@ void KktDevice::factor_core(const double* dE, const double* dD) {
     if (!factor_pass(dE, dD, use_panel_, use_panel_)) {
         tm_.panel_redos++;
         for (int b = 0; b < 4; b++) tm_.redo_where[b] += (hFlags_[1] >> b) & 1;
-        const bool tail_only = hFlags_[1] == 4 && hFlags_[4] > 0;
+        // bit 16: a dependent-pivot pass of the tail failed its check (restore first)
+        const bool tail_only = (hFlags_[1] & ~16) == 4 && hFlags_[4] > 0;
         if (repair && tail_only) repair_tail();
-        else if (!factor_pass(dE, dD, false, repair) && repair && hFlags_[1] == 4 && hFlags_[4] > 0) repair_tail();
+        else if (!factor_pass(dE, dD, false, repair) && repair && (hFlags_[1] & ~16) == 4 && hFlags_[4] > 0)
+            repair_tail();
     }
     tm_.factors++;
     // one occurrence per factorisation, whatever redos and repairs it took
@@ -3705,6 +3713,9 @@ void KktDevice::factor_core(const double* dE, const double* dD) {
         for (int ph : {kPhGather, kPhDiag, kPhTrsm, kPhSyrk, kPhTail}) tm_.phase_count[ph]++;
     ndep_ = xch_ ? static_cast<int>(hScal_[1]) : hFlags_[0];
     if (-hScal_[0] < 1.0e-14) epsdiag_ *= 10;
+    // developer diagnostics (IPO_HIP_EPSDIAG_MAX, tools/status_loss_probe.py):
+    // a cap on the growth above, to measure what a stalled solve owes to it
+    if (epsdiag_cap_ > 0.0 && epsdiag_ > epsdiag_cap_) epsdiag_ = epsdiag_cap_;
 }
 
 // One numeric factorisation, the sparse levels by the fused kernels (fused)
@@ -3856,6 +3867,7 @@ void KktDevice::repair_tail() {
         if (timing_) IPO_HIP_CHECK(hipEventRecord(ev0_, s));
         IPO_HIP_CHECK(hipMemsetAsync(dFlags_.get() + 1, 0, 2 * sizeof(int), s));
         TailView tv = tail_view();
+        if (hFlags_[1] & 16) launch_tail_restore(pv, tv, tb, s);   // other workgroups of the DEP pass wrote
         ph_begin(s);
         if (tb > 0) launch_tail_colupdate(pv, tv, tb - 1, s);
         ph_end(kPhTail, tb > 0, s);
@@ -3882,7 +3894,7 @@ void KktDevice::repair_tail() {
         for (int t = tb + 1; t < plan_.ntb; t++) launch_tail_step(pv, tail_view(), t, s);
         ph_end(kPhTail, plan_.ntb - tb - 1, s);
         if (finish_pass(true)) break;
-        if (hFlags_[1] != 4 || hFlags_[4] - 1 <= tb)   // cannot happen: a later tail column or nothing
+        if ((hFlags_[1] & ~16) != 4 || hFlags_[4] - 1 <= tb)   // cannot happen: a later tail column or nothing
             throw std::runtime_error("kkt: dense-tail repair did not advance");
     }
 }

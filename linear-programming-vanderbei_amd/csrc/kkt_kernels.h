@@ -79,6 +79,8 @@ void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, int r
 size_t tail_dep_state_doubles(int ntb);
 // Block t's update of block column t + 1 alone.
 void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, hipStream_t s);
+// Block column kb as it was before a failed dependent-pivot pass (k_tail_restore).
+void launch_tail_restore(const PlanView& pv, const TailView& tv, int kb, hipStream_t s);
 // Fused panel of supernodes sups[q0 .. q0+count) that have at most 16
 // columns and 64 rows (one wave each, k_panel_s); same bail-out contract.
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s);

@@ -122,6 +122,7 @@ void orc_kkt_diag(const orc_kkt *k, double *d);     /* [N]   numeric D after fac
 double orc_kkt_epsdiag(const orc_kkt *k);
 void   orc_kkt_set_epsdiag(orc_kkt *k, double e);   /* tests: start from a captured state */
 int  orc_kkt_ndep(const orc_kkt *k);
+double orc_kkt_last_resid(const orc_kkt *k);  /* last refined solve's max residual / (max|rhs| + 1) */
 void orc_kkt_live(const orc_kkt *k, int *live);      /* [N] "mark" (new order) after factor */
 /* stability probe: lltnum's contributions summed in the reference's order
  * (0), reversed (1) or by increasing source column (2); ORC_PERTURB env */

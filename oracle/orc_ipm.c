@@ -100,6 +100,7 @@ int orc_hsd(int m, int n, int nz, const int *iA, const int *kA, const double *A,
 "- - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - - \n");
         fflush(tr);
     }
+    const int dbg_step = getenv("ORC_DEBUG_STEP") != NULL;
     for (iter = 0; iter < maxit; iter++) {
         mu = (orc_dot(z, x, n) + orc_dot(w, y, m) + phi * psi) / (n + m + 1);
         delta = (iter % 2 == 0) ? 0.0 : 1.0;
@@ -144,6 +145,8 @@ int orc_hsd(int m, int n, int nz, const int *iA, const int *kA, const double *A,
         for (int j = 0; j < n; j++) fx[j] = -sig[j];
         for (int i = 0; i < m; i++) fy[i] = rho[i];
         orc_kkt_solve(K, E, D, fy, fx);
+        int dbg_p1 = orc_kkt_last_passes(K);
+        double dbg_r1 = orc_kkt_last_resid(K);
         for (int j = 0; j < n; j++) gx[j] = -c[j];
         for (int i = 0; i < m; i++) gy[i] = -b[i];
         orc_kkt_solve(K, E, D, gy, gx);
@@ -167,6 +170,25 @@ int orc_hsd(int m, int n, int nz, const int *iA, const int *kA, const double *A,
         }
         if (theta < -dphi / phi) theta = -dphi / phi;
         if (theta < -dpsi / psi) theta = -dpsi / psi;
+        if (dbg_step) {   /* diagnostics (ORC_DEBUG_STEP): the step and the KKT solves behind it */
+            int bk = -1, bi = -1;
+            double bt = 0.0;
+            for (int j = 0; j < n; j++) {
+                if (-dx[j] / x[j] > bt) { bt = -dx[j] / x[j]; bk = 0; bi = j; }
+                if (-dz[j] / z[j] > bt) { bt = -dz[j] / z[j]; bk = 1; bi = j; }
+            }
+            for (int i = 0; i < m; i++) {
+                if (-dy[i] / y[i] > bt) { bt = -dy[i] / y[i]; bk = 2; bi = i; }
+                if (-dw[i] / w[i] > bt) { bt = -dw[i] / w[i]; bk = 3; bi = i; }
+            }
+            if (-dphi / phi > bt) { bt = -dphi / phi; bk = 4; bi = 0; }
+            if (-dpsi / psi > bt) { bt = -dpsi / psi; bk = 5; bi = 0; }
+            static const char *kn[] = {"x", "z", "y", "w", "phi", "psi"};
+            fprintf(stderr, "step %3d: theta %.3e by %s[%d] ndep %d epsdiag %.0e passes %d/%d resid %.1e/%.1e "
+                            "phi %.3e psi %.3e dphi %.3e\n", iter, 0.95 / theta > 1.0 ? 1.0 : 0.95 / theta,
+                    bk >= 0 ? kn[bk] : "-", bi, orc_kkt_ndep(K), orc_kkt_epsdiag(K), dbg_p1,
+                    orc_kkt_last_passes(K), dbg_r1, orc_kkt_last_resid(K), phi, psi, dphi);
+        }
         theta = (0.95 / theta > 1.0) ? 1.0 : 0.95 / theta;   /* MIN(0.95/theta, 1.0) */
 
         for (int j = 0; j < n; j++) { x[j] = x[j] + theta * dx[j]; z[j] = z[j] + theta * dz[j]; }

@@ -61,6 +61,7 @@ struct orc_kkt {
     double *acc; int *first, *link, *pos;
     double *zr, *dy, *dx, *ry, *rx, *qy;
     int passes;
+    double rs, bc;               /* last refined solve: final residual, its bound scale (diagnostics) */
 };
 
 static inline double dmax(double a, double b) { return a > b ? a : b; }   /* macros.h MAX */
@@ -321,6 +322,8 @@ void orc_kkt_destroy(orc_kkt *K)
 }
 
 /* left-looking LDL^T (lltnum, ldlt.c:517-636) */
+static int g_depblk = -2;   /* ORC_DEBUG_DEPBLK (diagnostics) */
+
 static void numeric_ldlt(orc_kkt *K)
 {
     int T = K->T, m = K->m;
@@ -343,6 +346,10 @@ static void numeric_ldlt(orc_kkt *K)
         g_perturb = !e ? 0 : !strcmp(e, "reverse") ? 1 : !strcmp(e, "sorted") ? 2 : 0;
     }
     const int perturb = g_perturb;
+    if (g_depblk == -2) {
+        const char *e = getenv("ORC_DEBUG_DEPBLK");   /* first column of the GPU's dense tail */
+        g_depblk = e ? atoi(e) : -1;
+    }
     int *js = perturb ? malloc(sizeof(int) * (size_t)(T ? T : 1)) : NULL;
     int *ks = perturb ? malloc(sizeof(int) * (size_t)(T ? T : 1)) : NULL;
 
@@ -398,6 +405,13 @@ static void numeric_ldlt(orc_kkt *K)
             K->ndep++;
             double off = 0.0;
             for (int kk = kb; kk < ke; kk++) off = dmax(off, dabs(Lx[kk]));
+            if (g_depblk >= 0 && col >= g_depblk) {   /* diagnostics: the off-diagonal max inside col's 64-block */
+                double ob = 0.0;
+                for (int kk = kb; kk < ke; kk++)
+                    if ((Li[kk] - g_depblk) / 64 == (col - g_depblk) / 64) ob = dmax(ob, dabs(Lx[kk]));
+                fprintf(stderr, "dep col %d block %d: off_block %.3e off_all %.3e -> %s\n", col, (col - g_depblk) / 64,
+                        ob, off, off < 1.0e+6 * EPS_PIVOT ? "drop" : "keep");
+            }
             if (off < 1.0e+6 * EPS_PIVOT) live[col] = 0;
             else piv = sgn * EPS_PIVOT;
         }
@@ -475,6 +489,11 @@ void orc_kkt_factor(orc_kkt *K, const double *E, const double *D)
     double mind = HUGE_VAL;
     for (int v = 0; v < T; v++) if (dabs(d[v]) < mind) mind = dabs(d[v]);
     if (mind < 1.0e-14) K->epsdiag *= 10;
+    {   /* diagnostics (ORC_EPSDIAG_MAX): cap the growth, to test what a stall owes to it */
+        static double cap = -1.0;
+        if (cap < 0) cap = getenv("ORC_EPSDIAG_MAX") ? atof(getenv("ORC_EPSDIAG_MAX")) : 0.0;
+        if (cap > 0 && K->epsdiag > cap) K->epsdiag = cap;
+    }
     if (getenv("ORC_DEBUG_NDEP")) {
         int dropped = 0;
         for (int v = 0; v < T; v++) dropped += !K->live[v];
@@ -560,6 +579,8 @@ int orc_kkt_solve(orc_kkt *K, const double *E, const double *D, double *fy, doub
     for (int j = 0; j < m; j++) fy[j] = dy[j];
     for (int i = 0; i < n; i++) fx[i] = dx[i];
     K->passes = pass;
+    K->rs = rs;
+    K->bc = bc;
     return ok;
 }
 
@@ -578,3 +599,4 @@ void orc_kkt_set_epsdiag(orc_kkt *K, double e) { K->epsdiag = e; }
 int  orc_kkt_ndep(const orc_kkt *K) { return K->ndep; }
 void orc_kkt_live(const orc_kkt *K, int *p) { memcpy(p, K->live, sizeof(int) * (size_t)K->T); }
 int  orc_kkt_last_passes(const orc_kkt *K) { return K->passes; }
+double orc_kkt_last_resid(const orc_kkt *K) { return K->rs / K->bc; }

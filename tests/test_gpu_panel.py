@@ -135,3 +135,54 @@ def test_tail_chain_lead_bitwise(name):
     last blocks: the extra step after the two-step loop), 12 (greenbea 732,
     partial) and 3 (brandy 155: no helper workgroups)."""
     assert _solve_env("IPO_HIP_CHAIN_LEAD", "0", name) == _solve_env("IPO_HIP_CHAIN_LEAD", "1", name)
+
+
+def test_tail_dependent_pivots_in_panel_bitwise():
+    """Dependent pivots of the look-ahead dense tail resolved inside the panel
+    launch (IPO_HIP_TAIL_SPEC=1, default: a second panel pass applies the rule
+    of ldlt.c:600-614 in the chain, dropped columns checked tile by tile,
+    kkt_dense.hip panel_w_body) against the host repair of every such block
+    column (IPO_HIP_TAIL_SPEC=0) and against the pass whose every drop is
+    taken as contradicted, so that the other workgroups' writes are put back
+    (k_tail_restore) before the host repair (IPO_HIP_TAIL_SPEC=2): the same
+    operations on every entry, so identical dfl001 HSD solves (trace and final
+    values); the in-panel path leaves fewer block columns to the host."""
+    runs = {}
+    for v in ("0", "1", "2"):
+        status, text, st = _with_env("IPO_HIP_TAIL_SPEC", v, lambda: ipo_amd.run_mps(mps_path("dfl001"), "hsd"))
+        runs[v] = (status, text, {k: st[k] for k in sorted(st) if k.startswith("final") or k == "iters"},
+                   st["tail_repairs"])
+    assert runs["0"][:3] == runs["1"][:3] == runs["2"][:3]
+    print("tail repairs by the host: spec 0 %d, 1 %d, 2 %d" % (runs["0"][3], runs["1"][3], runs["2"][3]))
+    assert runs["0"][3] > 0, "dfl001's HSD solve no longer meets a dependent pivot in the dense tail"
+    assert runs["1"][3] < runs["0"][3]
+    assert runs["2"][3] >= runs["1"][3]
+
+
+@pytest.mark.parametrize("state", ["dfl001_100", "dfl001_110", "dfl001_114"])
+def test_tail_dependent_pivots_states_bitwise(state):
+    """The same three paths on captured late-iteration dfl001 systems
+    (tests/golden/kkt_states; many dependent pivots): pivots, live marks and
+    the refined solution bit for bit."""
+    import os as _os
+    st = np.load(_os.path.join(_os.path.dirname(__file__), "golden", "kkt_states", state + ".npz"))
+    E, D, eps = st["E"], st["D"], float(st["epsdiag"])
+    p = ipo_amd.load_mps(mps_path("dfl001"))
+    rng = np.random.default_rng(5)
+    fy, fx = rng.uniform(-1, 1, p.m), rng.uniform(-1, 1, p.n)
+
+    def run():
+        k = ipo_amd.KktFactor(p.m, p.n, p.kA, p.iA, p.A)
+        try:
+            k.set_epsdiag(eps)
+            k.factor(E, D)
+            d, live = k.pivots()
+            gy, gx, ok = k.solve(E, D, fy, fx)
+            return d.copy(), live.copy(), gy, gx, ok, k.info()["ndep"]
+        finally:
+            k.close()
+    outs = [_with_env("IPO_HIP_TAIL_SPEC", v, run) for v in ("0", "1", "2")]
+    for o in outs[1:]:
+        assert o[4] == outs[0][4] and o[5] == outs[0][5]
+        for a, b in zip(o[:4], outs[0][:4]):
+            assert np.array_equal(a, b)

@@ -7,3 +7,4 @@ bash tools/gpu_step.sh 60 ub_tail_st35.log tools/ubench_tail_st 4441 3 35 || exi
 bash tools/gpu_step.sh 60 ub_tail_st66.log tools/ubench_tail_st 4441 3 66 || exit 1
 bash tools/gpu_step.sh 600 gputests.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit 1
 bash tools/gpu_step.sh 400 bench.log python3 bench.py || exit 1
+bash tools/gpu_step.sh 500 status_loss.log python3 tools/status_loss_probe.py gpurun_out/status_loss.json || exit 1
