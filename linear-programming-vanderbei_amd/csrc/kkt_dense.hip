@@ -633,6 +633,7 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
             // the LDS runs one wave's operations in issue order
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __hip_atomic_store(prog, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (i == WIN - 1) PANEL_STAMP(5);
             dsc = dsc + fabs(l * c);
             double cc[WIN];
             if (i + 2 < WIN) win_row(&Ct[k][cw0], cc);
@@ -664,6 +665,27 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
 template <bool DSC>
 __device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw, int lane, int cw0,
                                           double (*Ct)[CTS], double (*L)[PC], const int* prog) {
+#ifdef IPO_EXP_APPLY_EAGER
+    // experiment: each column applied as soon as it is published
+    {
+        int seen = 0;
+#pragma unroll 2
+        for (int i = 0; i < WIN; i++) {
+            const int k = kw + i;
+            df_wait(prog, i + 1, seen);
+            if (i + 1 == WIN) PANEL_STAMP(6);
+            const double l = L[k][lane];
+            const double ck = DSC ? Ct[k][lane] : 0.0;
+            double cc[WIN];
+            win_row(&Ct[k][cw0], cc);
+#pragma unroll
+            for (int q = 0; q < WIN; q++) a[q] = a[q] - l * cc[q];
+            if (DSC) dsc = dsc + fabs(l * ck);
+        }
+        PANEL_STAMP(7);
+        return;
+    }
+#endif
     // software-pipelined: step i + 1's LDS operands are read before step i's
     // arithmetic, so the read latency hides under the updates
     int seen = 0;
@@ -678,6 +700,7 @@ __device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw,
         double ln = 0.0, ckn = 0.0, cn[WIN];
         if (i + 1 < WIN) {
             df_wait(prog, i + 2, seen);
+            if (i + 2 == WIN) PANEL_STAMP(6);
             ln = L[k + 1][lane];
             if (DSC) ckn = Ct[k + 1][lane];
             win_row(&Ct[k + 1][cw0], cn);
@@ -690,6 +713,7 @@ __device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw,
 #pragma unroll
         for (int q = 0; q < WIN; q++) cc[q] = cn[q];
     }
+    PANEL_STAMP(7);
 }
 
 // Window solve of the tile rows (half 1, wave w): solve_rows' form, step i
@@ -832,7 +856,7 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
     double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
     double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
     if (!pre && bailed && bailed - 1 < bt) return false;
-    if (DEP) {
+    if (DEP && !fu_sup) {
         // what this pass may overwrite, saved for k_tail_restore: the tile
         // rows (rows >= 64 of the block column, as in S) and workgroup 0's
         // |terms| of the block's pivots (rows 0..nc-1 of W's column 0)
@@ -979,16 +1003,13 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
         // dense-tail panel that bails is resumed from its block column
         // (KktDevice::repair_tail), so its rows of S wait for the check
         // below (W is rewritten by the repair).
-        if (h1 ? rok : (j == 0 && lane >= nc && lane < h0)) {
+        if (wbuf && (h1 ? rok : (j == 0 && lane >= nc && lane < h0))) {
             double dw[WIN];
             win_row(&dv[cw0], dw);        // one LDS round trip, not one per column
 #pragma unroll
             for (int q = 0; q < WIN; q++) {
                 const int c = cw0 + q;
-                if (c < nc) {
-                    if (fu_sup) panel[row + (size_t)c * ld] = a[q];
-                    if (wbuf) wbuf[row + (size_t)c * ld] = a[q] * dw[q];
-                }
+                if (c < nc) wbuf[row + (size_t)c * ld] = a[q] * dw[q];
             }
         }
     }
@@ -1009,20 +1030,21 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
         if (tid == 0) {
             atomicOr(&p.flags[1], fu_sup ? 2 : DEP ? 4 | 16 : 4);   // bit: where it bailed (16: restore first)
             if (!fu_sup) atomicMax(&p.flags[2], kb + 1);   // the dense-tail block column
-            if (DEP && j == 0) p.flags[3] = 0;            // workgroup 0 added no dependent pivots
+            if (DEP && !fu_sup && j == 0) p.flags[3] = 0;   // workgroup 0 added no dependent pivots
         }
         return false;
     }
-    if (!fu_sup) {
-        if (w < nwin && (h1 ? rok && tile : (j == 0 && lane >= nc && lane < h0))) {
+    // the rows of L21 (half 1) and of R_s inside the first 64 rows (half 0 of
+    // workgroup 0), once the panel holds: a first pass that meets a dependent
+    // pivot ends unwritten, so its DEP pass starts from the same input
+    if (w < nwin && (h1 ? rok && tile : (j == 0 && lane >= nc && lane < h0))) {
 #pragma unroll
-            for (int q = 0; q < WIN; q++) {
-                const int c = cw0 + q;
-                if (c < nc) panel[row + (size_t)c * ld] = a[q];
-            }
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            if (c < nc) panel[row + (size_t)c * ld] = a[q];
         }
-        if (pre && j == 0 && !h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc_pre;
     }
+    if (!fu_sup && pre && j == 0 && !h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc_pre;
     if (j != 0) return false;
     // workgroup 0: L11' into the upper slot through an LDS transpose (Ct is
     // free again), D, mark
@@ -1036,7 +1058,7 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
     if (tid < nc) { p.dg[c0 + tid] = dv[tid]; p.live[c0 + tid] = DEP ? S.lv[tid] : 1; }
     if (DEP && tid == 0) {
         if (S.ndep) atomicAdd(&p.flags[0], S.ndep);
-        p.flags[3] = S.ndep;                       // taken back by k_tail_restore if a later check fails
+        if (!fu_sup) p.flags[3] = S.ndep;          // taken back by k_tail_restore if a later check fails
     }
     PANEL_STAMP(13);
     return false;
@@ -1045,7 +1067,14 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
 __global__ void __launch_bounds__(PNT)
 k_panel_w(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j, int f0, TailView tv, int kb) {
     __shared__ __attribute__((aligned(16))) char lds[sizeof(PanelLds)];
-    panel_w_body(p, fu_sup, fu_j, f0, tv, kb, blockIdx.x, *reinterpret_cast<PanelLds*>(lds), tv.W);
+    PanelLds& S = *reinterpret_cast<PanelLds*>(lds);
+    // sparse panels: a dependent pivot is resolved by a second, DEP pass
+    // (panel_w_body); a failed check there bails to the redo from the assembly
+    const int dep = fu_sup ? (tv.sdep ? 1 : 0) : 0;
+    if (panel_w_body<false>(p, fu_sup, fu_j, f0, tv, kb, blockIdx.x, S, tv.W, false, nullptr, 0, dep)) {
+        __syncthreads();
+        panel_w_body<true>(p, fu_sup, fu_j, f0, tv, kb, blockIdx.x, S, tv.W, false, nullptr, 0, dep);
+    }
 }
 
 // ------------------------------------------- dense tail: look-ahead steps
@@ -1312,7 +1341,7 @@ __host__ __device__ __forceinline__ int visit_hi(int t, int c, int K) { return c
 // the panel workgroups apply block t - 1's to their own rows first
 // (panel_w_body's pre-update, k_tail_syrk's fragments and order).
 __global__ void __launch_bounds__(PNT)
-k_tail_pr(PlanView p, TailView tv, int t, int gp) {
+k_tail_pr(PlanView p, TailView tv, int t, int gp, int vbase) {
     __shared__ __attribute__((aligned(16))) char lds[kTailStepLds];
     // a panel of an earlier step bailed (flags[2] = 1 + its block column;
     // not this launch's own, whose visits must complete): the host
@@ -1323,6 +1352,12 @@ k_tail_pr(PlanView p, TailView tv, int t, int gp) {
             __syncthreads();           // every wave has read the first pass's verdict
             panel_w_body<true>(p, nullptr, nullptr, 0, tv, t, blockIdx.x, S, nullptr, t > 0, p.flags + 2, t, tv.dep);
         }
+        return;
+    }
+    if (tv.vlist) {
+        const unsigned v = tv.vlist[vbase + blockIdx.x - gp];
+        visit_tile512(p, tv, v & 255, (v >> 8) & 255, (v >> 16) & 255, v >> 24, *reinterpret_cast<SyrkLds*>(lds),
+                      p.flags + 2, t);
         return;
     }
     int tile = blockIdx.x - gp, c = t + 1;
@@ -1371,7 +1406,7 @@ k_tail_col(PlanView p, TailView tv, int t) {
 constexpr int SNC = 16;
 
 __global__ void __launch_bounds__(256)
-k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count) {
+k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count, int dep) {
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + wv;
     if (q >= count) return;
@@ -1389,17 +1424,32 @@ k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count) {
     }
     double dsc = lane < nc ? p.dscale[c0 + lane] : 0.0;
     double mydv = 0.0;
+    int mylive = 1, ndep = 0;
 #pragma unroll
     for (int k = 0; k < SNC; k++) {
         if (k < nc) {
-            const double dk = lane_bcast(a[k], k);
+            double dk = lane_bcast(a[k], k);
             const double dsk = lane_bcast(dsc, k);
+            int alive = 1;
             if (fabs(dk) <= p.tau * dsk) {          // wave-uniform
-                if (lane == 0) atomicOr(&p.flags[1], 8);
-                return;
+                // ldlt.c:600-614: every row of the column is in this wave
+                // (the supernode's rows and R_s), so the largest entry below
+                // the pivot decides here: +-1e-8 by node class if it reaches
+                // 1e-2, else the column is dropped; a NaN (whose place in the
+                // reference's max fold matters) goes to the redo
+                const bool in = lane > k && rok;
+                const bool nan = __ballot(in && a[k] != a[k]) != 0;
+                if (!dep || nan) {
+                    if (lane == 0) atomicOr(&p.flags[1], 8);
+                    return;
+                }
+                if (__ballot(in && !(fabs(a[k]) < 1.0e+6 * 1.0e-8)) != 0) dk = (p.sign[c0 + k] < 0 ? -1.0 : 1.0) * 1.0e-8;
+                else alive = 0;
+                ndep++;
             }
+            mylive = lane == k ? alive : mylive;
             const bool below = lane > k && rok;
-            const double l = below ? a[k] / dk : 0.0;
+            const double l = alive && below ? a[k] / dk : 0.0;     // a dropped column's L is 0
             a[k] = below ? l : a[k];
             mydv = lane == k ? dk : mydv;
             const double c = l * dk;
@@ -1417,7 +1467,8 @@ k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count) {
             else if (c < lane && lane < nc) panel[c + (size_t)lane * ld] = a[c];
         }
     }
-    if (lane < nc) { p.dg[c0 + lane] = mydv; p.live[c0 + lane] = 1; }
+    if (lane < nc) { p.dg[c0 + lane] = mydv; p.live[c0 + lane] = mylive; }
+    if (ndep && lane == 0) atomicAdd(&p.flags[0], ndep);
 }
 
 }  // namespace
@@ -1426,6 +1477,62 @@ int tail_visit_tiles(int ntb, int t, int K) {
     int n = 0;
     for (int c = t + 1; c < ntb && visit_hi(t, c, K) > 0; c++) n += ntb - c;
     return t > 0 ? n : 0;
+}
+
+// Launch t runs panel t on gp(t) workgroups beside its visits; with one
+// workgroup per CU (the kernel's LDS) a launch of more than `cap` workgroups
+// takes two rounds of visits: on dfl001 launches 21-37 under visit_hi's
+// chunks (up to 286 workgroups, 37-47 us against ~30).  Those launches carry
+// the first chunks of later columns' tiles (blocks 0 .. b1 - 1 with b1 <= 6),
+// which are ready from launch b1 on: moved, latest-first, into the latest
+// earlier launch with room.  Every tile keeps its chunks and their order (its
+// first chunk only comes earlier), so the factor is bitwise the same.
+std::vector<unsigned> tail_visit_schedule(int ntb, int nt, int K, int cap, std::vector<int>& ptr) {
+    struct V { int bi, c, b0, b1; };
+    std::vector<std::vector<V>> L(ntb);
+    std::vector<int> tot(ntb, 0);
+    for (int t = 0; t < ntb; t++) {
+        const int h = nt - t * PC;
+        tot[t] = std::max(1, (h + TR - 1) / TR - 1);          // launch_tail_step's panel workgroups
+        if (t == 0) continue;
+        for (int c = t + 1; c < ntb && visit_hi(t, c, K) > 0; c++) {
+            const int b1 = visit_hi(t, c, K), b0 = std::max(0, b1 - K);
+            for (int bi = c; bi < ntb; bi++) L[t].push_back({bi, c, b0, b1});
+        }
+        tot[t] += static_cast<int>(L[t].size());
+    }
+    for (int t = ntb - 1; t > 1; t--) {
+        while (tot[t] > cap) {
+            // a first chunk of this launch, the one ready earliest (then the
+            // farthest column: its tiles have the longest wait before their
+            // panel anyway)
+            int best = -1;
+            for (int q = 0; q < static_cast<int>(L[t].size()); q++) {
+                const V& v = L[t][q];
+                if (v.b0 != 0) continue;
+                if (best < 0 || v.b1 < L[t][best].b1 || (v.b1 == L[t][best].b1 && v.c > L[t][best].c)) best = q;
+            }
+            if (best < 0) break;
+            int dst = -1;
+            for (int u = t - 1; u >= std::max(1, L[t][best].b1); u--)
+                if (tot[u] < cap) { dst = u; break; }
+            if (dst < 0) break;
+            L[dst].push_back(L[t][best]);
+            tot[dst]++;
+            L[t].erase(L[t].begin() + best);
+            tot[t]--;
+        }
+    }
+    std::vector<unsigned> out;
+    ptr.assign(ntb + 1, 0);
+    for (int t = 0; t < ntb; t++) {
+        ptr[t] = static_cast<int>(out.size());
+        for (const V& v : L[t])
+            out.push_back(static_cast<unsigned>(v.bi) | static_cast<unsigned>(v.c) << 8 |
+                          static_cast<unsigned>(v.b0) << 16 | static_cast<unsigned>(v.b1) << 24);
+    }
+    ptr[ntb] = static_cast<int>(out.size());
+    return out;
 }
 
 void tail_visit_work(int ntb, int nt, int K, double& flops, double& bytes) {
@@ -1448,8 +1555,8 @@ void tail_visit_work(int ntb, int nt, int K, double& flops, double& bytes) {
 void launch_tail_step(const PlanView& pv, const TailView& tv, int t, hipStream_t s) {
     const int h = tv.nt - t * PC;
     const int gp = std::max(1, (h + TR - 1) / TR - 1);
-    const int nr = tail_visit_tiles(tv.ntb, t, tv.vk);
-    hipLaunchKernelGGL(k_tail_pr, dim3(gp + nr), dim3(PNT), 0, s, pv, tv, t, gp);
+    const int nr = tv.vlist ? tv.vptr[t + 1] - tv.vptr[t] : tail_visit_tiles(tv.ntb, t, tv.vk);
+    hipLaunchKernelGGL(k_tail_pr, dim3(gp + nr), dim3(PNT), 0, s, pv, tv, t, gp, tv.vlist ? tv.vptr[t] : 0);
 }
 
 void launch_tail_restore(const PlanView& pv, const TailView& tv, int kb, hipStream_t s) {
@@ -1477,8 +1584,8 @@ void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, int r
                        st + out * half, sti + 4 * in, sti + 4 * out);
 }
 
-void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s) {
-    if (count > 0) hipLaunchKernelGGL(k_panel_s, dim3((count + 3) / 4), dim3(256), 0, s, pv, sups, q0, count);
+void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, int dep, hipStream_t s) {
+    if (count > 0) hipLaunchKernelGGL(k_panel_s, dim3((count + 3) / 4), dim3(256), 0, s, pv, sups, q0, count, dep);
 }
 
 void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,

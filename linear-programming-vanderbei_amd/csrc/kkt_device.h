@@ -32,6 +32,12 @@ struct TailView {
     double* W;        // nt x 64 workspace: L21 * D of the current block column
     int vk = kTailVisitBlocks;   // blocks per deferred trailing update (visit) of a tile
     int dep = 1;      // dependent pivots inside the look-ahead panel (kkt_dense.hip panel_w_body; 0: bail to the host)
+    // visit schedule (tail_visit_schedule): launch t's visits are vlist[vptr[t] ..
+    // vptr[t + 1]), each (bi | c << 8 | b0 << 16 | b1 << 24); vlist on the
+    // device, vptr on the host; null: the visit_hi formula alone
+    const unsigned* vlist = nullptr;
+    const int* vptr = nullptr;
+    int sdep = 1;     // dependent pivots inside the sparse fused panels (k_panel_w, k_panel_s; 0: redo the factor)
 };
 
 // Device-time phases of the KKT core (timing mode), with the algorithmic
@@ -249,10 +255,13 @@ class KktDevice {
     int chain_epoch_ = 0;      // the chains' launch epoch (one per launch, never reused)
     int visit_blocks_ = kTailVisitBlocks;   // TailView::vk (IPO_HIP_VISIT_BLOCKS)
     double epsdiag_cap_ = 0.0;     // IPO_HIP_EPSDIAG_MAX (diagnostics; 0: the reference's unbounded growth)
-    int tail_spec_ = 1;            // TailView::dep when the host repair backs it (IPO_HIP_TAIL_SPEC: 0 off, 2 tests)
+    int tail_spec_ = 1;
+    int sparse_dep_ = 1;           // TailView::sdep (IPO_HIP_SPARSE_DEP)            // TailView::dep when the host repair backs it (IPO_HIP_TAIL_SPEC: 0 off, 2 tests)
     bool chain_pairs_ = false; // dense-tail chains with two blocks per workgroup (k_tail_fwd_pair / _bwd_pair)
     bool chain_lead_ = false;  // forward dense-tail sweep by one lead workgroup + helpers (k_tail_fwd_lead)
     DevBuf<int> dtail_task_ptr_, dtail_kslot_, dtail_kslot_ptr_;
+    DevBuf<unsigned> dvisit_list_;     // TailView::vlist (tail_visit_schedule; IPO_HIP_VISIT_SCHED=0: none)
+    std::vector<int> visit_ptr_;       // TailView::vptr
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;
     DevBuf<double> dDepSt_;        // k_tail_dep's block state and per-tile maxima

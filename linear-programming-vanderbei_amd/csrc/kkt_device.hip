@@ -3385,7 +3385,20 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         }
     }
     if (const char* vb = std::getenv("IPO_HIP_VISIT_BLOCKS")) visit_blocks_ = std::max(1, std::atoi(vb));
+    if (plan_.nt > 0 && plan_.ntb <= 255) {
+        // look-ahead launches of at most one workgroup per CU (tail_visit_schedule)
+        const char* vs = std::getenv("IPO_HIP_VISIT_SCHED");
+        if (!vs || std::atoi(vs) != 0) {
+            int dev = 0, cus = 0;
+            IPO_HIP_CHECK(hipGetDevice(&dev));
+            IPO_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            const std::vector<unsigned> vl = tail_visit_schedule(plan_.ntb, plan_.nt, visit_blocks_, cus, visit_ptr_);
+            dvisit_list_.upload(vl, s);
+            IPO_HIP_CHECK(hipStreamSynchronize(s));   // vl is a local
+        }
+    }
     if (const char* ts = std::getenv("IPO_HIP_TAIL_SPEC")) tail_spec_ = std::atoi(ts);
+    if (const char* sd = std::getenv("IPO_HIP_SPARSE_DEP")) sparse_dep_ = std::atoi(sd);
     if (const char* em = std::getenv("IPO_HIP_EPSDIAG_MAX")) epsdiag_cap_ = std::atof(em);
 
     mark("dLx_.alloc(plan_.lx_size > 0");
@@ -3639,10 +3652,17 @@ TailView KktDevice::tail_view() const {
     t.tasks = reinterpret_cast<const TailTask*>(dtail_tasks_.get());
     t.W = dW_.get();
     t.vk = visit_blocks_;
+    if (!visit_ptr_.empty()) {
+        t.vlist = dvisit_list_.get();
+        t.vptr = visit_ptr_.data();
+    }
     // dependent pivots in the look-ahead panel: its failed checks fall back on
     // the host repair, which the sharded solve does not use
     const char* rp = std::getenv("IPO_HIP_TAIL_REPAIR");
     t.dep = use_panel_ && !xch_ && (!rp || std::atoi(rp) != 0) ? tail_spec_ : 0;
+    // in the sparse panels a failed check falls back on redoing the factor
+    // from the assembly, on every shard alike (the bail flags are reduced)
+    t.sdep = sparse_dep_;
     return t;
 }
 
@@ -3749,7 +3769,7 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
         ph_begin(s);
         if (fused) {
             const int nsm = small_ptr_[l + 1] - small_ptr_[l], nfu = fu_ptr_[l + 1] - fu_ptr_[l];
-            launch_panel_small(pv, dsmall_sups_.get(), small_ptr_[l], nsm, s);
+            launch_panel_small(pv, dsmall_sups_.get(), small_ptr_[l], nsm, tv.sdep, s);
             launch_panel(pv, dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], nfu, tv, -1, s);
             ph_end(kPhDiag, (nsm > 0) + (nfu > 0), s);
         } else {

@@ -67,6 +67,11 @@ void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0
 void launch_tail_step(const PlanView& pv, const TailView& tv, int t, hipStream_t s);
 // visit tiles of launch t (tail of ntb block columns, chunks of K blocks)
 int tail_visit_tiles(int ntb, int t, int K);
+// The visits of every look-ahead launch placed so that no launch needs more
+// than `cap` workgroups (one round on `cap` CUs): visit_hi's chunks, with
+// tiles' first chunks moved into earlier launches where a launch would
+// overflow.  Returns the list (TailView::vlist layout) and ptr[0..ntb].
+std::vector<unsigned> tail_visit_schedule(int ntb, int nt, int K, int cap, std::vector<int>& ptr);
 // algorithmic flops / bytes of every visit of one factorisation
 void tail_visit_work(int ntb, int nt, int K, double& flops, double& bytes);
 // Repair path, block column kb of the dense tail with the dependent-pivot
@@ -83,6 +88,6 @@ void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, hipStr
 void launch_tail_restore(const PlanView& pv, const TailView& tv, int kb, hipStream_t s);
 // Fused panel of supernodes sups[q0 .. q0+count) that have at most 16
 // columns and 64 rows (one wave each, k_panel_s); same bail-out contract.
-void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, hipStream_t s);
+void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, int dep, hipStream_t s);
 
 }  // namespace ipo

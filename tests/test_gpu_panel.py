@@ -159,11 +159,17 @@ def test_tail_dependent_pivots_in_panel_bitwise():
     assert runs["2"][3] >= runs["1"][3]
 
 
+@pytest.mark.parametrize("var,vals", [("IPO_HIP_TAIL_SPEC", ("0", "1", "2")), ("IPO_HIP_SPARSE_DEP", ("0", "1"))])
 @pytest.mark.parametrize("state", ["dfl001_100", "dfl001_110", "dfl001_114"])
-def test_tail_dependent_pivots_states_bitwise(state):
+def test_tail_dependent_pivots_states_bitwise(state, var, vals):
     """The same three paths on captured late-iteration dfl001 systems
     (tests/golden/kkt_states; many dependent pivots): pivots, live marks and
-    the refined solution bit for bit."""
+    the refined solution bit for bit.  Likewise dependent pivots in the
+    sparse fused panels resolved in the kernels (IPO_HIP_SPARSE_DEP=1,
+    default: exact in k_panel_s, whose wave holds every row of the column; a
+    DEP pass in k_panel_w as in the tail, a failed check bailing) against
+    the redo of the whole factorisation with the per-phase kernels
+    (IPO_HIP_SPARSE_DEP=0)."""
     import os as _os
     st = np.load(_os.path.join(_os.path.dirname(__file__), "golden", "kkt_states", state + ".npz"))
     E, D, eps = st["E"], st["D"], float(st["epsdiag"])
@@ -181,8 +187,26 @@ def test_tail_dependent_pivots_states_bitwise(state):
             return d.copy(), live.copy(), gy, gx, ok, k.info()["ndep"]
         finally:
             k.close()
-    outs = [_with_env("IPO_HIP_TAIL_SPEC", v, run) for v in ("0", "1", "2")]
+    outs = [_with_env(var, v, run) for v in vals]
     for o in outs[1:]:
         assert o[4] == outs[0][4] and o[5] == outs[0][5]
         for a, b in zip(o[:4], outs[0][:4]):
             assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["dfl001", "greenbea"])
+def test_tail_visit_schedule_bitwise(name):
+    """The look-ahead launches with the capacity-aware visit schedule
+    (tail_visit_schedule, default: tiles' first chunks moved into earlier
+    launches so that no launch needs more workgroups than the device has
+    CUs) against visit_hi's placement alone (IPO_HIP_VISIT_SCHED=0): every
+    tile receives the same chunks in the same order, so the HSD solves are
+    identical (trace and final values)."""
+    assert _solve_env("IPO_HIP_VISIT_SCHED", "0", name) == _solve_env("IPO_HIP_VISIT_SCHED", "1", name)
+
+
+def test_sparse_dependent_pivots_bitwise():
+    """Whole dfl001 HSD solves with the sparse panels' dependent pivots
+    resolved in the kernels (IPO_HIP_SPARSE_DEP=1) and by redoing the
+    factorisation (0): identical traces and final values."""
+    assert _solve_env("IPO_HIP_SPARSE_DEP", "0") == _solve_env("IPO_HIP_SPARSE_DEP", "1")

@@ -45,6 +45,22 @@ int main(int argc, char** argv) {
     ipo::TailView tv{};
     tv.S = dS; tv.nt = nt; tv.ntb = ntb; tv.tc = 0; tv.W = dW;
     if (const char* vb = std::getenv("IPO_HIP_VISIT_BLOCKS")) tv.vk = std::atoi(vb);
+    // the library's visit schedule (IPO_HIP_VISIT_SCHED=0: the visit_hi formula alone)
+    std::vector<int> vptr;
+    unsigned* dvl = nullptr;
+    const char* vs = std::getenv("IPO_HIP_VISIT_SCHED");
+    if (!vs || std::atoi(vs) != 0) {
+        int cus = 0;
+        CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+        const std::vector<unsigned> vl = ipo::tail_visit_schedule(ntb, nt, tv.vk, cus, vptr);
+        CK(hipMalloc(&dvl, vl.size() * sizeof(unsigned) + 4));
+        CK(hipMemcpy(dvl, vl.data(), vl.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+        tv.vlist = dvl;
+        tv.vptr = vptr.data();
+        std::printf("visit schedule on %d CUs: workgroups per launch", cus);
+        for (int t = 0; t < ntb; t++) std::printf(" %d", std::max(1, (nt - t * 64 + 63) / 64 - 1) + vptr[t + 1] - vptr[t]);
+        std::printf("\n");
+    }
     std::vector<hipEvent_t> ev(ntb + 1);
     for (auto& e : ev) CK(hipEventCreate(&e));
     std::vector<double> step_us(ntb, 0.0);
@@ -106,12 +122,13 @@ int main(int argc, char** argv) {
     long long st[8][16];
     CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(ipo::g_stamps), sizeof(st)));
     std::printf("step %d, workgroup 0 stamps (cycles since wave 0 entry); slots: 15 entry, 3 pre-update operands in LDS, "
-                "4 products formed, 14 pre-update done, 0 loaded, 1 after updates, 2 window done, 12 end, 13 done\n",
+                "4 products formed, 14 pre-update done, 0 loaded, 6 last column of the previous window seen, 7 its update applied, "
+                "1 after updates, 5 own last column published, 2 window done, 12 end, 13 done\n",
                 stamp_step);
     const long long b = st[0][15];
     for (int w = 0; w < 8; w++) {
         std::printf("wave %d:", w);
-        for (int sl : {15, 3, 4, 14, 0, 1, 2, 12, 13}) std::printf(" %d:%lld", sl, st[w][sl] - b);
+        for (int sl : {15, 3, 4, 14, 0, 6, 7, 1, 5, 2, 12, 13}) std::printf(" %d:%lld", sl, st[w][sl] - b);
         std::printf("\n");
     }
 #endif
