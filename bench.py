@@ -54,7 +54,7 @@ METRIC = "IPM iterations/sec (ADA^T factor+solve) on netlib dfl001; duality gap 
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, AMD spec (the guide has no fp64 row)
 PHASE_KERNELS = {"gather": "k_update|k_update_flat|k_update_quad",
                  "diag": "k_panel_w|k_panel_s|k_diag", "trsm": "k_trsm",
-                 "tail_syrk": "k_tail_syrk", "tail": "k_tail_pr|k_tail_col|k_tail_dep",
+                 "tail_syrk": "k_tail_syrk", "tail": "k_tail_pr|k_tail_col|k_tail_dep|k_tail_restore",
                  "forward": "k_forward|k_fwd_leaf|k_fwd_diag|k_fwd_gemv|k_fwd_sf|k_tail_gather|k_tail_fwd|k_tail_fwd_chain",
                  "backward": "k_backward|k_bwd_leaf|k_bwd_partial|k_bwd_finish|k_bwd_sf|k_tail_dscale|k_tail_bwd|"
                              "k_tail_bwd_chain"}

@@ -260,6 +260,8 @@ class KktDevice {
     bool chain_pairs_ = false; // dense-tail chains with two blocks per workgroup (k_tail_fwd_pair / _bwd_pair)
     bool chain_lead_ = false;  // forward dense-tail sweep by one lead workgroup + helpers (k_tail_fwd_lead)
     DevBuf<int> dtail_task_ptr_, dtail_kslot_, dtail_kslot_ptr_;
+    DevBuf<int> dlead_ticket_;         // k_tail_fwd_lead's role tickets (never reset within a run)
+    long long lead_ticket_next_ = 0;
     DevBuf<unsigned> dvisit_list_;     // TailView::vlist (tail_visit_schedule; IPO_HIP_VISIT_SCHED=0: none)
     std::vector<int> visit_ptr_;       // TailView::vptr
     DevBuf<uint64_t> dtail_tasks_, dutasks_;

@@ -1075,23 +1075,20 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
     }
     __syncthreads();
     SF_STAMP(stamp_it, 5);
-    if (wv == 0) {
-        int bad[R] = {};
-        double zr[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) zr[r] = lane < nc ? zl[r][lane] : 0.0;
-        tri_lower<R, true>(zr, Ls, lv, nc, eps, bad);
+    if (wv < R) {                 // wave r solves right-hand side r (independent chains)
+        const int r = wv;
+        int bad[1] = {};
+        double zr[1] = {lane < nc ? zl[r][lane] : 0.0};
+        const double e1[1] = {r == 0 ? eps[0] : eps[R - 1]};
+        tri_lower<1, true>(zr, Ls, lv, nc, e1, bad);
         if (lane < nc) {
             // zout: z_s goes to a mirror instead (the chunk items of one
             // supernode each solve it and must all read its right-hand side)
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                if (zout) sc1_store(zout + r * zos + lane, zr[r]);
-                else V.z[r * V.zs + c0 + lane] = zr[r];
-                zl[r][lane] = zr[r];
-            }
+            if (zout) sc1_store(zout + r * zos + lane, zr[0]);
+            else V.z[r * V.zs + c0 + lane] = zr[0];
+            zl[r][lane] = zr[0];
         }
-        flag_bad<R>(p, bad);
+        if (bad[0]) atomicOr(&p.incons[r], 1);
     }
     __syncthreads();
 }
@@ -1329,20 +1326,16 @@ k_backward(PlanView p, const int* __restrict__ level_sups, int q0, SweepVecs V, 
             }
     }
     __syncthreads();
-    if (wv != 0) return;
-    double eps[R];
-    load_eps<R>(epsp, eps);
-    int bad[R] = {};
-    double zr[R];
-#pragma unroll
-    for (int r = 0; r < R; r++)
-        zr[r] = lane < nc ? dscale_rule(p, c0 + lane, V.z[r * V.zs + c0 + lane], eps[r], bad[r]) - xs[r][lane] : 0.0;
-    tri_upper<R>(zr, Ls, lv, nc, eps, bad);
-    if (lane < nc) {
-#pragma unroll
-        for (int r = 0; r < R; r++) V.z[r * V.zs + c0 + lane] = zr[r];
-    }
-    flag_bad<R>(p, bad);
+    if (wv >= R) return;
+    // wave r solves right-hand side r (independent chains, one wave each)
+    const int r = wv;
+    const double e1[1] = {epsp[r]};
+    int bad[1] = {};
+    double zr[1];
+    zr[0] = lane < nc ? dscale_rule(p, c0 + lane, V.z[r * V.zs + c0 + lane], e1[0], bad[0]) - xs[r][lane] : 0.0;
+    tri_upper<1>(zr, Ls, lv, nc, e1, bad);
+    if (lane < nc) V.z[r * V.zs + c0 + lane] = zr[0];
+    if (bad[0]) atomicOr(&p.incons[r], 1);
 }
 
 // Backward for levels with large panels, part 1: per 64-row chunk of R_s,
@@ -1408,22 +1401,18 @@ k_bwd_finish(PlanView p, const int* __restrict__ level_sups, int q0, const int* 
         for (int r = 0; r < R; r++) xs[r][wv][lane] = x[r];
     }
     __syncthreads();
-    if (wv != 0) return;
-    double eps[R];
-    load_eps<R>(epsp, eps);
-    int bad[R] = {};
-    double zr[R];
-#pragma unroll
-    for (int r = 0; r < R; r++)
-        zr[r] = lane < nc ? dscale_rule(p, c0 + lane, V.z[r * V.zs + c0 + lane], eps[r], bad[r]) -
-                                (((xs[r][0][lane] + xs[r][1][lane]) + xs[r][2][lane]) + xs[r][3][lane])
-                          : 0.0;
-    tri_upper<R>(zr, Ls, lv, nc, eps, bad);
-    if (lane < nc) {
-#pragma unroll
-        for (int r = 0; r < R; r++) V.z[r * V.zs + c0 + lane] = zr[r];
-    }
-    flag_bad<R>(p, bad);
+    if (wv >= R) return;
+    // wave r solves right-hand side r (independent chains, one wave each)
+    const int r = wv;
+    const double e1[1] = {epsp[r]};
+    int bad[1] = {};
+    double zr[1];
+    zr[0] = lane < nc ? dscale_rule(p, c0 + lane, V.z[r * V.zs + c0 + lane], e1[0], bad[0]) -
+                            (((xs[r][0][lane] + xs[r][1][lane]) + xs[r][2][lane]) + xs[r][3][lane])
+                      : 0.0;
+    tri_upper<1>(zr, Ls, lv, nc, e1, bad);
+    if (lane < nc) V.z[r * V.zs + c0 + lane] = zr[0];
+    if (bad[0]) atomicOr(&p.incons[r], 1);
 }
 
 // ---------------------------------------------------- dense-tail solves
@@ -1700,13 +1689,16 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
     stage_l11(tv.S + k0 + (size_t)k0 * nt, nt, nc, Ls);
     if (tid < nc) lv[tid] = p.live[tc + k0 + tid];
     const int kq = wv * 16, nq = min(16, nc - kq);
-    // D^{-1} z of the own block does not depend on the chain: formed first
+    // D^{-1} z of the own block does not depend on the chain: formed first,
+    // by the wave that solves its right-hand side (wave r solves r: the two
+    // triangular solves of R = 2 are independent chains, one wave each runs
+    // them at about twice the pace of one wave interleaving both)
     double eps[R], zd[R];
     int bad[R] = {};
     load_eps<R>(epsp, eps);
 #pragma unroll
     for (int r = 0; r < R; r++)
-        zd[r] = (wv == 0 && lane < nc) ? dscale_rule(p, tc + k0 + lane, V.z[r * V.zs + tc + k0 + lane], eps[r], bad[r])
+        zd[r] = (wv == r && lane < nc) ? dscale_rule(p, tc + k0 + lane, V.z[r * V.zs + tc + k0 + lane], eps[r], bad[r])
                                        : 0.0;
     double acc[R][16];
 #pragma unroll
@@ -1740,19 +1732,17 @@ k_tail_bwd_chain(PlanView p, TailView tv, SweepVecs V, const double* __restrict_
     __syncthreads();
     if (tid < R * PC && tid % PC < nc) xs[tid / PC][tid % PC] = colsum_tree(red, tid / PC, tid % PC);
     __syncthreads();
-    if (wv == 0) {
-        double zr[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) zr[r] = lane < nc ? zd[r] - (i < ntb - 1 ? xs[r][lane] : 0.0) : 0.0;
-        tri_upper<R>(zr, Ls, lv, nc, eps, bad);
+    if (wv < R) {
+        const int r = wv;
+        double zr[1] = {lane < nc ? zd[r] - (i < ntb - 1 ? xs[r][lane] : 0.0) : 0.0};
+        const double e1[1] = {eps[r]};
+        int b1[1] = {bad[r]};
+        tri_upper<1>(zr, Ls, lv, nc, e1, b1);
         if (lane < nc) {
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                gran_put(gran + (((size_t)i * R + r) * 64 + lane) * 2, epoch, zr[r]);
-                V.z[r * V.zs + tc + k0 + lane] = zr[r];
-            }
+            gran_put(gran + (((size_t)i * R + r) * 64 + lane) * 2, epoch, zr[0]);
+            V.z[r * V.zs + tc + k0 + lane] = zr[0];
         }
-        flag_bad<R>(p, bad);
+        if (b1[0]) atomicOr(&p.incons[r], 1);
     }
 }
 
@@ -2046,7 +2036,7 @@ __device__ __forceinline__ double buf_ld(__amdgpu_buffer_rsrc_t rs, int voff, in
     const i32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
     return __builtin_bit_cast(double, v);
 }
-constexpr int kLeadNT = 384;
+constexpr int kLeadNT = 448;
 constexpr int kHelpBatch = 4;
 // helper partials: block i, right-hand side r, column group g, lane l ->
 // granules ((((i R + r) 4 + g) 64 + l) 2 + {0, 1}
@@ -2062,18 +2052,29 @@ __device__ __forceinline__ void lds_sync() {     // LDS-only barrier: global sto
 template <int R>
 __global__ void __launch_bounds__(kLeadNT)
 k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__ epsp, gran_t* __restrict__ gran,
-                gran_t* __restrict__ pgran, unsigned epoch) {
+                gran_t* __restrict__ pgran, unsigned epoch, int* __restrict__ ticket, int tbase) {
     extern __shared__ double lds[];
     constexpr int K = kLeadBlocks;
     const int nt = tv.nt, tc = tv.tc, ntb = tv.ntb;
-    // waves: 0 solves; 1, 2, 3 and 5 are column groups 0-3; 4 (which would
-    // share the solver's SIMD) leaves at once
+    // waves: 0 solves (right-hand side 0; 6, on SIMD 2, solves 1 when R = 2:
+    // two independent chains at one wave each); 1, 2, 3 and 5 are column
+    // groups 0-3; 4 (which would share wave 0's SIMD) leaves at once
     const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = wv <= 3 ? wv - 1 : wv - 2;     // wave-uniform (scalar buffer offsets)
     const int pl = g * 64 + lane;
-    if (wv == 4) return;
-    if (blockIdx.x > 0) {        // helper of block i
-        const int i = blockIdx.x + K, k0 = i * PC, nc = min(PC, nt - k0), jend = i - K;
+    // roles by ticket, not by blockIdx: the workgroup that draws ticket 0 is
+    // the lead, ticket t > 0 the helper of block t + K.  A helper waits only
+    // on z the lead publishes and the lead only on partials of helpers with
+    // lower tickets, each drawn by a workgroup that is running or done, so
+    // the grid drains on any share of the CUs (co-tenant kernels, shards on
+    // one device) without relying on dispatch order (ADVICE/VERDICT r04)
+    __shared__ int role_sh;
+    if (tid == 0) role_sh = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - tbase;
+    __syncthreads();
+    const int role = role_sh;
+    if (wv == 4 || (wv == 6 && (R == 1 || role > 0))) return;
+    if (role > 0) {              // helper of block i
+        const int i = role + K, k0 = i * PC, nc = min(PC, nt - k0), jend = i - K;
         double* zb = lds;        // zb[(b R + r) PC + c]
         const __amdgpu_buffer_rsrc_t rs = tail_rsrc(tv.S);
         const int nt8 = nt * 8, g16 = __builtin_amdgcn_readfirstlane(g * 16);
@@ -2126,13 +2127,12 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
     double* zh = lds + 2 * PC * (PC + 1);     // z of the last K blocks: zh[((j % K) R + r) PC + c]
     double* red = zh + K * R * PC;            // red[(r 4 + g) 64 + lane]
     int* lv = reinterpret_cast<int*>(red + R * 4 * 64);    // lv[buf PC + c]
-    if (wv == 0) {
-        // ---- solver wave
-        double eps[R], zown[R];
-        int bad[R] = {};
-        load_eps<R>(epsp, eps);
-#pragma unroll
-        for (int r = 0; r < R; r++) zown[r] = lane < min(PC, nt) ? V.z[r * V.zs + tc + lane] : 0.0;
+    if (wv == 0 || wv == 6) {
+        // ---- solver wave(s): right-hand side rs
+        const int rs = wv == 0 ? 0 : 1;
+        double eps[1] = {epsp[rs]}, zown[1];
+        int bad[1] = {};
+        zown[0] = lane < min(PC, nt) ? V.z[rs * V.zs + tc + lane] : 0.0;
 #ifdef IPO_LEAD_STAMPS
         long long sa = 0, st = 0, sb = 0;
 #endif
@@ -2140,32 +2140,24 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
         for (int i = 0; i < ntb; i++) {
             LEAD_T(t0);
             const int k0 = i * PC, nc = min(PC, nt - k0);
-            double znext[R];
+            double znext;
             const int k1 = k0 + PC, nc1 = i + 1 < ntb ? min(PC, nt - k1) : 0;
-#pragma unroll
-            for (int r = 0; r < R; r++) znext[r] = lane < nc1 ? V.z[r * V.zs + tc + k1 + lane] : 0.0;
+            znext = lane < nc1 ? V.z[rs * V.zs + tc + k1 + lane] : 0.0;
             lds_sync();                                                  // A_i
             LEAD_T(t1);
-            double zr[R];
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                const double* rd = red + r * 4 * 64 + lane;
-                zr[r] = lane < nc ? zown[r] - (((rd[0] + rd[64]) + rd[128]) + rd[192]) : 0.0;
+            double zr[1];
+            {
+                const double* rd = red + rs * 4 * 64 + lane;
+                zr[0] = lane < nc ? zown[0] - (((rd[0] + rd[64]) + rd[128]) + rd[192]) : 0.0;
             }
-            tri_lower<R, true>(zr, Ls[i & 1], lv + (i & 1) * PC, nc, eps, bad);
+            tri_lower<1, true>(zr, Ls[i & 1], lv + (i & 1) * PC, nc, eps, bad);
             LEAD_T(t2);
             if (lane < nc) {
-#pragma unroll
-                for (int r = 0; r < R; r++) {
-                    gran_put(gran + (((size_t)i * R + r) * 64 + lane) * 2, epoch, zr[r]);
-                    V.z[r * V.zs + tc + k0 + lane] = zr[r];
-                }
+                gran_put(gran + (((size_t)i * R + rs) * 64 + lane) * 2, epoch, zr[0]);
+                V.z[rs * V.zs + tc + k0 + lane] = zr[0];
             }
-#pragma unroll
-            for (int r = 0; r < R; r++) {
-                zh[((i % K) * R + r) * PC + lane] = lane < nc ? zr[r] : 0.0;
-                zown[r] = znext[r];
-            }
+            zh[((i % K) * R + rs) * PC + lane] = lane < nc ? zr[0] : 0.0;
+            zown[0] = znext;
             lds_sync();                                                  // B_i
 #ifdef IPO_LEAD_STAMPS
             LEAD_T(t3);
@@ -2173,12 +2165,12 @@ k_tail_fwd_lead(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
 #endif
         }
 #ifdef IPO_LEAD_STAMPS
-        if (lane == 0) {
+        if (lane == 0 && wv == 0) {
             g_lead_stats[0][0] = sa * 0.01 / ntb; g_lead_stats[0][1] = st * 0.01 / ntb;
             g_lead_stats[0][2] = sb * 0.01 / ntb;
         }
 #endif
-        flag_bad<R>(p, bad);
+        if (bad[0]) atomicOr(&p.incons[rs], 1);
         return;
     }
     // ---- product waves
@@ -2580,40 +2572,38 @@ __device__ __forceinline__ void sf_zrow(const SfView& sf, const SweepVecs& V, in
     for (int r = 0; r < R; r++) zi[r] = pi >= 0 ? sc1_load(sf.zpad + r * sf.zps + pi) : V.z[r * V.zs + ri];
 }
 
-// Wave 0 of a backward item: z_s = D^-1 z_s - sub (dscale_rule on the
+// Wave r of a backward item solves right-hand side r (the R chains are
+// independent; one wave each): z_s = D^-1 z_s - sub (dscale_rule on the
 // prefetched own z, d, mark; ldlt.c:473-480), then L11', z_s to z and to the
 // zpad mirror.  sub = the four wave partials of xs summed in k_bwd_finish's
 // order (chunked supernodes) or xs[r][0] (whole ones).
 template <int R>
 __device__ __forceinline__ void bwd_sf_solve(const PlanView& p, const SfView& sf, const SweepVecs& V, int s, int c0,
-                                             int nc, bool chunked, const double (&zown)[R], int lvo, double dgo,
+                                             int nc, bool chunked, double zo, int lvo, double dgo,
                                              const double (&eps)[R], const double (*Ls)[PC + 1], const int* lv,
-                                             const double (*xs)[4][PC]) {
+                                             const double (*xs)[4][PC], int r) {
     const int lane = threadIdx.x & 63;
-    int bad[R] = {};
-    double zr[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
+    const double e1[1] = {r == 0 ? eps[0] : eps[R - 1]};
+    int bad[1] = {};
+    double zr[1];
+    {
         const double sub = chunked ? ((xs[r][0][lane] + xs[r][1][lane]) + xs[r][2][lane]) + xs[r][3][lane]
                                    : xs[r][0][lane];
         double zd = 0.0;
         if (lane < nc) {
-            zd = zown[r];
+            zd = zo;
             if (lvo) zd = zd / dgo;
-            else if (fabs(zd) > eps[r]) bad[r] = 1;
+            else if (fabs(zd) > e1[0]) bad[0] = 1;
             else zd = 0.0;
         }
-        zr[r] = lane < nc ? zd - sub : 0.0;
+        zr[0] = lane < nc ? zd - sub : 0.0;
     }
-    tri_upper<R, true>(zr, Ls, lv, nc, eps, bad);
+    tri_upper<1, true>(zr, Ls, lv, nc, e1, bad);
     if (lane < nc) {
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-            V.z[r * V.zs + c0 + lane] = zr[r];
-            sc1_store(sf.zpad + r * sf.zps + sf.zbase[s] + lane, zr[r]);
-        }
+        V.z[r * V.zs + c0 + lane] = zr[0];
+        sc1_store(sf.zpad + r * sf.zps + sf.zbase[s] + lane, zr[0]);
     }
-    flag_bad<R>(p, bad);
+    if (bad[0]) atomicOr(&p.incons[r], 1);
 }
 
 template <int R>
@@ -2661,11 +2651,10 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             for (int q = 0; q < 16; q++) t[q] = col[(size_t)min(q, max(nq, 1) - 1) * h];
             stage_l11(panel, h, nc, Ls);
             if (tid < nc) lv[tid] = p.live[c0 + tid];
-            double zown[R], dgo = 1.0;
+            double zown = 0.0, dgo = 1.0;     // of the right-hand side wave wv < R solves
             int lvo = 1;
-            if (wv == 0 && lane < nc) {
-#pragma unroll
-                for (int r = 0; r < R; r++) zown[r] = sc1_load(sf.zpad + r * sf.zps + sf.zbase[s] + lane);
+            if (wv < R && lane < nc) {
+                zown = sc1_load(sf.zpad + wv * sf.zps + sf.zbase[s] + lane);
                 lvo = p.live[c0 + lane];
                 dgo = p.dg[c0 + lane];
             }
@@ -2705,7 +2694,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
 #pragma unroll
             for (int r = 0; r < R; r++) xs[r][wv][lane] = x[r];
             __syncthreads();
-            if (wv == 0) bwd_sf_solve<R>(p, sf, V, s, c0, nc, true, zown, lvo, dgo, eps, Ls, lv, xs);
+            if (wv < R) bwd_sf_solve<R>(p, sf, V, s, c0, nc, true, zown, lvo, dgo, eps, Ls, lv, xs, wv);
             sf_publish_next(sf.flag, s, sf.epoch, slot, nxt);
             continue;
         }
@@ -2716,13 +2705,11 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
         // lookups are loaded before the wait
         stage_l11(panel, h, nc, Ls);
         if (tid < nc) lv[tid] = p.live[c0 + tid];
-        double zown[R], dgo = 1.0;
+        double zown = 0.0, dgo = 1.0;     // of the right-hand side wave wv < R solves
         int lvo = 1;
-        if (wv == 0 && lane < nc) {
+        if (wv < R && lane < nc) {
             // a chunked supernode's forward z_s is in the zpad mirror (k_fwd_sf)
-#pragma unroll
-            for (int r = 0; r < R; r++)
-                zown[r] = code == -2 ? sc1_load(sf.zpad + r * sf.zps + sf.zbase[s] + lane) : V.z[r * V.zs + c0 + lane];
+            zown = code == -2 ? sc1_load(sf.zpad + wv * sf.zps + sf.zbase[s] + lane) : V.z[wv * V.zs + c0 + lane];
             lvo = p.live[c0 + lane];
             dgo = p.dg[c0 + lane];
         }
@@ -2805,7 +2792,7 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
             if (tid < R * PC && tid % PC < nc) xs[tid / PC][0][tid % PC] = colsum_tree(red, tid / PC, tid % PC);
             __syncthreads();
         }
-        if (wv == 0) bwd_sf_solve<R>(p, sf, V, s, c0, nc, code == -2, zown, lvo, dgo, eps, Ls, lv, xs);
+        if (wv < R) bwd_sf_solve<R>(p, sf, V, s, c0, nc, code == -2, zown, lvo, dgo, eps, Ls, lv, xs, wv);
         sf_publish_next(sf.flag, s, sf.epoch, slot, nxt);
     }
 }
@@ -3360,6 +3347,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         dDepI_.alloc(8);
         // R <= 2 right-hand sides: z of every block, then k_tail_fwd_lead's helper partials
         dChainGran_.alloc(static_cast<size_t>(plan_.ntb) * (2 * 128 + 2 * 4 * 64 * 2));
+        dlead_ticket_.alloc(1);
+        IPO_HIP_CHECK(hipMemsetAsync(dlead_ticket_.get(), 0, sizeof(int), s));
+        lead_ticket_next_ = 0;
         IPO_HIP_CHECK(hipMemsetAsync(dChainGran_.get(), 0, dChainGran_.bytes(), s));
         if (plan_.ntb <= kChainMaxBlocks) {
             for (const void* f : {reinterpret_cast<const void*>(&k_tail_fwd_chain<1>),
@@ -4041,11 +4031,18 @@ void KktDevice::sweep(double* dz, const double* epsp) {
         hipLaunchKernelGGL(k_tail_gather<R>, dim3(ceil_div(plan_.nt, 4)), dim3(NT), 0, s, tv, dyrow_ptr_.get(),
                            dyrow_idx_.get(), V);
         tail_rhs_end(dz, R);
-        if (chain_lead_)
-            hipLaunchKernelGGL(k_tail_fwd_lead<R>, dim3(1 + std::max(0, plan_.ntb - 1 - kLeadBlocks)), dim3(kLeadNT),
-                               kChainLds, s, pv, tv, V, epsp, dChainGran_.get(),
-                               dChainGran_.get() + static_cast<size_t>(plan_.ntb) * 2 * 128, ++chain_epoch_);
-        else if (chain_pairs_)
+        if (chain_lead_) {
+            const int grid = 1 + std::max(0, plan_.ntb - 1 - kLeadBlocks);
+            if (lead_ticket_next_ + grid > (1LL << 30)) {
+                IPO_HIP_CHECK(hipMemsetAsync(dlead_ticket_.get(), 0, sizeof(int), s));
+                lead_ticket_next_ = 0;
+            }
+            const int tb = static_cast<int>(lead_ticket_next_);
+            lead_ticket_next_ += grid;
+            hipLaunchKernelGGL(k_tail_fwd_lead<R>, dim3(grid), dim3(kLeadNT), kChainLds, s, pv, tv, V, epsp,
+                               dChainGran_.get(), dChainGran_.get() + static_cast<size_t>(plan_.ntb) * 2 * 128,
+                               ++chain_epoch_, dlead_ticket_.get(), tb);
+        } else if (chain_pairs_)
             hipLaunchKernelGGL(k_tail_fwd_pair<R>, dim3((plan_.ntb + 1) / 2), dim3(NT), kPairFwdLds, s, pv, tv, V, epsp,
                                dChainGran_.get(), ++chain_epoch_);
         else
