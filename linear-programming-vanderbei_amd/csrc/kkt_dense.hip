@@ -1523,11 +1523,35 @@ std::vector<unsigned> tail_visit_schedule(int ntb, int nt, int K, int cap, std::
             tot[t]--;
         }
     }
+    // XCD grouping (speed only, never correctness): workgroups b and b + 8
+    // share an XCD and its L2 (MI355X_MICROARCH.md, round-robin placement),
+    // and every visit of column c reads the same blocks L(c, b0 .. b1 - 1)
+    // (the B operand, W = L D): the visits of column c go to workgroup ids of
+    // one residue mod 8 where possible, so those blocks come from one L2
     std::vector<unsigned> out;
     ptr.assign(ntb + 1, 0);
+    const bool xcd = !std::getenv("IPO_HIP_VISIT_XCD") || std::atoi(std::getenv("IPO_HIP_VISIT_XCD")) != 0;
     for (int t = 0; t < ntb; t++) {
         ptr[t] = static_cast<int>(out.size());
-        for (const V& v : L[t])
+        std::vector<V> order;
+        if (xcd && !L[t].empty()) {
+            const int gp = tot[t] - static_cast<int>(L[t].size());
+            std::vector<std::vector<V>> q(8);
+            for (const V& v : L[t]) q[v.c % 8].push_back(v);
+            std::vector<size_t> head(8, 0);
+            for (size_t e = 0; e < L[t].size(); e++) {
+                int x = (gp + static_cast<int>(e)) % 8;
+                if (head[x] == q[x].size()) {           // this residue's columns are used up: the fullest other
+                    size_t best = 0;
+                    for (int y = 0; y < 8; y++)
+                        if (q[y].size() - head[y] > best) { best = q[y].size() - head[y]; x = y; }
+                }
+                order.push_back(q[x][head[x]++]);
+            }
+        } else {
+            order = L[t];
+        }
+        for (const V& v : order)
             out.push_back(static_cast<unsigned>(v.bi) | static_cast<unsigned>(v.c) << 8 |
                           static_cast<unsigned>(v.b0) << 16 | static_cast<unsigned>(v.b1) << 24);
     }

@@ -201,8 +201,11 @@ def test_tail_visit_schedule_bitwise(name):
     launches so that no launch needs more workgroups than the device has
     CUs) against visit_hi's placement alone (IPO_HIP_VISIT_SCHED=0): every
     tile receives the same chunks in the same order, so the HSD solves are
-    identical (trace and final values)."""
+    identical (trace and final values).  The same holds for the launches'
+    visit order grouped by XCD (IPO_HIP_VISIT_XCD, default on) against the
+    schedule's own order: a launch holds at most one chunk of a tile."""
     assert _solve_env("IPO_HIP_VISIT_SCHED", "0", name) == _solve_env("IPO_HIP_VISIT_SCHED", "1", name)
+    assert _solve_env("IPO_HIP_VISIT_XCD", "0", name) == _solve_env("IPO_HIP_VISIT_XCD", "1", name)
 
 
 def test_sparse_dependent_pivots_bitwise():
