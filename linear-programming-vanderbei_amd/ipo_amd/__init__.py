@@ -482,6 +482,24 @@ def rccl_unique_id() -> bytes:
     return buf.raw
 
 
+def host_allreduce_callback(host_allreduce):
+    """exchange.h's HostAllreduceFn around `host_allreduce(buf, op)` (a
+    float64 numpy view of the staged buffer, reduced in place; op 0 sum,
+    1 max, 2 min): what make_host_exchange calls between its device-to-host
+    and host-to-device copies.  A raised exception returns 1, which the C
+    side turns into the solve's failure.  Keep the returned object alive as
+    long as the C side may call it."""
+    def _allreduce(user, buf, n, op):
+        try:
+            host_allreduce(np.ctypeslib.as_array(buf, shape=(n,)), op)
+            return 0
+        except Exception:       # noqa: BLE001 -- reported through the C side's failure path
+            import traceback
+            traceback.print_exc()
+            return 1
+    return ALLREDUCE_FN(_allreduce)
+
+
 class ShardContext(Context):
     """One shard of a block-angular LP on this process's GPU (ipo_hip_ctx_create_shard).
 
@@ -505,15 +523,7 @@ class ShardContext(Context):
         self._cb = None
         cb = None
         if rccl_id is None and host_allreduce is not None:
-            def _allreduce(user, buf, n, op):
-                try:
-                    host_allreduce(np.ctypeslib.as_array(buf, shape=(n,)), op)
-                    return 0
-                except Exception:       # noqa: BLE001 -- reported through the C side's failure path
-                    import traceback
-                    traceback.print_exc()
-                    return 1
-            self._cb = ALLREDUCE_FN(_allreduce)
+            self._cb = host_allreduce_callback(host_allreduce)
             cb = C.cast(self._cb, C.c_void_p)
         uid = C.create_string_buffer(bytes(rccl_id), 128) if rccl_id is not None else None
         self.h = lib().ipo_hip_ctx_create_shard(

@@ -8,7 +8,14 @@ is the global Schur complement, the tail right-hand side is summed the same
 way, every shard solves the tail itself and back-substitutes its own
 blocks.  This restates exactly that exchange with dense numpy on each
 rank's local problem (ipo_amd.shard_block_angular) and requires the global
-KKT solution; the GPU path is tests/test_gpu_shard.py.
+KKT solution.  The reductions go over one of two transports:
+  * gloo (torch.distributed), the harness's CPU stand-in for RCCL;
+  * the library's host transport: exchange.h's HostAllreduceFn as the
+    package builds it (ipo_amd.host_allreduce_callback), called through its
+    C function pointer exactly as make_host_exchange calls it after staging
+    the device buffer, over ipo_amd.hostcomm's sockets.  exchange.cpp's
+    staging copies need a device; tests/test_gpu_shard.py runs the same
+    transport through them (two processes sharing the GPU).
 """
 import os
 import socket
@@ -46,14 +53,33 @@ def local_index(p, loc):
     return rows, np.arange(b["col0"], b["col0"] + loc.n)
 
 
-def _rank_main(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    sys.path[:0] = [os.path.join(REPO, "linear-programming-vanderbei_amd"), os.path.join(REPO, "tests")]
-    import torch
-    import torch.distributed as dist
+def _allreducer(transport, rank, world):
+    """(allreduce-sum-in-place of a float64 array, close)"""
+    if transport == "gloo":
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        return (lambda a: dist.all_reduce(torch.from_numpy(a))), dist.destroy_process_group
+    import ctypes as C
 
     import ipo_amd
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ipo_amd.hostcomm import HostComm
+    comm = HostComm(rank, world)
+    ops = {0: "sum", 1: "max", 2: "min"}
+    cb = ipo_amd.host_allreduce_callback(lambda buf, op: comm.allreduce(buf, ops[op]))
+    fn = ipo_amd.ALLREDUCE_FN(C.cast(cb, C.c_void_p).value)     # the pointer the C side holds
+
+    def allreduce(a, keep=cb):      # cb owns the thunk behind fn
+        assert a.dtype == np.float64 and a.flags.c_contiguous
+        assert fn(None, a.ctypes.data_as(C.POINTER(C.c_double)), a.size, 0) == 0
+    return allreduce, comm.close
+
+
+def _rank_main(rank, world, port, q, transport="gloo"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path[:0] = [os.path.join(REPO, "linear-programming-vanderbei_amd"), os.path.join(REPO, "tests")]
+    import ipo_amd
+    allreduce, close = _allreducer(transport, rank, world)
     try:
         p = ipo_amd.synth_block_angular(*DIMS)
         E, D, fy, fx = scaling(p)
@@ -72,27 +98,29 @@ def _rank_main(rank, world, port, q):
         X = np.linalg.solve(KFF, np.column_stack([KLF.T, rF]))
         S = KLL - KLF @ X[:, :nl]
         t = rL - KLF @ X[:, nl]
-        dist.all_reduce(torch.from_numpy(S))        # in place: S and t become the global tail
-        dist.all_reduce(torch.from_numpy(t))
+        S = np.ascontiguousarray(S)
+        allreduce(S)                # in place: S and t become the global tail
+        allreduce(t)
         xL = np.linalg.solve(S, t)
         xF = np.linalg.solve(KFF, rF - KLF.T @ xL)
         q.put((rank, xL, xF[:mf], xF[mf:], None))
     except Exception as e:  # noqa: BLE001
         q.put((rank, None, None, None, repr(e)))
     finally:
-        dist.destroy_process_group()
+        close()
 
 
 @pytest.mark.timeout(180)
-def test_tail_exchange_reproduces_global_kkt_solution():
-    import torch.multiprocessing as mp
+@pytest.mark.parametrize("transport", ["gloo", "host"])
+def test_tail_exchange_reproduces_global_kkt_solution(transport):
+    import multiprocessing as mp
 
     import ipo_amd
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, q, transport)) for r in range(world)]
     for pr in procs:
         pr.start()
     out = sorted((q.get(timeout=150) for _ in procs), key=lambda t: t[0])
