@@ -5,7 +5,10 @@
 #include "kkt_plan.h"
 
 #include <algorithm>
+#include <atomic>
+#include <functional>
 #include <iterator>
+#include <memory>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -49,6 +52,53 @@ struct KeyHeap {
         }
     }
 };
+
+// Threads for the bit-matrix clique steps of the minimum-degree ordering:
+// run(fn) calls fn(tid) on every thread (tid 0 = the caller) and returns
+// when all have; between steps the workers spin briefly, then yield.
+class StepPool {
+  public:
+    explicit StepPool(int nth) {
+        for (int i = 1; i < nth; i++) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~StepPool() {
+        stop_.store(true, std::memory_order_relaxed);
+        gen_.fetch_add(1, std::memory_order_release);
+        for (auto& t : th_) t.join();
+    }
+    template <class F>
+    void run(F&& f) {
+        fn_ = std::ref(f);
+        done_.store(0, std::memory_order_relaxed);
+        gen_.fetch_add(1, std::memory_order_release);
+        f(0);
+        while (done_.load(std::memory_order_acquire) != static_cast<int>(th_.size())) relax();
+    }
+
+  private:
+    static void relax() { __builtin_ia32_pause(); }
+    void loop(int tid) {
+        unsigned seen = 0;
+        for (;;) {
+            unsigned g;
+            for (int spins = 0; (g = gen_.load(std::memory_order_acquire)) == seen; spins++) {
+                if (spins < 4096) relax();
+                else std::this_thread::yield();
+            }
+            seen = g;
+            if (stop_.load(std::memory_order_relaxed)) return;
+            fn_(tid);
+            done_.fetch_add(1, std::memory_order_release);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::function<void(int)> fn_;
+    std::atomic<unsigned> gen_{0};
+    std::atomic<int> done_{0};
+    std::atomic<bool> stop_{false};
+};
+constexpr size_t kPoolMinGroup = 256;   // smaller groups stay on the caller
+constexpr size_t kPoolChunk = 8;        // members per claim
 
 // Forced tail (kkt_plan.h): the free columns [0, Tfree) are ordered and
 // their free-row pattern is known; the forced rows (y-nodes mf..m-1) go
@@ -243,8 +293,10 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
     constexpr int kBitsNodes = 8192;
     int bw = 0;                                  // words per bit-matrix row (0: lists only)
     std::vector<uint64_t> bits;
-    std::vector<int> cidx(T, -1), gpos;
-    std::vector<uint64_t> gmask, pmask;
+    std::vector<int> cidx(T, -1), cnode, gpos;  // bit-matrix column of a node and back
+    std::vector<uint64_t> gmask, alive;
+    std::vector<std::vector<uint64_t>> pmask(1);  // per pool thread
+    std::unique_ptr<StepPool> pool;
     while (step < Tfree) {
         const int piv = hp.slot[1];
         const int dg = deg[piv];
@@ -259,32 +311,57 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
         int next = step + 1;
         group.clear();
         for (int w : nb[piv]) iperm[w] = step;
+        // (on the bit matrix: w's live row inside piv's row plus piv)
+        const uint64_t* prow = bw > 0 ? bits.data() + static_cast<size_t>(cidx[piv]) * bw : nullptr;
         for (int w : nb[piv]) {
             bool twin = false;
             if (deg[w] == dg && tier[w] == tier[piv]) {
                 twin = true;
-                for (int q : nb[w])
-                    if (!dead[q] && iperm[q] < step) { twin = false; break; }
+                if (bw > 0) {
+                    const uint64_t* row = bits.data() + static_cast<size_t>(cidx[w]) * bw;
+                    const int cp = cidx[piv];
+                    for (int k = 0; k < bw && twin; k++) {
+                        uint64_t x = row[k] & alive[k] & ~prow[k];
+                        if (k == (cp >> 6)) x &= ~(1ull << (cp & 63));
+                        twin = x == 0;
+                    }
+                } else {
+                    for (int q : nb[w])
+                        if (!dead[q] && iperm[q] < step) { twin = false; break; }
+                }
             }
             if (twin) { perm[next] = w; iperm[w] = next; next++; }
             else group.push_back(w);
         }
 
+        // L's column s: its live neighbours after it (their order is free:
+        // the relabel sorts every column)
         int width = dg;
         for (int s = step; s < next; s++) {
             const int v = perm[s];
             o.Lp[s + 1] = o.Lp[s] + width;
-            for (int w : nb[v]) {
-                if (dead[w]) continue;
-                int r = iperm[w];
+            auto take = [&](int w) {
+                const int r = iperm[w];
                 if (r > s || (r == step && w != piv)) lrows.push_back(w);
+            };
+            if (bw > 0) {
+                const uint64_t* row = bits.data() + static_cast<size_t>(cidx[v]) * bw;
+                for (int k = 0; k < bw; k++)
+                    for (uint64_t x = row[k] & alive[k]; x; x &= x - 1) take(cnode[(k << 6) + __builtin_ctzll(x)]);
+            } else {
+                for (int w : nb[v])
+                    if (!dead[w]) take(w);
             }
             width--;
         }
 
         // piv and its twins leave the survivors' lists (as dead entries)
         const int nel = next - step;
-        for (int s = step; s < next; s++) dead[perm[s]] = 1;
+        for (int s = step; s < next; s++) {
+            const int v = perm[s];
+            dead[v] = 1;
+            if (bw > 0) alive[cidx[v] >> 6] &= ~(1ull << (cidx[v] & 63));
+        }
         for (int w : group) { deg[w] -= nel; ndead[w] += nel; }
         for (int s = step; s < next; s++) {      // leave the heap
             const int v = perm[s];
@@ -323,11 +400,13 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
                 wlo = std::min(wlo, c >> 6);
                 whi = std::max(whi, c >> 6);
             }
+            // A member reads and writes only its own row, list and degree,
+            // so large groups are split over the step pool's threads (the
+            // result is the serial loop's, bit for bit).
             const size_t pw = (group.size() + 63) / 64;
-            if (pmask.size() < pw) pmask.resize(pw, 0ull);
-            for (size_t a = 0; a < group.size(); a++) {
+            auto member = [&](size_t a, uint64_t* pm) {
                 const int w = group[a], cw = cidx[w];
-                const uint64_t* row = bits.data() + static_cast<size_t>(cw) * bw;
+                uint64_t* row = bits.data() + static_cast<size_t>(cw) * bw;
                 // missing members into a bit set over group positions,
                 // read back in position order (no sort)
                 int nmiss = 0;
@@ -336,27 +415,39 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
                     if (k == (cw >> 6)) x &= ~(1ull << (cw & 63));
                     while (x) {
                         const int b = gpos[(k << 6) + __builtin_ctzll(x)];
-                        pmask[b >> 6] |= 1ull << (b & 63);
+                        pm[b >> 6] |= 1ull << (b & 63);
                         nmiss++;
                         x &= x - 1;
                     }
+                    row[k] |= gmask[k];                 // the row takes the whole clique
                 }
-                if (nmiss == 0) continue;
+                row[cw >> 6] &= ~(1ull << (cw & 63));
+                if (nmiss == 0) return;
+                auto& lst = nb[w];
                 for (size_t k = 0; k < pw; k++) {
-                    uint64_t x = pmask[k];
-                    pmask[k] = 0;
+                    uint64_t x = pm[k];
+                    if (!x) continue;
+                    pm[k] = 0;
+                    const int* gk = group.data() + (k << 6);
                     while (x) {
-                        nb[w].push_back(group[(k << 6) + __builtin_ctzll(x)]);
+                        lst.push_back(gk[__builtin_ctzll(x)]);
                         x &= x - 1;
                     }
                 }
                 deg[w] += nmiss;
-            }
-            for (size_t a = 0; a < group.size(); a++) {
-                const int cw = cidx[group[a]];
-                uint64_t* row = bits.data() + static_cast<size_t>(cw) * bw;
-                for (int k = wlo; k <= whi; k++) row[k] |= gmask[k];
-                row[cw >> 6] &= ~(1ull << (cw & 63));
+            };
+            if (pool && group.size() >= kPoolMinGroup) {
+                std::atomic<size_t> next_a{0};
+                pool->run([&](int tid) {
+                    auto& pm = pmask[tid];
+                    if (pm.size() < pw) pm.resize(pw, 0ull);
+                    for (size_t a0; (a0 = next_a.fetch_add(kPoolChunk, std::memory_order_relaxed)) < group.size();)
+                        for (size_t a = a0; a < std::min(group.size(), a0 + kPoolChunk); a++) member(a, pm.data());
+                });
+            } else {
+                auto& pm = pmask[0];
+                if (pm.size() < pw) pm.resize(pw, 0ull);
+                for (size_t a = 0; a < group.size(); a++) member(a, pm.data());
             }
             for (int k = wlo; k <= whi; k++) gmask[k] = 0;
         } else {
@@ -386,12 +477,21 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
             const int R = Tfree - step;
             bw = (R + 63) / 64;
             bits.assign(static_cast<size_t>(R) * bw, 0ull);
+            const int nth = setup_threads();
+            if (nth > 1) {
+                pool = std::make_unique<StepPool>(nth);
+                pmask.resize(nth);
+            }
             gmask.assign(bw, 0ull);
             gpos.assign(R, -1);
+            cnode.assign(R, -1);
+            alive.assign(bw, 0ull);
             int c = 0;
             for (int k = 1; k <= hp.count; k++) {
                 const int v = hp.slot[k];
                 if (v >= mf && v < m) continue;          // forced rows: outside the graph
+                cnode[c] = v;
+                alive[c >> 6] |= 1ull << (c & 63);
                 cidx[v] = c++;
             }
             for (int k = 1; k <= hp.count; k++) {
@@ -404,22 +504,35 @@ KktOrdering order_tiered_min_degree(int m, int n, const int* kA, const int* iA,
         }
     }
     o.denwin = denwin;
-    // relabel and sort every column: bucket the entries by row (columns
-    // ascending inside a row), then deal the rows out in ascending order
-    {
-        const size_t nz = lrows.size();
+    // relabel and sort every column: with the step pool, every column sorted
+    // on its own, columns split over the threads; else bucket the entries by
+    // row (columns ascending inside a row) and deal the rows out in order
+    const size_t nz = lrows.size();
+    o.Li.resize(nz);
+    if (pool) {
+        std::atomic<int> next_s{0};
+        pool->run([&](int) {
+            constexpr int kCols = 64;
+            for (int s0; (s0 = next_s.fetch_add(kCols, std::memory_order_relaxed)) < Tfree;)
+                for (int s = s0; s < std::min(Tfree, s0 + kCols); s++) {
+                    int* li = o.Li.data() + o.Lp[s];
+                    const int len = o.Lp[s + 1] - o.Lp[s];
+                    for (int k = 0; k < len; k++) li[k] = iperm[lrows[o.Lp[s] + k]];
+                    std::sort(li, li + len);
+                }
+        });
+    } else {
         std::vector<int> rptr(T + 1, 0), rcol(nz);
         for (size_t k = 0; k < nz; k++) rptr[iperm[lrows[k]] + 1]++;
         for (int v = 0; v < T; v++) rptr[v + 1] += rptr[v];
         std::vector<int> fill(rptr.begin(), rptr.end() - 1);
         for (int s = 0; s < Tfree; s++)
             for (int k = o.Lp[s]; k < o.Lp[s + 1]; k++) rcol[fill[iperm[lrows[k]]]++] = s;
-        std::vector<int>().swap(lrows);
-        o.Li.resize(nz);
         std::copy(o.Lp.begin(), o.Lp.end() - 1, fill.begin());
         for (int r = 0; r < T; r++)
             for (int k = rptr[r]; k < rptr[r + 1]; k++) o.Li[fill[rcol[k]]++] = r;
     }
+    std::vector<int>().swap(lrows);
     if (nforced > 0) add_forced_tail(o, m, kA, iA, nforced);
     double na = 0.0;
     for (int v = 0; v < T; v++) { double c = o.Lp[v + 1] - o.Lp[v]; na += c * c; }
