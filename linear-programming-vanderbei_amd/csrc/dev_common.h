@@ -158,6 +158,7 @@ struct RedJobs {
     int len[8];
     int op[8];    // 0 = dot, 1 = maxabs, 2 = max(-a/b) (ratio test)
     int nj;
+    int segmin;   // dots of at least this many entries in the segmented order (0: kOrderedMaxLen)
 };
 __global__ void __launch_bounds__(kRedThreads)
 k_reduce_jobs(RedJobs jobs, double* __restrict__ part);
@@ -165,9 +166,20 @@ k_reduce_jobs(RedJobs jobs, double* __restrict__ part);
 // Host helper: run jobs, finish into out[0..nj) (device), async on stream.
 // With g_ordered_reductions (default) dot jobs are summed in index order like
 // the reference's dotprod(); otherwise by a fixed-shape tree.
-// dots of at least kOrderedMaxLen entries use a fixed segmented order instead
-// (dev_common.hip, k_dot_segments / k_dot_finish; part: kRedBlocks per job)
+// dots of at least kOrderedMaxLen entries (RedJobs::segmin when set) use a
+// fixed segmented order instead, and maxima of at least kSegMaxLen entries
+// are taken over the same segments (order-free: bitwise the one-block form)
+// (dev_common.hip, k_dot_segments / k_dot_finish; part: kRedBlocks per job).
+// No netlib problem has a vector of kOrderedMaxLen entries; problems that do
+// (the synthetic configs) set segmin = kSegDotLen for every dot of theirs
+// (IpmSolver, dot_segmin), whose serial chains took ~1 ms each at m = 2e5.
 constexpr int kOrderedMaxLen = 1 << 19;
+constexpr int kSegDotLen = 1 << 12;
+constexpr int kSegMaxLen = 1 << 16;
+__host__ __device__ inline int dot_segmin(const RedJobs& j) { return j.segmin > 0 ? j.segmin : kOrderedMaxLen; }
+__host__ __device__ inline bool job_segmented(const RedJobs& j, int q) {
+    return j.len[q] >= (j.op[q] == 0 ? dot_segmin(j) : kSegMaxLen);
+}
 extern bool g_ordered_reductions;
 void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st);
 

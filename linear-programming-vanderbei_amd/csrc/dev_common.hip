@@ -55,6 +55,7 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
     const int len = jobs.len[j];
     const int op = jobs.op[j];
     const int tid = threadIdx.x;
+    if (job_segmented(jobs, j)) return;     // k_dot_segments / k_dot_finish (launch_reduce)
     if (op != 0) {
         // maxima are order-free: eight loads in flight per thread
         __shared__ double sh[4];
@@ -78,7 +79,6 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
         if (tid == 0) out[j] = acc;
         return;
     }
-    if (len >= kOrderedMaxLen) return;     // k_dot_segments / k_dot_finish (launch_reduce)
     constexpr int CH = 8192;
     __shared__ __attribute__((aligned(16))) double prod[CH + 16];   // + one batch of read-ahead
     double s = 0.0e0;
@@ -121,18 +121,21 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
     if (tid == 0) out[j] = s;
 }
 
-// Dots of at least kOrderedMaxLen entries (synthetic LPs of 10^6 columns; no
-// netlib problem comes near): one sequential chain of len adds took 4.3 ms,
-// one 256-thread block 1.1 ms.  Fixed segmented order instead: the vector
-// in kRedBlocks contiguous segments, segment g summed by block g (thread t
+// Segmented jobs (job_segmented): dots of at least kOrderedMaxLen entries
+// (or the job set's segmin -- synthetic LPs of 10^6 columns; no netlib
+// problem comes near) and long maxima.  One sequential chain of len adds
+// took 4.3 ms at 10^6, one 256-thread block 1.1 ms, and the serial chain of
+// a 2 x 10^5 dot ~1 ms.  Fixed segmented order instead: the vector in
+// kRedBlocks contiguous segments, segment g reduced by block g (thread t
 // takes its entries i = t, t + 256, ... in index order, the 256 partials
-// added in thread order), the segment sums added in segment order by
-// k_dot_finish -- deterministic, not the reference's rounding.
+// added in thread order), the segment results added in segment order by
+// k_dot_finish -- deterministic, not the reference's rounding (maxima are
+// order-free, so theirs is exact).
 __global__ void __launch_bounds__(kOrdThreads)
 k_dot_segments(RedJobs jobs, double* __restrict__ part) {
     const int j = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
-    const int len = jobs.len[j];
-    if (jobs.op[j] != 0 || len < kOrderedMaxLen) return;
+    const int len = jobs.len[j], op = jobs.op[j];
+    if (!job_segmented(jobs, j)) return;
     const long seg = (static_cast<long>(len) + kRedBlocks - 1) / kRedBlocks;
     const long b = seg * g, e = min(static_cast<long>(len), b + seg);
     const double* a = jobs.a[j];
@@ -145,17 +148,21 @@ k_dot_segments(RedJobs jobs, double* __restrict__ part) {
         for (int u = 0; u < 8; u++) {
             const long i = i0 + u * kOrdThreads + tid;
             pa[u] = i < e ? a[i] : 0.0;
-            pb[u] = i < e ? bb[i] : 0.0;
+            pb[u] = i < e && op != 1 ? bb[i] : 1.0;
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++)
-            if (i0 + u * kOrdThreads + tid < e) acc += pa[u] * pb[u];
+        for (int u = 0; u < 8; u++) {
+            if (i0 + u * kOrdThreads + tid >= e) continue;
+            if (op == 0) acc += pa[u] * pb[u];
+            else if (op == 1) acc = fmax(acc, ref_abs(pa[u]));
+            else acc = fmax(acc, -pa[u] / pb[u]);      // NaN ratios are ignored like hsd.c:249-258
+        }
     }
     sh[tid] = acc;
     __syncthreads();
     if (tid == 0) {
         double s = 0.0;
-        for (int t = 0; t < kOrdThreads; t++) s += sh[t];
+        for (int t = 0; t < kOrdThreads; t++) s = op == 0 ? s + sh[t] : fmax(s, sh[t]);
         part[j * kRedBlocks + g] = s;
     }
 }
@@ -163,9 +170,10 @@ k_dot_segments(RedJobs jobs, double* __restrict__ part) {
 __global__ void __launch_bounds__(64)
 k_dot_finish(RedJobs jobs, const double* __restrict__ part, double* __restrict__ out) {
     const int j = threadIdx.x;
-    if (j >= jobs.nj || jobs.op[j] != 0 || jobs.len[j] < kOrderedMaxLen) return;
+    if (j >= jobs.nj || !job_segmented(jobs, j)) return;
+    const bool mx = jobs.op[j] != 0;
     double s = 0.0;
-    for (int g = 0; g < kRedBlocks; g++) s += part[j * kRedBlocks + g];
+    for (int g = 0; g < kRedBlocks; g++) s = mx ? fmax(s, part[j * kRedBlocks + g]) : s + part[j * kRedBlocks + g];
     out[j] = s;
 }
 
@@ -323,7 +331,7 @@ void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t s
     if (g_ordered_reductions) {
         hipLaunchKernelGGL(k_reduce_ordered, dim3(jobs.nj), dim3(kOrdThreads), 0, st, jobs, out);
         bool longdot = false;
-        for (int j = 0; j < jobs.nj; j++) longdot |= jobs.op[j] == 0 && jobs.len[j] >= kOrderedMaxLen;
+        for (int j = 0; j < jobs.nj; j++) longdot |= job_segmented(jobs, j);
         if (longdot) {     // part holds kRedBlocks partials per job (the callers' buffers: 8 jobs)
             hipLaunchKernelGGL(k_dot_segments, dim3(kRedBlocks, jobs.nj), dim3(kOrdThreads), 0, st, jobs, part);
             hipLaunchKernelGGL(k_dot_finish, dim3(1), dim3(64), 0, st, jobs, part, out);

@@ -103,6 +103,7 @@ class IpmSolver {
     Exchange* xch_ = nullptr;
     int mcnt_ = 0;               // rows this shard counts in sums (linking rows on rank 0 only)
     int mg_ = 0, ng_ = 0;        // global sizes (mu's denominator, the trace)
+    int dot_segmin_ = 0;         // RedJobs::segmin of the solver's dots (dev_common.h)
     long nzg_ = 0;
     std::unique_ptr<KktDevice> kkt_;
     DevBuf<double> b_, c_, x_, y_, w_, z_;

@@ -343,6 +343,10 @@ IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A
             if (xch_->rank() != 0) mcnt_ = m - nforced_;   // linking rows are counted on rank 0
         }
     }
+    // LPs with a vector of kOrderedMaxLen entries (none in netlib) take every
+    // dot of theirs in the segmented order; IPO_HIP_DOT_SEGMIN overrides
+    dot_segmin_ = std::max(mg_, ng_) >= kOrderedMaxLen ? kSegDotLen : 0;
+    if (const char* e = std::getenv("IPO_HIP_DOT_SEGMIN")) dot_segmin_ = std::max(0, std::atoi(e));
     if (!stream_) {
         IPO_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
         own_stream_ = true;
@@ -461,6 +465,7 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
     for (iter = 0; iter < opt.max_iter; iter++) {
         RedJobs j{};
         j.nj = 4;
+        j.segmin = dot_segmin_;
         j.a[0] = z_.get(); j.b[0] = x_.get(); j.len[0] = n; j.op[0] = 0;
         j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = mcnt_; j.op[1] = 0;
         j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
@@ -557,6 +562,7 @@ int IpmSolver::run_hsd(const IpmOptions& opt, IpmResult* res) {
 
         RedJobs q{};
         q.nj = 4;
+        q.segmin = dot_segmin_;
         q.a[0] = c_.get(); q.b[0] = fx_.get(); q.len[0] = n; q.op[0] = 0;
         q.a[1] = b_.get(); q.b[1] = fy_.get(); q.len[1] = mcnt_; q.op[1] = 0;
         q.a[2] = c_.get(); q.b[2] = gx_.get(); q.len[2] = n; q.op[2] = 0;
@@ -605,6 +611,7 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
     for (iter = 0; iter < opt.max_iter; iter++) {
         RedJobs j{};
         j.nj = 4;
+        j.segmin = dot_segmin_;
         j.a[0] = z_.get(); j.b[0] = x_.get(); j.len[0] = n; j.op[0] = 0;
         j.a[1] = w_.get(); j.b[1] = y_.get(); j.len[1] = mcnt_; j.op[1] = 0;
         j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
@@ -647,6 +654,7 @@ int IpmSolver::run_hsdls(const IpmOptions& opt, IpmResult* res) {
 
         RedJobs q{};
         q.nj = 4;
+        q.segmin = dot_segmin_;
         q.a[0] = c_.get(); q.b[0] = fx_.get(); q.len[0] = n; q.op[0] = 0;
         q.a[1] = b_.get(); q.b[1] = fy_.get(); q.len[1] = mcnt_; q.op[1] = 0;
         q.a[2] = c_.get(); q.b[2] = gx_.get(); q.len[2] = n; q.op[2] = 0;
@@ -707,6 +715,7 @@ int IpmSolver::run_intpt(const IpmOptions& opt, IpmResult* res) {
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, part_.get(), 2, 0u, scal_.get() + 8);
         RedJobs j{};
         j.nj = 4;
+        j.segmin = dot_segmin_;
         j.a[0] = z_.get(); j.b[0] = x_.get(); j.len[0] = n; j.op[0] = 0;
         j.a[1] = y_.get(); j.b[1] = w_.get(); j.len[1] = mcnt_; j.op[1] = 0;
         j.a[2] = c_.get(); j.b[2] = x_.get(); j.len[2] = n; j.op[2] = 0;
