@@ -353,6 +353,17 @@ IpmSolver::IpmSolver(int m, int n, const int* kA, const int* iA, const double* A
     }
     kkt_ = std::make_unique<KktDevice>(m, n, kA, iA, A, stream_, nforced_);
     kkt_->set_exchange(xch_);
+    if (dot_segmin_ > 0 && !xch_) {
+        // trailing rows of at least kLongRow entries (the linking rows of a
+        // block-angular LP): their serial row products held up the whole
+        // refinement residual (1.5 ms a launch on configs[4])
+        constexpr int kLongRow = 256;
+        std::vector<int> cnt(m > 0 ? m : 1, 0);
+        for (int k = 0; k < kA[n]; k++) cnt[iA[k]]++;
+        int r0 = m;
+        while (r0 > 0 && cnt[r0 - 1] >= kLongRow) r0--;
+        if (r0 < m) kkt_->set_long_rows(r0);
+    }
     const size_t mm = m > 0 ? m : 1, nn = n > 0 ? n : 1;
     b_.upload(b, m, stream_);
     c_.upload(c, n, stream_);

@@ -127,6 +127,12 @@ class KktDevice {
     double epsdiag() const { return epsdiag_; }
     void set_pivot_tolerance(double t) { pivot_tol_ = t; }
     void set_epsdiag(double e) { epsdiag_ = e; }
+    // The refinement's residual takes rows row0..m-1 (trailing long rows, an
+    // unsharded solve) from one wave each (launch_link_ax: lanes strided,
+    // then a wave sum -- a fixed order, not sparse_dot's) instead of one
+    // thread's serial sparse_dot.  For LPs on the segmented-dot policy only
+    // (IpmSolver, dev_common.h kOrderedMaxLen).
+    void set_long_rows(int row0);
     double pivot_tolerance() const { return pivot_tol_; }
     int ndep() const { return ndep_; }
     int last_passes() const { return last_passes_; }
@@ -159,6 +165,8 @@ class KktDevice {
     int nforced_ = 0;
     Exchange* xch_ = nullptr;      // not owned
     DevBuf<double> dLinkAx_;       // [2 * nforced] linking-row products A_link dx per right-hand side
+    int long_row0_ = -1;           // set_long_rows: rows >= it by one wave each (-1: none)
+    DevBuf<double> dLongAx_;       // [2 * (m - long_row0_)] their products A dx per right-hand side
     bool shard_minor() const { return xch_ && xch_->rank() != 0; }   // holds replicas of the linking rows
     void xsum(double* d, size_t n, RedOp op) { if (xch_) xch_->allreduce(d, n, op, stream_); }
     hipStream_t stream_;

@@ -4186,6 +4186,12 @@ void KktDevice::tail_rhs_end(double* dz, int R) {
     for (int r = 0; r < R; r++) xsum(dz + (size_t)r * T_ + plan_.tail_c0, plan_.nt, RedOp::Sum);
 }
 
+void KktDevice::set_long_rows(int row0) {
+    if (xch_ || row0 < 0 || row0 >= m_) return;
+    long_row0_ = row0;
+    dLongAx_.alloc(2 * static_cast<size_t>(m_ - row0));
+}
+
 // rawsolve (ldlt.c:433-505) of R right-hand sides at dz + r * K, in place.
 void KktDevice::rawsolve(double* dz, int R) {
     hipStream_t s = stream_;
@@ -4264,11 +4270,14 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
             if (!active[r]) continue;
             hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), zv(r), dyv(r),
                                dxv(r), pass[r] == 0 ? 0 : 1);
-            const int mrow = xch_ ? m - nforced_ : m;
-            double* axl = dLinkAx_.get() + (size_t)r * nforced_;
+            const int mrow = xch_ ? m - nforced_ : long_row0_ >= 0 ? long_row0_ : m;
+            double* axl = xch_ ? dLinkAx_.get() + (size_t)r * nforced_
+                               : long_row0_ >= 0 ? dLongAx_.get() + (size_t)r * (m - long_row0_) : nullptr;
             if (xch_) {
                 launch_link_ax(mrow, m, dkAt_.get(), diAt_.get(), dAt_.get(), dxv(r), axl, s);
                 xsum(axl, nforced_, RedOp::Sum);
+            } else if (long_row0_ >= 0) {
+                launch_link_ax(mrow, m, dkAt_.get(), diAt_.get(), dAt_.get(), dxv(r), axl, s);
             }
             hipLaunchKernelGGL(k_kkt_residual, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, dkAt_.get(), diAt_.get(),
                                dAt_.get(), dkA_.get(), diA_.get(), dA_.get(), dE, dD, dfy[r], dfx[r], dyv(r), dxv(r),
