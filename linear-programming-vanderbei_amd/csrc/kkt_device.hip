@@ -370,7 +370,8 @@ k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
          const int* __restrict__ ck_part, int c0, double* __restrict__ partial,
          const int* __restrict__ ck_q, const int* __restrict__ sp_p0, const int* __restrict__ sp_n,
          int* __restrict__ split_cnt) {
-    const int c = c0 + blockIdx.x;
+    const int c = c0 + (p.xcd > 0 && static_cast<int>(gridDim.x) >= p.xcd ? xcd_chunk(blockIdx.x, gridDim.x)
+                                                                     : static_cast<int>(blockIdx.x));
     const int u = ck_u[c], kb = ck_b[c], ke = ck_e[c], pi = ck_part[c];
     const GatherTile g = unit_tile(p, tv, u, tail);
     const int lane = threadIdx.x & 63;
@@ -3625,6 +3626,11 @@ static PlanView make_view(const KktPlan&, const DevBuf<int>& col0, const DevBuf<
                              dybase_.get())
 
 static PlanView with_scale(PlanView v, double* dscale, double tau, int* incons, const int* ybase) {
+    static const int xcd = [] {
+        const char* e = std::getenv("IPO_HIP_UPDATE_XCD");     // launches of at least this many chunks (0: off)
+        return e ? std::max(0, std::atoi(e)) : 1024;
+    }();
+    v.xcd = xcd;
     v.dscale = dscale;
     v.tau = tau;
     v.incons = incons;

@@ -37,7 +37,18 @@ struct PlanView {
     double tau;      // pivot d is "zero" when |d| <= tau * dscale
     int* incons;     // [r]: right-hand side r met a dropped column with |z| > eps (ldlt.c:462)
     const int* ybase; // per supernode: first ybuf slot of its forward update values
+    int xcd;          // k_update launches of at least xcd chunks: consecutive chunks on one XCD (0: never)
 };
+
+// Workgroup b of a G-workgroup launch runs on XCD b mod 8 (round-robin
+// placement, MI355X_MICROARCH.md).  xcd_chunk(b, G) gives XCD x the
+// contiguous chunk range [start_x, start_x + count_x), in dispatch order,
+// so neighbouring chunks (the tiles of one target panel, which read the same
+// source columns for their B operand) share one L2.  A bijection on [0, G).
+static __device__ __forceinline__ int xcd_chunk(int b, int G) {
+    const int q = G >> 3, r = G & 7, x = b & 7, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
 
 // value of v in lane j (j wave-uniform), via two v_readlane_b32
 static __device__ __forceinline__ double lane_bcast(double v, int j) {
