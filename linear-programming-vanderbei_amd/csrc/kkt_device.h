@@ -242,6 +242,8 @@ class KktDevice {
     void repair_tail();
     std::vector<int> chunk_ptr_;          // per level: solve chunks [chunk_ptr_[l], chunk_ptr_[l+1])
     std::vector<int> leaf_cnt_;           // per level: leading single-column supernodes of dsweep_sups_
+    std::vector<int> leaf8_cnt_;          // per level: the first of them, small leaves (k_fwd_leaf8 / k_bwd_leaf8)
+    int small_leaves_ = 0;                // levels with at least this many small leaves pack them (IPO_HIP_SMALL_LEAVES; 0: never)
     DevBuf<int> dsweep_sups_;             // level_sups in sweep order (leaves first on unchunked levels)
     DevBuf<int> dchunk_sup_, dchunk_r0_, dsup_chunk0_;
     DevBuf<double> dPartial_;    // backward partial sums, one 64-vector per chunk

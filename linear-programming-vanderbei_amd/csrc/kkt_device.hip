@@ -1220,6 +1220,106 @@ k_bwd_leaf(PlanView p, const int* __restrict__ sups, int q0, int cnt, SweepVecs 
     if (lane == 0) flag_bad<R>(p, bad);
 }
 
+// Small leaves (<= 8 rows below, <= 8 update-list entries: the x-node
+// leaves of a large LP) eight to a wave, lanes 8q .. 8q + 7 for leaf q.
+// k_fwd_leaf's butterfly over 64 lanes, with entry e in lane e, reduces to
+// the three in-group stages followed by adds of +0.0 from the empty lanes
+// (one `+ 0.0`: further ones change nothing); k_bwd_leaf's wave_sum reaches
+// lane 0 through lanes 0-7 the same way (three adds of +0.0, then the
+// row-down steps 4, 2, 1).  Bitwise the one-wave kernels.
+constexpr int kSmallLeaf = 8;
+constexpr int kSmallLeafMinCount = 32768;     // per level, else one wave per leaf
+
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_fwd_leaf8(PlanView p, const int* __restrict__ sups, int q0, int cnt, const int* __restrict__ yrow_ptr,
+            const int* __restrict__ yrow_idx, SweepVecs V, const double* __restrict__ epsp) {
+    const int w = (blockIdx.x * NT + threadIdx.x) / kSmallLeaf, lq = threadIdx.x & (kSmallLeaf - 1);
+    if (w >= cnt) return;          // whole groups leave together
+    const int s = sups[q0 + w];
+    const int c0 = p.col0[s], hb = p.rowptr[s + 1] - p.rowptr[s];
+    const int e0 = yrow_ptr[c0], e1 = yrow_ptr[c0 + 1];
+    double pr[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) pr[r] = 0.0;
+    if (e0 + lq < e1) {
+        const int ix = yrow_idx[e0 + lq];
+#pragma unroll
+        for (int r = 0; r < R; r++) pr[r] += V.y[r * V.ys + ix];
+    }
+    double z[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        for (int o = 1; o < kSmallLeaf; o <<= 1) {
+            const double ot = __shfl_xor(pr[r], o, kSmallLeaf);
+            pr[r] = (lq & o) ? ot + pr[r] : pr[r] + ot;
+        }
+        pr[r] = pr[r] + 0.0;
+        z[r] = __shfl(V.z[r * V.zs + c0] - pr[r], 0, kSmallLeaf);
+    }
+    if (!p.live[c0]) {          // dropped column (ldlt.c:446-470)
+        double eps[R];
+        load_eps<R>(epsp, eps);
+        int bad[R] = {};
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (fabs(z[r]) > eps[r]) bad[r] = 1;
+            else z[r] = 0.0;
+        }
+        if (lq == 0) flag_bad<R>(p, bad);
+    }
+    if (lq == 0) {
+#pragma unroll
+        for (int r = 0; r < R; r++) V.z[r * V.zs + c0] = z[r];
+    }
+    if (lq < hb) {
+        const double l = p.Lx[p.off[s] + 1 + lq];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            double acc = 0.0;
+            acc += l * z[r];
+            V.y[r * V.ys + p.ybase[s] + lq] = acc;
+        }
+    }
+}
+
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_bwd_leaf8(PlanView p, const int* __restrict__ sups, int q0, int cnt, SweepVecs V, const double* __restrict__ epsp) {
+    const int w = (blockIdx.x * NT + threadIdx.x) / kSmallLeaf, lq = threadIdx.x & (kSmallLeaf - 1);
+    if (w >= cnt) return;
+    const int s = sups[q0 + w];
+    const int c0 = p.col0[s], hb = p.rowptr[s + 1] - p.rowptr[s];
+    double acc[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) acc[r] = 0.0;
+    if (lq < hb) {
+        const int ri = p.rows[p.rowptr[s] + lq];
+        const double t = p.Lx[p.off[s] + 1 + lq];
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] += t * V.z[r * V.zs + ri];
+    }
+    double eps[R];
+    load_eps<R>(epsp, eps);
+    int bad[R] = {};
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        double v = acc[r] + 0.0;                      // wave_sum's steps from lanes 32+, 16+, 8+
+        v += __shfl_down(v, 4, kSmallLeaf);
+        v += __shfl_down(v, 2, kSmallLeaf);
+        v += __shfl_down(v, 1, kSmallLeaf);
+        if (lq == 0) {
+            double zr = dscale_rule(p, c0, V.z[r * V.zs + c0], eps[r], bad[r]) - v;
+            if (!p.live[c0]) {
+                if (fabs(zr) > eps[r]) bad[r] = 1;
+                else zr = 0.0;
+            }
+            V.z[r * V.zs + c0] = zr;
+        }
+    }
+    if (lq == 0) flag_bad<R>(p, bad);
+}
+
 // Forward for levels with large panels, part 1: diagonal parts only.
 template <int R>
 __global__ void __launch_bounds__(NT)
@@ -3028,6 +3128,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         // each, k_fwd_leaf / k_bwd_leaf), the rest after them
         std::vector<int> ss(plan_.level_sups);
         leaf_cnt_.assign(plan_.nlevels, 0);
+        leaf8_cnt_.assign(plan_.nlevels, 0);
+        small_leaves_ = kSmallLeafMinCount;
+        if (const char* e = std::getenv("IPO_HIP_SMALL_LEAVES")) small_leaves_ = std::max(0, std::atoi(e));
         for (int l = 0; l < plan_.nlevels; l++) {
             if (chunk_ptr_[l + 1] > chunk_ptr_[l]) continue;
             const auto b = ss.begin() + plan_.level_ptr[l], e = ss.begin() + plan_.level_ptr[l + 1];
@@ -3035,6 +3138,19 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
                 return plan_.col0[sp + 1] - plan_.col0[sp] == 1 && plan_.rowptr[sp + 1] - plan_.rowptr[sp] <= 64;
             });
             leaf_cnt_[l] = static_cast<int>(mid - b);
+            if (small_leaves_ > 0) {   // the small ones first (k_fwd_leaf8 / k_bwd_leaf8)
+                const auto mid8 = std::stable_partition(b, mid, [&](int sp) {
+                    const int c = plan_.col0[sp];
+                    return plan_.rowptr[sp + 1] - plan_.rowptr[sp] <= kSmallLeaf &&
+                           plan_.yrow_ptr[c + 1] - plan_.yrow_ptr[c] <= kSmallLeaf;
+                });
+                leaf8_cnt_[l] = static_cast<int>(mid8 - b);
+                // a wave of eight leaves touches eight times the cache lines
+                // per load: slower on latency-bound levels (dfl001's sweeps
+                // 4 ms slower per solve), faster from tens of thousands of
+                // leaves on (configs[3]: 10^6)
+                if (leaf8_cnt_[l] < small_leaves_) leaf8_cnt_[l] = 0;
+            }
         }
         dsweep_sups_.upload(ss, s);
         IPO_HIP_CHECK(hipStreamSynchronize(s));
@@ -4010,10 +4126,13 @@ void KktDevice::sweep(double* dz, const double* epsp) {
             hipLaunchKernelGGL(k_fwd_gemv<R>, dim3(ce - cb), dim3(NT), 0, s, pv, dchunk_sup_.get(), dchunk_r0_.get(), cb,
                                V);
         } else {
-            const int nl = leaf_cnt_[l];
-            if (nl > 0)
-                hipLaunchKernelGGL(k_fwd_leaf<R>, dim3(ceil_div(nl, NT / 64)), dim3(NT), 0, s, pv, dsweep_sups_.get(),
-                                   q0, nl, dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+            const int nl = leaf_cnt_[l], n8 = leaf8_cnt_[l];
+            if (n8 > 0)
+                hipLaunchKernelGGL(k_fwd_leaf8<R>, dim3(ceil_div(n8, NT / kSmallLeaf)), dim3(NT), 0, s, pv,
+                                   dsweep_sups_.get(), q0, n8, dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+            if (nl > n8)
+                hipLaunchKernelGGL(k_fwd_leaf<R>, dim3(ceil_div(nl - n8, NT / 64)), dim3(NT), 0, s, pv,
+                                   dsweep_sups_.get(), q0 + n8, nl - n8, dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
             if (q1 - q0 > nl)
                 hipLaunchKernelGGL(k_forward<R>, dim3(q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(), q0 + nl,
                                    dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
@@ -4094,10 +4213,13 @@ void KktDevice::sweep(double* dz, const double* epsp) {
             hipLaunchKernelGGL(k_bwd_finish<R>, dim3(q1 - q0), dim3(NT), 0, s, pv, dlevel_sups_.get(), q0,
                                dsup_chunk0_.get(), dPartial_.get(), ps, V, epsp);
         } else {
-            const int nl = leaf_cnt_[l];
-            if (nl > 0)
-                hipLaunchKernelGGL(k_bwd_leaf<R>, dim3(ceil_div(nl, NT / 64)), dim3(NT), 0, s, pv, dsweep_sups_.get(),
-                                   q0, nl, V, epsp);
+            const int nl = leaf_cnt_[l], n8 = leaf8_cnt_[l];
+            if (n8 > 0)
+                hipLaunchKernelGGL(k_bwd_leaf8<R>, dim3(ceil_div(n8, NT / kSmallLeaf)), dim3(NT), 0, s, pv,
+                                   dsweep_sups_.get(), q0, n8, V, epsp);
+            if (nl > n8)
+                hipLaunchKernelGGL(k_bwd_leaf<R>, dim3(ceil_div(nl - n8, NT / 64)), dim3(NT), 0, s, pv,
+                                   dsweep_sups_.get(), q0 + n8, nl - n8, V, epsp);
             if (q1 - q0 > nl)
                 hipLaunchKernelGGL(k_backward<R>, dim3(q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(), q0 + nl,
                                    V, epsp);

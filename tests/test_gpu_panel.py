@@ -213,3 +213,23 @@ def test_sparse_dependent_pivots_bitwise():
     resolved in the kernels (IPO_HIP_SPARSE_DEP=1) and by redoing the
     factorisation (0): identical traces and final values."""
     assert _solve_env("IPO_HIP_SPARSE_DEP", "0") == _solve_env("IPO_HIP_SPARSE_DEP", "1")
+
+
+def test_small_leaves_bitwise(monkeypatch):
+    """Leaf sweeps with the small leaves (<= 8 rows below, <= 8 update-list
+    entries) eight to a wave (k_fwd_leaf8 / k_bwd_leaf8; by default on levels
+    of >= 32,768 of them, here forced on every level: IPO_HIP_SMALL_LEAVES=1)
+    against one wave per leaf (IPO_HIP_SMALL_LEAVES=0): dfl001 HSD solves
+    identical (trace and final values), and a banded LP under nested
+    dissection (10,000 x-node leaves) to the same final iterate, bit for bit."""
+    assert _solve_env("IPO_HIP_SMALL_LEAVES", "0") == _solve_env("IPO_HIP_SMALL_LEAVES", "1")
+    monkeypatch.setenv("IPO_HIP_ORDER", "nd")
+    p = ipo_amd.synth_random(2000, 10000, 4, 64)
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("IPO_HIP_SMALL_LEAVES", v)
+        r = ipo_amd.solver(p, "hsd")
+        outs.append((r["status"], r["stats"]["iters"], r["x"], r["y"], r["w"], r["z"]))
+    assert outs[0][:2] == outs[1][:2]
+    for a, b in zip(outs[0][2:], outs[1][2:]):
+        assert np.array_equal(a, b)

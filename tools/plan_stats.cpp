@@ -4,7 +4,9 @@
 // the 64 x 64 per slot an MFMA tile performs.
 //   g++ -O2 -std=c++17 -I linear-programming-vanderbei_amd/csrc tools/plan_stats.cpp \
 //       linear-programming-vanderbei_amd/csrc/kkt_symbolic.cpp linear-programming-vanderbei_amd/csrc/lp_io.cpp \
-//       -o tools/plan_stats && tools/plan_stats tests/golden/netlib/dfl001.mps.gz
+//       linear-programming-vanderbei_amd/csrc/kkt_order_nd.cpp linear-programming-vanderbei_amd/csrc/synth.cpp \
+//       -o tools/plan_stats -lz -lpthread
+//   tools/plan_stats tests/golden/netlib/dfl001.mps.gz | tools/plan_stats banded [m n band] | tools/plan_stats blockang
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -12,19 +14,34 @@
 
 #include "kkt_plan.h"
 #include "lp_io.h"
+#include "synth.h"
+#include <cstring>
+#include <cstdlib>
 
 using namespace ipo;
 
 int main(int argc, char** argv) {
-    MpsProblem mp;
-    std::string err;
-    if (read_mps(argv[1], mp, &err)) { std::printf("read: %s\n", err.c_str()); return 1; }
     SolverForm sf;
-    to_solver_form(mp, sf);
+    if (argc > 1 && !std::strcmp(argv[1], "banded")) {        // BASELINE configs[3]: banded m n band
+        SynthLP lp;
+        sf.m = argc > 2 ? std::atoi(argv[2]) : 200000;
+        sf.n = argc > 3 ? std::atoi(argv[3]) : 1000000;
+        synth_random(sf.m, sf.n, 4, argc > 4 ? std::atoi(argv[4]) : 256, 20251121ull, lp);
+        sf.kA = lp.kA; sf.iA = lp.iA; sf.A.assign(lp.iA.size(), 1.0);
+    } else if (argc > 1 && !std::strcmp(argv[1], "blockang")) {   // configs[4], one process
+        SynthLP lp;
+        synth_block_angular(8, 25000, 100000, 4, 256, 512, 2000, 20251121ull, lp);
+        sf.m = lp.m; sf.n = lp.n; sf.kA = lp.kA; sf.iA = lp.iA; sf.A.assign(lp.iA.size(), 1.0);
+    } else {
+        MpsProblem mp;
+        std::string err;
+        if (read_mps(argv[1], mp, &err)) { std::printf("read: %s\n", err.c_str()); return 1; }
+        to_solver_form(mp, sf);
+    }
     std::vector<int> kAt, iAt;
     std::vector<double> At;
     csc_transpose(sf.m, sf.n, sf.kA.data(), sf.iA.data(), sf.A.data(), kAt, iAt, At);
-    KktPlan P = build_kkt_plan(sf.m, sf.n, sf.kA.data(), sf.iA.data(), kAt.data(), iAt.data());
+    KktPlan P = build_kkt_plan(sf.m, sf.n, sf.kA.data(), sf.iA.data(), kAt.data(), iAt.data(), 0, kTailDensity);
     std::printf("m %d n %d T %d nsup %d levels %d nt %d ntb %d\n", P.m, P.n, P.T, P.nsup, P.nlevels, P.nt, P.ntb);
     // tail tiles
     const int ntile = P.ntb * (P.ntb + 1) / 2;
