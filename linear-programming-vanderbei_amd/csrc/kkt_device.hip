@@ -3086,6 +3086,23 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             fu_ptr_[l + 1] = static_cast<int>(fs.size());
             small_ptr_[l + 1] = static_cast<int>(ss.size());
         }
+        // Levels whose fused units outnumber their supernodes many times
+        // over and fill the device several times (the separator levels of
+        // nested dissection: 1,000-3,500 units, 7-14 per supernode) run the
+        // per-phase kernels instead: the fused units each refactor their
+        // supernode's diagonal block, k_diag factors it once and k_trsm's
+        // tiles only read it.  The same operations on every entry in the
+        // same order (the IPO_HIP_PANEL=0 path), so bitwise the fused one.
+        // IPO_HIP_PANEL_SPLIT: the unit count from which a level splits (0: never)
+        int split_min = 768;
+        if (const char* e = std::getenv("IPO_HIP_PANEL_SPLIT")) split_min = std::max(0, std::atoi(e));
+        split_level_.assign(plan_.nlevels, 0);
+        for (int l = 0; l < plan_.nlevels && split_min > 0; l++) {
+            const int nfu = fu_ptr_[l + 1] - fu_ptr_[l];
+            int nsup = 0;
+            for (int q = fu_ptr_[l]; q < fu_ptr_[l + 1]; q++) nsup += fj[q] == 0;
+            split_level_[l] = nfu >= split_min && nfu >= 4 * nsup;
+        }
         dfu_sup_.upload(fs, s);
         dfu_j_.upload(fj, s);
         dsmall_sups_.upload(ss, s);
@@ -3879,7 +3896,11 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
         }
         const int q0 = plan_.level_ptr[l], q1 = plan_.level_ptr[l + 1];
         ph_begin(s);
-        if (fused) {
+        if (fused && split_level_[l]) {
+            launch_diag(pv, dlevel_sups_.get(), q0, q1 - q0, tv, 0, s);
+            launch_trsm(pv, u0, u1 - u0, tv, 0, s);
+            ph_end(kPhDiag, 2, s);
+        } else if (fused) {
             const int nsm = small_ptr_[l + 1] - small_ptr_[l], nfu = fu_ptr_[l + 1] - fu_ptr_[l];
             launch_panel_small(pv, dsmall_sups_.get(), small_ptr_[l], nsm, tv.sdep, s);
             launch_panel(pv, dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], nfu, tv, -1, s);

@@ -233,3 +233,23 @@ def test_small_leaves_bitwise(monkeypatch):
     assert outs[0][:2] == outs[1][:2]
     for a, b in zip(outs[0][2:], outs[1][2:]):
         assert np.array_equal(a, b)
+
+
+def test_split_panel_levels_bitwise(monkeypatch):
+    """Wide levels by k_diag + k_trsm instead of the fused panel units (by
+    default levels of >= 768 units and >= 4 per supernode; forced on every
+    level with >= 4 units per supernode here: IPO_HIP_PANEL_SPLIT=1) against
+    the fused units on every level (IPO_HIP_PANEL_SPLIT=0): dfl001 HSD solves
+    identical (trace and final values), and a banded LP under nested
+    dissection to the same final iterate, bit for bit."""
+    assert _solve_env("IPO_HIP_PANEL_SPLIT", "0") == _solve_env("IPO_HIP_PANEL_SPLIT", "1")
+    monkeypatch.setenv("IPO_HIP_ORDER", "nd")
+    p = ipo_amd.synth_random(2000, 10000, 4, 64)
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("IPO_HIP_PANEL_SPLIT", v)
+        r = ipo_amd.solver(p, "hsd")
+        outs.append((r["status"], r["stats"]["iters"], r["x"], r["y"], r["w"], r["z"]))
+    assert outs[0][:2] == outs[1][:2]
+    for a, b in zip(outs[0][2:], outs[1][2:]):
+        assert np.array_equal(a, b)
