@@ -363,8 +363,13 @@ __device__ __forceinline__ void split_sum(const double* __restrict__ partial, in
 // (MI355X_MICROARCH.md hand-off table row 1: last arriver told by its own
 // add's return value).  It resets the counter for the next factorisation.
 // tail >= 0: units are dense-tail tiles.
-template <int SG>
-__global__ void __launch_bounds__(NT)
+// OCC: workgroups per CU the registers are sized for (1: the compiler's
+// choice, 160 VGPRs = 3 per CU; 4 (default for SG = 1): 116 VGPRs, no
+// spills -- one more workgroup's slab loads in flight per CU: dfl001's
+// gather 51.1 -> 47.9 ms per solve, configs[3] / [4] +3 / +7 %;
+// IPO_HIP_UPDATE_OCC=1 restores the compiler's choice)
+template <int SG, int OCC>
+__global__ void __launch_bounds__(NT, OCC)
 k_update(PlanView p, TailView tv, int tail, const SlotRec* __restrict__ recs,
          const int* __restrict__ ck_u, const int* __restrict__ ck_b, const int* __restrict__ ck_e,
          const int* __restrict__ ck_part, int c0, double* __restrict__ partial,
@@ -4085,14 +4090,21 @@ int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, i
                            dsp_p0_.get(), dsp_n_.get(), dSplitCnt_.get(), stq);
         return 1;
     }
-    if (ck_wide_[group])
-    hipLaunchKernelGGL(k_update<4>, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
-                       dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(), dsp_n_.get(),
-                       dSplitCnt_.get());
-    else
-    hipLaunchKernelGGL(k_update<1>, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
-                       dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(), dsp_n_.get(),
-                       dSplitCnt_.get());
+    static const int occ = [] {
+        const char* e = std::getenv("IPO_HIP_UPDATE_OCC");
+        return e ? std::atoi(e) : 4;
+    }();
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(c1 - c0), dim3(NT), 0, s, pv, tv, tail, recs, dck_u_.get(), dck_b_.get(),
+                           dck_e_.get(), dck_part_.get(), c0, dPartialTile_.get(), dck_q_.get(), dsp_p0_.get(),
+                           dsp_n_.get(), dSplitCnt_.get());
+    };
+    if (ck_wide_[group]) {
+        go(k_update<4, 1>);          // (its four-partial sums spill at 128 VGPRs)
+    } else {
+        if (occ == 4) go(k_update<1, 4>);
+        else go(k_update<1, 1>);
+    }
     return 1;
 }
 
