@@ -1471,6 +1471,51 @@ k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count, int dep) 
     if (ndep && lane == 0) atomicAdd(&p.flags[0], ndep);
 }
 
+// Single-column small panels with at most 8 rows (the x-node leaves of a
+// large LP, 10^6 on configs[3]) eight to a wave, lanes 8q .. 8q + 7 for
+// panel q: k_panel_s's nc = 1 step lane for lane (the pivot and its |terms|
+// from the group's lane 0, the zero test, the dependent-pivot rule over the
+// group's rows, l = a / d below it), so bitwise the same factor.  A group
+// that bails stores nothing, as k_panel_s's wave.
+constexpr int kPanel1Rows = 8;
+
+__global__ void __launch_bounds__(256)
+k_panel_s1(PlanView p, const int* __restrict__ sups, int q0, int count, int dep) {
+    const int lane = threadIdx.x & 63, lq = lane & (kPanel1Rows - 1), gb = lane & ~(kPanel1Rows - 1);
+    const int q = (blockIdx.x * 256 + threadIdx.x) / kPanel1Rows;
+    if (q >= count) return;           // whole groups leave together
+    const int s = sups[q0 + q];
+    const int c0 = p.col0[s];
+    const int h = 1 + (p.rowptr[s + 1] - p.rowptr[s]);
+    double* panel = p.Lx + p.off[s];
+    const bool rok = lq < h;
+    const double a = rok ? panel[lq] : 0.0;
+    const double dsc = lq == 0 ? p.dscale[c0] : 0.0;
+    double dk = __shfl(a, 0, kPanel1Rows);
+    const double dsk = __shfl(dsc, 0, kPanel1Rows);
+    int alive = 1, ndep = 0;
+    const unsigned long long gmask = 0xffull << gb;
+    if (fabs(dk) <= p.tau * dsk) {                 // group-uniform
+        const bool in = lq > 0 && rok;
+        const bool nan = (__ballot(in && a != a) & gmask) != 0;
+        if (!dep || nan) {
+            if (lq == 0) atomicOr(&p.flags[1], 8);
+            return;
+        }
+        if ((__ballot(in && !(fabs(a) < 1.0e+6 * 1.0e-8)) & gmask) != 0) dk = (p.sign[c0] < 0 ? -1.0 : 1.0) * 1.0e-8;
+        else alive = 0;
+        ndep++;
+    }
+    const bool below = lq > 0 && rok;
+    const double l = alive && below ? a / dk : 0.0;     // a dropped column's L is 0
+    if (below) panel[lq] = l;
+    if (lq == 0) {
+        p.dg[c0] = dk;
+        p.live[c0] = alive;
+        if (ndep) atomicAdd(&p.flags[0], ndep);
+    }
+}
+
 }  // namespace
 
 int tail_visit_tiles(int ntb, int t, int K) {
@@ -1608,8 +1653,12 @@ void launch_tail_dep_round(const PlanView& pv, const TailView& tv, int kb, int r
                        st + out * half, sti + 4 * in, sti + 4 * out);
 }
 
-void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, int dep, hipStream_t s) {
-    if (count > 0) hipLaunchKernelGGL(k_panel_s, dim3((count + 3) / 4), dim3(256), 0, s, pv, sups, q0, count, dep);
+void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, int dep, hipStream_t s, int n1) {
+    if (n1 > 0)
+        hipLaunchKernelGGL(k_panel_s1, dim3((n1 + 256 / kPanel1Rows - 1) / (256 / kPanel1Rows)), dim3(256), 0, s, pv,
+                           sups, q0, n1, dep);
+    if (count > n1)
+        hipLaunchKernelGGL(k_panel_s, dim3((count - n1 + 3) / 4), dim3(256), 0, s, pv, sups, q0 + n1, count - n1, dep);
 }
 
 void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,

@@ -236,6 +236,7 @@ class KktDevice {
     DevBuf<int> dfu_sup_, dfu_j_;         // fused panel unit -> supernode, tile pair index
     std::vector<int> small_ptr_;          // per level: small panels [small_ptr_[l], small_ptr_[l+1]) (k_panel_s)
     std::vector<char> split_level_;       // per level: k_diag + k_trsm instead of the fused panels (wide levels)
+    std::vector<int> small1_cnt_;         // per level: leading single-column small panels of <= 8 rows (k_panel_s1)
     DevBuf<int> dsmall_sups_;
     bool use_panel_ = true;               // fused diagonal-block + panel kernels (IPO_HIP_PANEL=0: off)
     bool factor_pass(const double* dE, const double* dD, bool fused, bool tail_fused);

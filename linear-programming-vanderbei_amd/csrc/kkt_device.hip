@@ -3108,6 +3108,21 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             for (int q = fu_ptr_[l]; q < fu_ptr_[l + 1]; q++) nsup += fj[q] == 0;
             split_level_[l] = nfu >= split_min && nfu >= 4 * nsup;
         }
+        // single-column small panels of <= 8 rows first in each level's list,
+        // eight to a wave (k_panel_s1) on levels of many of them (the leaf
+        // sweeps' threshold, IPO_HIP_SMALL_LEAVES)
+        small1_cnt_.assign(plan_.nlevels, 0);
+        {
+            int thr = kSmallLeafMinCount;
+            if (const char* e = std::getenv("IPO_HIP_SMALL_LEAVES")) thr = std::max(0, std::atoi(e));
+            for (int l = 0; l < plan_.nlevels && thr > 0; l++) {
+                const auto b = ss.begin() + small_ptr_[l], e = ss.begin() + small_ptr_[l + 1];
+                const auto mid = std::stable_partition(b, e, [&](int sp) {
+                    return plan_.col0[sp + 1] - plan_.col0[sp] == 1 && 1 + plan_.rowptr[sp + 1] - plan_.rowptr[sp] <= 8;
+                });
+                if (mid - b >= thr) small1_cnt_[l] = static_cast<int>(mid - b);
+            }
+        }
         dfu_sup_.upload(fs, s);
         dfu_j_.upload(fj, s);
         dsmall_sups_.upload(ss, s);
@@ -3907,7 +3922,7 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
             ph_end(kPhDiag, 2, s);
         } else if (fused) {
             const int nsm = small_ptr_[l + 1] - small_ptr_[l], nfu = fu_ptr_[l + 1] - fu_ptr_[l];
-            launch_panel_small(pv, dsmall_sups_.get(), small_ptr_[l], nsm, tv.sdep, s);
+            launch_panel_small(pv, dsmall_sups_.get(), small_ptr_[l], nsm, tv.sdep, s, small1_cnt_[l]);
             launch_panel(pv, dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], nfu, tv, -1, s);
             ph_end(kPhDiag, (nsm > 0) + (nfu > 0), s);
         } else {

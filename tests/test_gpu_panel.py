@@ -217,11 +217,13 @@ def test_sparse_dependent_pivots_bitwise():
 
 def test_small_leaves_bitwise(monkeypatch):
     """Leaf sweeps with the small leaves (<= 8 rows below, <= 8 update-list
-    entries) eight to a wave (k_fwd_leaf8 / k_bwd_leaf8; by default on levels
-    of >= 32,768 of them, here forced on every level: IPO_HIP_SMALL_LEAVES=1)
-    against one wave per leaf (IPO_HIP_SMALL_LEAVES=0): dfl001 HSD solves
-    identical (trace and final values), and a banded LP under nested
-    dissection (10,000 x-node leaves) to the same final iterate, bit for bit."""
+    entries) eight to a wave (k_fwd_leaf8 / k_bwd_leaf8), and single-column
+    small panels of <= 8 rows factored eight to a wave (k_panel_s1) -- by
+    default on levels of >= 32,768 of them, here forced on every level:
+    IPO_HIP_SMALL_LEAVES=1 -- against one wave each (IPO_HIP_SMALL_LEAVES=0):
+    dfl001 HSD solves identical (trace and final values), and a banded LP
+    under nested dissection (10,000 x-node leaves) to the same final
+    iterate, bit for bit."""
     assert _solve_env("IPO_HIP_SMALL_LEAVES", "0") == _solve_env("IPO_HIP_SMALL_LEAVES", "1")
     monkeypatch.setenv("IPO_HIP_ORDER", "nd")
     p = ipo_amd.synth_random(2000, 10000, 4, 64)
