@@ -4115,7 +4115,9 @@ int KktDevice::launch_gather(const PlanView& pv, const TailView& tv, int tail, i
                            dsp_n_.get(), dSplitCnt_.get());
     };
     if (ck_wide_[group]) {
-        go(k_update<4, 1>);          // (its four-partial sums spill at 128 VGPRs)
+        // (four partials in flight spill at 128 and at 168 VGPRs; 3 per CU
+        // with 16 spilled measured no faster than 2 per CU)
+        go(k_update<4, 1>);
     } else {
         if (occ == 4) go(k_update<1, 4>);
         else go(k_update<1, 1>);
