@@ -1103,15 +1103,15 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
 // diagonal part, then y_s = L21 z_s for the ancestors (one row per thread).
 // D^{-1} is applied at the start of the backward sweep.
 template <int R>
-__global__ void __launch_bounds__(NT)
-k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ yrow_ptr,
-          const int* __restrict__ yrow_idx, SweepVecs V, const double* __restrict__ epsp) {
+__device__ __forceinline__ void forward_body(const PlanView& p, const int* __restrict__ level_sups, int q0,
+                                             const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
+                                             const SweepVecs& V, const double* __restrict__ epsp, int bid) {
     __shared__ double zl[R][PC];
     __shared__ double Ls[PC][PC + 1];
     __shared__ int lv[PC];
     double eps[R];
     load_eps<R>(epsp, eps);
-    const int s = level_sups[q0 + blockIdx.x];
+    const int s = level_sups[q0 + bid];
     fwd_diag<R>(p, s, yrow_ptr, yrow_idx, V, eps, zl, Ls, lv);
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int hb = p.rowptr[s + 1] - p.rowptr[s], h = nc + hb;
@@ -1132,6 +1132,13 @@ k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __r
     }
 }
 
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __restrict__ yrow_ptr,
+          const int* __restrict__ yrow_idx, SweepVecs V, const double* __restrict__ epsp) {
+    forward_body<R>(p, level_sups, q0, yrow_ptr, yrow_idx, V, epsp, blockIdx.x);
+}
+
 // Single-column supernodes with at most 64 rows below (the bulk of the
 // bottom level: one per x-node of a large LP, 10^6 on configs[3]), one wave
 // each, four per workgroup -- k_forward / k_backward spend a 256-thread
@@ -1141,10 +1148,10 @@ k_forward(PlanView p, const int* __restrict__ level_sups, int q0, const int* __r
 // parts combined by the xor butterfly; the backward products summed by
 // wave_sum), so bitwise the same sweep.
 template <int R>
-__global__ void __launch_bounds__(NT)
-k_fwd_leaf(PlanView p, const int* __restrict__ sups, int q0, int cnt, const int* __restrict__ yrow_ptr,
-           const int* __restrict__ yrow_idx, SweepVecs V, const double* __restrict__ epsp) {
-    const int w = blockIdx.x * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+__device__ __forceinline__ void fwd_leaf_body(const PlanView& p, const int* __restrict__ sups, int q0, int cnt,
+                                              const int* __restrict__ yrow_ptr, const int* __restrict__ yrow_idx,
+                                              const SweepVecs& V, const double* __restrict__ epsp, int bid) {
+    const int w = bid * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (w >= cnt) return;
     const int s = sups[q0 + w];
     const int c0 = p.col0[s], hb = p.rowptr[s + 1] - p.rowptr[s];
@@ -1193,8 +1200,28 @@ k_fwd_leaf(PlanView p, const int* __restrict__ sups, int q0, int cnt, const int*
 
 template <int R>
 __global__ void __launch_bounds__(NT)
-k_bwd_leaf(PlanView p, const int* __restrict__ sups, int q0, int cnt, SweepVecs V, const double* __restrict__ epsp) {
-    const int w = blockIdx.x * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+k_fwd_leaf(PlanView p, const int* __restrict__ sups, int q0, int cnt, const int* __restrict__ yrow_ptr,
+           const int* __restrict__ yrow_idx, SweepVecs V, const double* __restrict__ epsp) {
+    fwd_leaf_body<R>(p, sups, q0, cnt, yrow_ptr, yrow_idx, V, epsp, blockIdx.x);
+}
+
+// One launch per level for a level's leaves and its other supernodes
+// (workgroups [0, nlb): four leaves each, fwd_leaf_body; the rest one
+// supernode each, forward_body) -- the two launches' work in one launch: the
+// solve phase's launches are host-bound (the device idles 4-13 us between
+// them), so every launch saved is time saved.
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_fwd_level(PlanView p, const int* __restrict__ sups, int q0, int nl, int nlb, const int* __restrict__ yrow_ptr,
+            const int* __restrict__ yrow_idx, SweepVecs V, const double* __restrict__ epsp) {
+    if (static_cast<int>(blockIdx.x) < nlb) fwd_leaf_body<R>(p, sups, q0, nl, yrow_ptr, yrow_idx, V, epsp, blockIdx.x);
+    else forward_body<R>(p, sups, q0 + nl, yrow_ptr, yrow_idx, V, epsp, blockIdx.x - nlb);
+}
+
+template <int R>
+__device__ __forceinline__ void bwd_leaf_body(const PlanView& p, const int* __restrict__ sups, int q0, int cnt,
+                                              const SweepVecs& V, const double* __restrict__ epsp, int bid) {
+    const int w = bid * (NT / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (w >= cnt) return;
     const int s = sups[q0 + w];
     const int c0 = p.col0[s], hb = p.rowptr[s + 1] - p.rowptr[s];
@@ -1223,6 +1250,12 @@ k_bwd_leaf(PlanView p, const int* __restrict__ sups, int q0, int cnt, SweepVecs 
         }
     }
     if (lane == 0) flag_bad<R>(p, bad);
+}
+
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_bwd_leaf(PlanView p, const int* __restrict__ sups, int q0, int cnt, SweepVecs V, const double* __restrict__ epsp) {
+    bwd_leaf_body<R>(p, sups, q0, cnt, V, epsp, blockIdx.x);
 }
 
 // Small leaves (<= 8 rows below, <= 8 update-list entries: the x-node
@@ -1385,12 +1418,12 @@ k_fwd_gemv(PlanView p, const int* __restrict__ chunk_sup, const int* __restrict_
 // z_s = D^{-1} z_s - L21' z_R, then L11'.  Wave w owns columns 16w..16w+15,
 // lanes stride the rows (coalesced column reads).
 template <int R>
-__global__ void __launch_bounds__(NT)
-k_backward(PlanView p, const int* __restrict__ level_sups, int q0, SweepVecs V, const double* __restrict__ epsp) {
+__device__ __forceinline__ void backward_body(const PlanView& p, const int* __restrict__ level_sups, int q0,
+                                              const SweepVecs& V, const double* __restrict__ epsp, int bid) {
     __shared__ double xs[R][PC];
     __shared__ double Ls[PC][PC + 1];     // Ls[j][r] = L(j, r)
     __shared__ int lv[PC];
-    const int s = level_sups[q0 + blockIdx.x];
+    const int s = level_sups[q0 + bid];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int hb = p.rowptr[s + 1] - p.rowptr[s];
     const int h = nc + hb;
@@ -1442,6 +1475,21 @@ k_backward(PlanView p, const int* __restrict__ level_sups, int q0, SweepVecs V, 
     tri_upper<1>(zr, Ls, lv, nc, e1, bad);
     if (lane < nc) V.z[r * V.zs + c0 + lane] = zr[0];
     if (bad[0]) atomicOr(&p.incons[r], 1);
+}
+
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_backward(PlanView p, const int* __restrict__ level_sups, int q0, SweepVecs V, const double* __restrict__ epsp) {
+    backward_body<R>(p, level_sups, q0, V, epsp, blockIdx.x);
+}
+
+// k_fwd_level's backward counterpart
+template <int R>
+__global__ void __launch_bounds__(NT)
+k_bwd_level(PlanView p, const int* __restrict__ sups, int q0, int nl, int nlb, SweepVecs V,
+            const double* __restrict__ epsp) {
+    if (static_cast<int>(blockIdx.x) < nlb) bwd_leaf_body<R>(p, sups, q0, nl, V, epsp, blockIdx.x);
+    else backward_body<R>(p, sups, q0 + nl, V, epsp, blockIdx.x - nlb);
 }
 
 // Backward for levels with large panels, part 1: per 64-row chunk of R_s,
@@ -3167,6 +3215,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         leaf_cnt_.assign(plan_.nlevels, 0);
         leaf8_cnt_.assign(plan_.nlevels, 0);
         small_leaves_ = kSmallLeafMinCount;
+        if (const char* e = std::getenv("IPO_HIP_MERGE_LEVELS")) merge_levels_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("IPO_HIP_SMALL_LEAVES")) small_leaves_ = std::max(0, std::atoi(e));
         for (int l = 0; l < plan_.nlevels; l++) {
             if (chunk_ptr_[l + 1] > chunk_ptr_[l]) continue;
@@ -3372,7 +3421,9 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         fwd_launches_ = bwd_launches_ = sf_level_ < plan_.nlevels ? 1 : 0;
         for (int l = 0; l < sf_level_; l++) {
             const int nsl = plan_.level_ptr[l + 1] - plan_.level_ptr[l];
-            const int k = chunk_ptr_[l + 1] > chunk_ptr_[l] ? 2 : (leaf_cnt_[l] > 0) + (nsl > leaf_cnt_[l]);
+            const int nl = leaf_cnt_[l], n8 = leaf8_cnt_[l];
+            const int k = chunk_ptr_[l + 1] > chunk_ptr_[l] ? 2
+                        : (n8 > 0) + (nl > n8 && nsl > nl && merge_levels_ ? 1 : (nl > n8) + (nsl > nl));
             fwd_launches_ += k;
             bwd_launches_ += k;
         }
@@ -4180,12 +4231,19 @@ void KktDevice::sweep(double* dz, const double* epsp) {
             if (n8 > 0)
                 hipLaunchKernelGGL(k_fwd_leaf8<R>, dim3(ceil_div(n8, NT / kSmallLeaf)), dim3(NT), 0, s, pv,
                                    dsweep_sups_.get(), q0, n8, dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
-            if (nl > n8)
-                hipLaunchKernelGGL(k_fwd_leaf<R>, dim3(ceil_div(nl - n8, NT / 64)), dim3(NT), 0, s, pv,
-                                   dsweep_sups_.get(), q0 + n8, nl - n8, dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
-            if (q1 - q0 > nl)
-                hipLaunchKernelGGL(k_forward<R>, dim3(q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(), q0 + nl,
-                                   dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+            if (nl > n8 && q1 - q0 > nl && merge_levels_) {
+                const int nlb = ceil_div(nl - n8, NT / 64);
+                hipLaunchKernelGGL(k_fwd_level<R>, dim3(nlb + q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(),
+                                   q0 + n8, nl - n8, nlb, dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+            } else {
+                if (nl > n8)
+                    hipLaunchKernelGGL(k_fwd_leaf<R>, dim3(ceil_div(nl - n8, NT / 64)), dim3(NT), 0, s, pv,
+                                       dsweep_sups_.get(), q0 + n8, nl - n8, dyrow_ptr_.get(), dyrow_idx_.get(), V,
+                                       epsp);
+                if (q1 - q0 > nl)
+                    hipLaunchKernelGGL(k_forward<R>, dim3(q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(),
+                                       q0 + nl, dyrow_ptr_.get(), dyrow_idx_.get(), V, epsp);
+            }
         }
     }
     if (sf_level_ < plan_.nlevels) {      // the narrow top levels in one launch
@@ -4267,12 +4325,18 @@ void KktDevice::sweep(double* dz, const double* epsp) {
             if (n8 > 0)
                 hipLaunchKernelGGL(k_bwd_leaf8<R>, dim3(ceil_div(n8, NT / kSmallLeaf)), dim3(NT), 0, s, pv,
                                    dsweep_sups_.get(), q0, n8, V, epsp);
-            if (nl > n8)
-                hipLaunchKernelGGL(k_bwd_leaf<R>, dim3(ceil_div(nl - n8, NT / 64)), dim3(NT), 0, s, pv,
-                                   dsweep_sups_.get(), q0 + n8, nl - n8, V, epsp);
-            if (q1 - q0 > nl)
-                hipLaunchKernelGGL(k_backward<R>, dim3(q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(), q0 + nl,
-                                   V, epsp);
+            if (nl > n8 && q1 - q0 > nl && merge_levels_) {
+                const int nlb = ceil_div(nl - n8, NT / 64);
+                hipLaunchKernelGGL(k_bwd_level<R>, dim3(nlb + q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(),
+                                   q0 + n8, nl - n8, nlb, V, epsp);
+            } else {
+                if (nl > n8)
+                    hipLaunchKernelGGL(k_bwd_leaf<R>, dim3(ceil_div(nl - n8, NT / 64)), dim3(NT), 0, s, pv,
+                                       dsweep_sups_.get(), q0 + n8, nl - n8, V, epsp);
+                if (q1 - q0 > nl)
+                    hipLaunchKernelGGL(k_backward<R>, dim3(q1 - q0 - nl), dim3(NT), 0, s, pv, dsweep_sups_.get(),
+                                       q0 + nl, V, epsp);
+            }
         }
     }
     ph_end(kPhBackward, bwd_launches_, s);

@@ -255,3 +255,11 @@ def test_split_panel_levels_bitwise(monkeypatch):
     assert outs[0][:2] == outs[1][:2]
     for a, b in zip(outs[0][2:], outs[1][2:]):
         assert np.array_equal(a, b)
+
+
+def test_merged_level_sweeps_bitwise():
+    """A level's leaves and other supernodes in one sweep launch
+    (k_fwd_level / k_bwd_level, default) against two launches
+    (IPO_HIP_MERGE_LEVELS=0): the same bodies, so identical dfl001 HSD solves
+    (trace and final values)."""
+    assert _solve_env("IPO_HIP_MERGE_LEVELS", "0") == _solve_env("IPO_HIP_MERGE_LEVELS", "1")
