@@ -2952,17 +2952,39 @@ k_bwd_sf(PlanView p, SfView sf, const int* __restrict__ chunk_r0, const int* __r
 }
 
 // -------------------------------------------------------- refinement glue
-// z[v] = rhs(perm[v]) with rhs = (fy | fx)
+// The refinement pass's per-system launches, both active systems in one
+// launch (blockIdx.y = the system's slot q; the refinement phase is
+// host-bound, so a launch saved is time saved)
+struct PermJobs {
+    const double* fy[2];
+    const double* fx[2];
+    double* z[2];
+    double* dy[2];
+    double* dx[2];
+    int mode[2];
+};
+// z[v] = rhs(perm[v]) with rhs = (fy | fx); the pass's first permutation also
+// clears the consistency flags and the dropped-column eps of its sweep
+// (zi[0..1], zd[0..1]; no fill launches)
 __global__ void __launch_bounds__(NT)
-k_perm_in(int T, int m, const int* __restrict__ perm, const double* __restrict__ fy, const double* __restrict__ fx,
-          double* __restrict__ z, int* __restrict__ zi, double* __restrict__ zd) {
-    const int v = blockIdx.x * NT + threadIdx.x;
-    // a pass's first permutation also clears the consistency flags and the
-    // dropped-column eps of its sweep (zi[0..1], zd[0..1]; no fill launches)
-    if (v < 2 && zi) { zi[v] = 0; zd[v] = 0.0; }
+k_perm_in2(int T, int m, const int* __restrict__ perm, PermJobs J, int* __restrict__ zi, double* __restrict__ zd) {
+    const int v = blockIdx.x * NT + threadIdx.x, q = blockIdx.y;
+    if (q == 0 && v < 2 && zi) { zi[v] = 0; zd[v] = 0.0; }
     if (v >= T) return;
     const int o = perm[v];
-    z[v] = o < m ? fy[o] : fx[o - m];
+    J.z[q][v] = o < m ? J.fy[q][o] : J.fx[q][o - m];
+}
+// dy/dx (=|+=|-=) z[iperm[.]]
+__global__ void __launch_bounds__(NT)
+k_perm_out2(int T, int m, const int* __restrict__ iperm, PermJobs J) {
+    const int o = blockIdx.x * NT + threadIdx.x, q = blockIdx.y;
+    if (o >= T) return;
+    const double v = J.z[q][iperm[o]];
+    double* dst = o < m ? J.dy[q] + o : J.dx[q] + (o - m);
+    const int mode = J.mode[q];
+    if (mode == 0) *dst = v;
+    else if (mode == 1) *dst = *dst + v;
+    else *dst = *dst - v;
 }
 
 // dy/dx (=|+=|-=) z[iperm[.]]
@@ -2982,14 +3004,13 @@ k_perm_out(int T, int m, const int* __restrict__ iperm, const double* __restrict
 //   ry_j = fy_j - ((A dx)_j - E_j dy_j)        row gather over CSR
 //   rx_i = fx_i - ((A' dy)_i + D_i dx_i)       column gather over CSC
 // plus max-abs partials of both (ldlt.c:401).
-__global__ void __launch_bounds__(kResThreads)
-k_kkt_residual(int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
-               const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
-               const double* __restrict__ E, const double* __restrict__ D, const double* __restrict__ fy,
-               const double* __restrict__ fx, const double* __restrict__ dy, const double* __restrict__ dx,
-               double* __restrict__ ry, double* __restrict__ rx, double* __restrict__ part, int mrow,
-               const double* __restrict__ axl, const int* __restrict__ kQ, const int* __restrict__ iQ,
-               const double* __restrict__ Q, double qmax) {
+__device__ __forceinline__ void kkt_residual_body(
+    int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
+    const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A, const double* __restrict__ E,
+    const double* __restrict__ D, const double* __restrict__ fy, const double* __restrict__ fx,
+    const double* __restrict__ dy, const double* __restrict__ dx, double* __restrict__ ry, double* __restrict__ rx,
+    double* __restrict__ part, int mrow, const double* __restrict__ axl, const int* __restrict__ kQ,
+    const int* __restrict__ iQ, const double* __restrict__ Q, double qmax) {
     __shared__ double sh[kResThreads / 64];
     double mx = 0.0;
     for (int i = blockIdx.x * kResThreads + threadIdx.x; i < m + n; i += kRedBlocks * kResThreads) {
@@ -3015,6 +3036,29 @@ k_kkt_residual(int m, int n, const int* __restrict__ kAt, const int* __restrict_
     }
     mx = block_max_w<kResThreads / 64>(mx, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = mx;
+}
+
+
+struct ResJobs {
+    const double* fy[2];
+    const double* fx[2];
+    const double* dy[2];
+    const double* dx[2];
+    double* ry[2];
+    double* rx[2];
+    const double* axl[2];
+};
+// the active systems' residuals, one launch: system q = blockIdx.y writes
+// the partials of slot q (part + q kRedBlocks)
+__global__ void __launch_bounds__(kResThreads)
+k_kkt_residual2(int m, int n, const int* __restrict__ kAt, const int* __restrict__ iAt, const double* __restrict__ At,
+                const int* __restrict__ kA, const int* __restrict__ iA, const double* __restrict__ A,
+                const double* __restrict__ E, const double* __restrict__ D, ResJobs J, double* __restrict__ part,
+                int mrow, const int* __restrict__ kQ, const int* __restrict__ iQ, const double* __restrict__ Q,
+                double qmax) {
+    const int q = blockIdx.y;
+    kkt_residual_body(m, n, kAt, iAt, At, kA, iA, A, E, D, J.fy[q], J.fx[q], J.dy[q], J.dx[q], J.ry[q], J.rx[q],
+                      part + (size_t)q * kRedBlocks, mrow, J.axl[q], kQ, iQ, Q, qmax);
 }
 
 // -min|d| partials, so that the max-finisher yields -min|d| (negated on host)
@@ -4495,38 +4539,51 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
     // right-hand-side slot q of an active system is read back after it
     int incons[2] = {0, 0};
     while (active[0] || active[1]) {
-        bool first = true;
-        for (int r = 0; r < R; r++)
-            if (active[r]) {
-                hipLaunchKernelGGL(k_perm_in, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, dperm_.get(),
-                                   pass[r] == 0 ? dfy[r] : ryv(r), pass[r] == 0 ? dfx[r] : rxv(r), zv(r),
-                                   first ? dIncons_.get() : static_cast<int*>(nullptr), dScal_.get() + 4);
-                first = false;
-            }
+        {
+            PermJobs J{};
+            int na = 0;
+            for (int r = 0; r < R; r++)
+                if (active[r]) {
+                    J.fy[na] = pass[r] == 0 ? dfy[r] : ryv(r);
+                    J.fx[na] = pass[r] == 0 ? dfx[r] : rxv(r);
+                    J.z[na] = zv(r);
+                    na++;
+                }
+            hipLaunchKernelGGL(k_perm_in2, dim3(ceil_div(T, NT), na), dim3(NT), 0, s, T, m, dperm_.get(), J,
+                               dIncons_.get(), dScal_.get() + 4);
+        }
         eps_cleared_ = true;
         if (active[0] && active[1]) rawsolve(zv(0), 2);
         else rawsolve(zv(active[0] ? 0 : 1), 1);
         eps_cleared_ = false;
         int nq = 0;
-        for (int r = 0; r < R; r++) {
-            if (!active[r]) continue;
-            hipLaunchKernelGGL(k_perm_out, dim3(ceil_div(T, NT)), dim3(NT), 0, s, T, m, diperm_.get(), zv(r), dyv(r),
-                               dxv(r), pass[r] == 0 ? 0 : 1);
+        {
+            PermJobs P{};
+            ResJobs J{};
             const int mrow = xch_ ? m - nforced_ : long_row0_ >= 0 ? long_row0_ : m;
-            double* axl = xch_ ? dLinkAx_.get() + (size_t)r * nforced_
-                               : long_row0_ >= 0 ? dLongAx_.get() + (size_t)r * (m - long_row0_) : nullptr;
-            if (xch_) {
-                launch_link_ax(mrow, m, dkAt_.get(), diAt_.get(), dAt_.get(), dxv(r), axl, s);
-                xsum(axl, nforced_, RedOp::Sum);
-            } else if (long_row0_ >= 0) {
-                launch_link_ax(mrow, m, dkAt_.get(), diAt_.get(), dAt_.get(), dxv(r), axl, s);
+            for (int r = 0; r < R; r++) {
+                if (!active[r]) continue;
+                P.z[nq] = zv(r); P.dy[nq] = dyv(r); P.dx[nq] = dxv(r); P.mode[nq] = pass[r] == 0 ? 0 : 1;
+                J.fy[nq] = dfy[r]; J.fx[nq] = dfx[r]; J.dy[nq] = dyv(r); J.dx[nq] = dxv(r);
+                J.ry[nq] = ryv(r); J.rx[nq] = rxv(r);
+                J.axl[nq] = xch_ ? dLinkAx_.get() + (size_t)r * nforced_
+                                 : long_row0_ >= 0 ? dLongAx_.get() + (size_t)r * (m - long_row0_) : nullptr;
+                nq++;
             }
-            hipLaunchKernelGGL(k_kkt_residual, dim3(kRedBlocks), dim3(kResThreads), 0, s, m, n, dkAt_.get(), diAt_.get(),
-                               dAt_.get(), dkA_.get(), diA_.get(), dA_.get(), dE, dD, dfy[r], dfx[r], dyv(r), dxv(r),
-                               ryv(r), rxv(r), dPart_.get() + (size_t)nq * kRedBlocks, mrow, axl,
+            hipLaunchKernelGGL(k_perm_out2, dim3(ceil_div(T, NT), nq), dim3(NT), 0, s, T, m, diperm_.get(), P);
+            for (int q = 0; q < nq; q++) {
+                double* axl = const_cast<double*>(J.axl[q]);
+                if (xch_) {
+                    launch_link_ax(mrow, m, dkAt_.get(), diAt_.get(), dAt_.get(), J.dx[q], axl, s);
+                    xsum(axl, nforced_, RedOp::Sum);
+                } else if (long_row0_ >= 0) {
+                    launch_link_ax(mrow, m, dkAt_.get(), diAt_.get(), dAt_.get(), J.dx[q], axl, s);
+                }
+            }
+            hipLaunchKernelGGL(k_kkt_residual2, dim3(kRedBlocks, nq), dim3(kResThreads), 0, s, m, n, dkAt_.get(),
+                               diAt_.get(), dAt_.get(), dkA_.get(), diA_.get(), dA_.get(), dE, dD, J, dPart_.get(), mrow,
                                dkQ_.get() ? dkQ_.get() : static_cast<const int*>(nullptr), diQ_.get(), dQ_.get(),
                                static_cast<double>(qmax_));
-            nq++;
         }
         hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), nq, (1u << nq) - 1u,
                            dScal_.get());
