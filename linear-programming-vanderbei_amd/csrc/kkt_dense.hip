@@ -1405,11 +1405,8 @@ k_tail_col(PlanView p, TailView tv, int t) {
 // flags[1], as the other fused kernels.
 constexpr int SNC = 16;
 
-__global__ void __launch_bounds__(256)
-k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count, int dep) {
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int q = blockIdx.x * 4 + wv;
-    if (q >= count) return;
+__device__ __forceinline__ void panel_s_body(const PlanView& p, const int* __restrict__ sups, int q0, int q, int dep) {
+    const int lane = threadIdx.x & 63;
     const int s = sups[q0 + q];
     const int c0 = p.col0[s], nc = p.col0[s + 1] - c0;
     const int h = nc + (p.rowptr[s + 1] - p.rowptr[s]), ld = h;
@@ -1469,6 +1466,35 @@ k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count, int dep) 
     }
     if (lane < nc) { p.dg[c0 + lane] = mydv; p.live[c0 + lane] = mylive; }
     if (ndep && lane == 0) atomicAdd(&p.flags[0], ndep);
+}
+
+__global__ void __launch_bounds__(256)
+k_panel_s(PlanView p, const int* __restrict__ sups, int q0, int count, int dep) {
+    const int q = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (q >= count) return;
+    panel_s_body(p, sups, q0, q, dep);
+}
+
+// A sparse level's fused panel units (workgroups [0, nfu): k_panel_w's
+// work) and its small panels (the rest: eight per workgroup, one a wave,
+// k_panel_s's work) in one launch: the level chain of a problem like
+// dfl001 is a sequence of small latency-bound launches, and the two
+// kernels of a level are independent.  The same bodies, so bitwise.
+__global__ void __launch_bounds__(PNT)
+k_panel_ws(PlanView p, const int* __restrict__ fu_sup, const int* __restrict__ fu_j, int f0, int nfu, TailView tv,
+           const int* __restrict__ ssups, int s0, int nsm, int dep) {
+    __shared__ __attribute__((aligned(16))) char lds[sizeof(PanelLds)];
+    if (static_cast<int>(blockIdx.x) >= nfu) {
+        const int q = (blockIdx.x - nfu) * (PNT / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        if (q < nsm) panel_s_body(p, ssups, s0, q, dep);
+        return;
+    }
+    PanelLds& S = *reinterpret_cast<PanelLds*>(lds);
+    const int sdep = tv.sdep ? 1 : 0;
+    if (panel_w_body<false>(p, fu_sup, fu_j, f0, tv, -1, blockIdx.x, S, tv.W, false, nullptr, 0, sdep)) {
+        __syncthreads();
+        panel_w_body<true>(p, fu_sup, fu_j, f0, tv, -1, blockIdx.x, S, tv.W, false, nullptr, 0, sdep);
+    }
 }
 
 // Single-column small panels with at most 8 rows (the x-node leaves of a
@@ -1659,6 +1685,12 @@ void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, 
                            sups, q0, n1, dep);
     if (count > n1)
         hipLaunchKernelGGL(k_panel_s, dim3((count - n1 + 3) / 4), dim3(256), 0, s, pv, sups, q0 + n1, count - n1, dep);
+}
+
+void launch_panel_ws(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int nfu, const TailView& tv,
+                     const int* ssups, int s0, int nsm, int dep, hipStream_t s) {
+    hipLaunchKernelGGL(k_panel_ws, dim3(nfu + (nsm + PNT / 64 - 1) / (PNT / 64)), dim3(PNT), 0, s, pv, fu_sup, fu_j, f0,
+                       nfu, tv, ssups, s0, nsm, dep);
 }
 
 void launch_panel(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int count, const TailView& tv,

@@ -246,6 +246,7 @@ class KktDevice {
     std::vector<int> leaf_cnt_;           // per level: leading single-column supernodes of dsweep_sups_
     std::vector<int> leaf8_cnt_;          // per level: the first of them, small leaves (k_fwd_leaf8 / k_bwd_leaf8)
     bool merge_levels_ = true;            // a level's leaves and other supernodes in one sweep launch (IPO_HIP_MERGE_LEVELS)
+    bool merge_panels_ = true;            // a level's fused and small panels in one launch (k_panel_ws; the same knob)
     int small_leaves_ = 0;                // levels with at least this many small leaves pack them (IPO_HIP_SMALL_LEAVES; 0: never)
     DevBuf<int> dsweep_sups_;             // level_sups in sweep order (leaves first on unchunked levels)
     DevBuf<int> dchunk_sup_, dchunk_r0_, dsup_chunk0_;

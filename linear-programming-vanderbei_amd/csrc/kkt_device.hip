@@ -3071,7 +3071,7 @@ k_min_abs_partial(const double* __restrict__ d, int T, double* __restrict__ part
     if (threadIdx.x == 0) part[blockIdx.x] = r;
 }
 
-__global__ void k_scale_scalar(double* e, double f) { e[0] *= f; }
+__global__ void k_scale_scalar(double* e, int n, double f) { if (static_cast<int>(threadIdx.x) < n) e[threadIdx.x] *= f; }
 // dst[2r] <- src[2r] (m values), dst[2r+1] <- src[2r+1] (n values), r < R
 struct CopyOut {
     const double* src[4];
@@ -3259,7 +3259,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         leaf_cnt_.assign(plan_.nlevels, 0);
         leaf8_cnt_.assign(plan_.nlevels, 0);
         small_leaves_ = kSmallLeafMinCount;
-        if (const char* e = std::getenv("IPO_HIP_MERGE_LEVELS")) merge_levels_ = std::atoi(e) != 0;
+        if (const char* e = std::getenv("IPO_HIP_MERGE_LEVELS")) merge_levels_ = merge_panels_ = std::atoi(e) != 0;
         if (const char* e = std::getenv("IPO_HIP_SMALL_LEAVES")) small_leaves_ = std::max(0, std::atoi(e));
         for (int l = 0; l < plan_.nlevels; l++) {
             if (chunk_ptr_[l + 1] > chunk_ptr_[l]) continue;
@@ -4017,9 +4017,17 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
             ph_end(kPhDiag, 2, s);
         } else if (fused) {
             const int nsm = small_ptr_[l + 1] - small_ptr_[l], nfu = fu_ptr_[l + 1] - fu_ptr_[l];
-            launch_panel_small(pv, dsmall_sups_.get(), small_ptr_[l], nsm, tv.sdep, s, small1_cnt_[l]);
-            launch_panel(pv, dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], nfu, tv, -1, s);
-            ph_end(kPhDiag, (nsm > 0) + (nfu > 0), s);
+            const int n1 = small1_cnt_[l];
+            if (merge_panels_ && nfu > 0 && nsm > n1) {
+                launch_panel_small(pv, dsmall_sups_.get(), small_ptr_[l], n1, tv.sdep, s, n1);
+                launch_panel_ws(pv, dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], nfu, tv, dsmall_sups_.get(),
+                                small_ptr_[l] + n1, nsm - n1, tv.sdep, s);
+                ph_end(kPhDiag, 1 + (n1 > 0), s);
+            } else {
+                launch_panel_small(pv, dsmall_sups_.get(), small_ptr_[l], nsm, tv.sdep, s, n1);
+                launch_panel(pv, dfu_sup_.get(), dfu_j_.get(), fu_ptr_[l], nfu, tv, -1, s);
+                ph_end(kPhDiag, (nsm > 0) + (nfu > 0), s);
+            }
         } else {
             launch_diag(pv, dlevel_sups_.get(), q0, q1 - q0, tv, 0, s);
             ph_end(kPhDiag, 1, s);
@@ -4488,7 +4496,7 @@ void KktDevice::rawsolve(double* dz, int R) {
         j.nj = R;
         for (int r = 0; r < R; r++) { j.a[r] = dz + (size_t)r * T_; j.b[r] = nullptr; j.len[r] = n_; j.op[r] = 1; }
         launch_reduce(j, dPart_.get(), epsp, s);
-        for (int r = 0; r < R; r++) hipLaunchKernelGGL(k_scale_scalar, dim3(1), dim3(1), 0, s, epsp + r, 1.0e-6);
+        hipLaunchKernelGGL(k_scale_scalar, dim3(1), dim3(64), 0, s, epsp, R, 1.0e-6);
         xsum(epsp, R, RedOp::Max);
     } else if (!eps_cleared_) {
         IPO_HIP_CHECK(hipMemsetAsync(epsp, 0, R * sizeof(double), s));

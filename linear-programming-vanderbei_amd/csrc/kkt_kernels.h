@@ -99,6 +99,9 @@ void launch_tail_colupdate(const PlanView& pv, const TailView& tv, int t, hipStr
 void launch_tail_restore(const PlanView& pv, const TailView& tv, int kb, hipStream_t s);
 // Fused panel of supernodes sups[q0 .. q0+count) that have at most 16
 // columns and 64 rows (one wave each, k_panel_s); same bail-out contract.
+// a level's fused panel units and small panels in one launch (k_panel_ws)
+void launch_panel_ws(const PlanView& pv, const int* fu_sup, const int* fu_j, int f0, int nfu, const TailView& tv,
+                     const int* ssups, int s0, int nsm, int dep, hipStream_t s);
 // the first n1 of them single-column panels of <= 8 rows, eight to a wave (k_panel_s1)
 void launch_panel_small(const PlanView& pv, const int* sups, int q0, int count, int dep, hipStream_t s, int n1 = 0);
 

@@ -259,7 +259,8 @@ def test_split_panel_levels_bitwise(monkeypatch):
 
 def test_merged_level_sweeps_bitwise():
     """A level's leaves and other supernodes in one sweep launch
-    (k_fwd_level / k_bwd_level, default) against two launches
+    (k_fwd_level / k_bwd_level), and a level's fused and small panels in one
+    factor launch (k_panel_ws) -- default -- against separate launches
     (IPO_HIP_MERGE_LEVELS=0): the same bodies, so identical dfl001 HSD solves
     (trace and final values)."""
     assert _solve_env("IPO_HIP_MERGE_LEVELS", "0") == _solve_env("IPO_HIP_MERGE_LEVELS", "1")

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 GPU call ac: refinement passes with both systems per launch -- the
+# round-5 GPU call ac (also ad): refinement passes with both systems per launch, merged panels -- the
 # GPU suite (golden traces, bitwise comparisons), then the bench
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
