@@ -53,11 +53,12 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 METRIC = "IPM iterations/sec (ADA^T factor+solve) on netlib dfl001; duality gap ≤1e-8"
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, AMD spec (the guide has no fp64 row)
 PHASE_KERNELS = {"gather": "k_update|k_update_flat|k_update_quad",
-                 "diag": "k_panel_w|k_panel_s|k_diag", "trsm": "k_trsm",
+                 "diag": "k_panel_w|k_panel_s|k_panel_s1|k_panel_ws|k_diag", "trsm": "k_trsm",
                  "tail_syrk": "k_tail_syrk", "tail": "k_tail_pr|k_tail_col|k_tail_dep|k_tail_restore",
-                 "forward": "k_forward|k_fwd_leaf|k_fwd_diag|k_fwd_gemv|k_fwd_sf|k_tail_gather|k_tail_fwd|k_tail_fwd_chain",
-                 "backward": "k_backward|k_bwd_leaf|k_bwd_partial|k_bwd_finish|k_bwd_sf|k_tail_dscale|k_tail_bwd|"
-                             "k_tail_bwd_chain"}
+                 "forward": "k_forward|k_fwd_leaf|k_fwd_leaf8|k_fwd_level|k_fwd_diag|k_fwd_gemv|k_fwd_pre|k_fwd_sf|"
+                            "k_tail_gather|k_tail_fwd|k_tail_fwd_chain|k_tail_fwd_pair|k_tail_fwd_lead",
+                 "backward": "k_backward|k_bwd_leaf|k_bwd_leaf8|k_bwd_level|k_bwd_partial|k_bwd_finish|k_bwd_sf|"
+                             "k_tail_dscale|k_tail_bwd|k_tail_bwd_chain|k_tail_bwd_pair"}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak, MI355X_MICROARCH.md
 GOLDEN_ITERS = {"dfl001": 117, "25fv47": 91, "afiro": 33}   # evaluate/v1-cf4d5ba/netlib/ipo/*.mps.sol
 
