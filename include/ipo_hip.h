@@ -226,6 +226,12 @@ int ipo_hip_symbolic_forced(int m, int n, const int *kA, const int *iA, int nfor
 int ipo_hip_vector_bench(int m, int n, const int *kA, const int *iA, const double *A, int reps, double *ms3,
                          double *bytes3);
 
+/* sum_i a[i] b[i] over host vectors, by the solver's ordered reduction
+ * (linalg.c:17-25 dotprod's order for n < 2^19, dev_common.hip
+ * k_reduce_ordered).  Test entry (no reference counterpart: dotprod is
+ * internal to the reference).  Returns 0, or -1 (ipo_hip_last_error). */
+int ipo_hip_dot_ordered(const double *a, const double *b, int n, double *out);
+
 int ipo_hip_synth_random(int m, int n, int per_col, int band, unsigned long long seed, int *nz, int *kA, int *iA,
                          double *A, double *b, double *c, double *xs, double *ys, double *ws, double *zs);
 /* nblocks diagonal blocks (mb x nb, banded random per block) + nlink linking

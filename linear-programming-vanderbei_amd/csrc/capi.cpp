@@ -194,6 +194,10 @@ struct ipo_hip_kkt {
     ipo::DevBuf<double> E, D, fy, fx;
 };
 
+namespace ipo {
+double dot_ordered_host(const double* a, const double* b, int n);   // dev_common.hip
+}
+
 extern "C" {
 
 int solver(int m, int n, int nz, int* iA, int* kA, double* A, double* b, double* c, double f, double* x, double* y,
@@ -723,6 +727,17 @@ int ipo_hip_vector_bench(int m, int n, const int* kA, const int* iA, const doubl
                          double* bytes3) {
     try {
         ipo::vector_bench(m, n, kA, iA, A, reps, ms3, bytes3);
+        return 0;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
+
+int ipo_hip_dot_ordered(const double* a, const double* b, int n, double* out) {
+    try {
+        if (n < 0 || (n > 0 && (!a || !b)) || !out) throw std::invalid_argument("dot_ordered: bad arguments");
+        *out = ipo::dot_ordered_host(a, b, n);
         return 0;
     } catch (const std::exception& e) {
         set_err(e.what());

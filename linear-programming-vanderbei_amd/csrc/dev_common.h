@@ -182,6 +182,8 @@ __host__ __device__ inline bool job_segmented(const RedJobs& j, int q) {
 }
 extern bool g_ordered_reductions;
 void launch_reduce(const RedJobs& jobs, double* part, double* out, hipStream_t st);
+// the ordered dot of two host vectors (tests: ipo_hip_dot_ordered)
+double dot_ordered_host(const double* a, const double* b, int n);
 
 // Linking-row products of the sharded solve (exchange.h): out[i - mrow] =
 // sum_k At[k] x[iAt[k]] for rows mrow <= i < m (CSR of A), one wave per row.

@@ -78,6 +78,7 @@ EXPORTED = [
     "ipo_hip_ctx_setup_seconds", "ipo_hip_kkt_set_epsdiag",
     "ipo_hip_synth_random", "ipo_hip_synth_block_angular", "ipo_hip_symbolic_forced",
     "ipo_hip_set_device", "ipo_hip_rccl_unique_id", "ipo_hip_ctx_create_shard", "ipo_hip_vector_bench",
+    "ipo_hip_dot_ordered",
     "ipo_hip_kkt_create_q", "ipo_hip_ldlt_set_q", "ipo_hip_symbolic_q", "ipo_hip_mps_quads",
 ]
 
@@ -161,6 +162,8 @@ def lib() -> C.CDLL:
     L.ipo_hip_ctx_destroy.restype = None
     L.ipo_hip_ctx_setup_seconds.argtypes = [_P]
     L.ipo_hip_ctx_setup_seconds.restype = _D
+    L.ipo_hip_dot_ordered.argtypes = [_P, _P, _I, _P]
+    L.ipo_hip_dot_ordered.restype = _I
     L.ipo_hip_vector_bench.argtypes = [_I, _I, _P, _P, _P, _I, _P, _P]
     L.ipo_hip_vector_bench.restype = _I
     L.ipo_hip_synth_random.argtypes = [_I, _I, _I, _I, C.c_ulonglong, C.POINTER(_I)] + [_P] * 9
@@ -602,6 +605,17 @@ def synth_random(m, n, per_col=4, band=0, seed=SYNTH_SEED) -> SynthProblem:
 
 
 VECTOR_KERNELS = ("k_hsd_residuals", "k_hsd_directions", "k_step")
+
+
+def dot_ordered(a, b) -> float:
+    """The solver's ordered dot of two float64 vectors on the GPU (test entry)."""
+    require_gpu()
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    out = np.zeros(1, np.float64)
+    if lib().ipo_hip_dot_ordered(_ptr(a), _ptr(b), int(a.size), _ptr(out)):
+        raise IpoHipError("dot_ordered: " + last_error())
+    return float(out[0])
 
 
 def vector_bench(p, reps=20) -> dict:
