@@ -149,6 +149,9 @@ __device__ __forceinline__ double block_max(double v, double* sh) {
 // max instead of sum.  One 256-thread block finishes nq quantities.
 __global__ void __launch_bounds__(kRedThreads)
 k_finish_reduce(const double* __restrict__ part, int nq, unsigned maxmask, double* __restrict__ out);
+__global__ void __launch_bounds__(kRedThreads)
+k_finish_reduce_pack(const double* __restrict__ part, int nq, unsigned maxmask, double* __restrict__ out,
+                     const int* __restrict__ f, int nf, double* __restrict__ outi);
 
 // Multi-job dot / max-abs partials: job j reduces a[j][i]*b[j][i] (dot) or
 // |a[j][i]| (maxabs, b == nullptr) over i < len[j].

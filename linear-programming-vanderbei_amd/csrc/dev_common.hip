@@ -39,6 +39,21 @@ k_finish_reduce(const double* __restrict__ part, int nq, unsigned maxmask, doubl
     }
 }
 
+// k_finish_reduce, then the nf ints at f copied into the doubles at outi
+// (one launch for a read-back's scalars and flags)
+__global__ void __launch_bounds__(kRedThreads)
+k_finish_reduce_pack(const double* __restrict__ part, int nq, unsigned maxmask, double* __restrict__ out,
+                     const int* __restrict__ f, int nf, double* __restrict__ outi) {
+    __shared__ double sh[4];
+    for (int q = 0; q < nq; q++) {
+        const bool mx = (maxmask >> q) & 1u;
+        double v = part[q * kRedBlocks + threadIdx.x];
+        const double r = mx ? block_max(v, sh) : block_sum(v, sh);
+        if (threadIdx.x == 0) out[q] = r;
+    }
+    if (static_cast<int>(threadIdx.x) < nf) reinterpret_cast<int*>(outi)[threadIdx.x] = f[threadIdx.x];
+}
+
 // dotprod() of linalg.c:17-25 in its own order: one running sum, i = 0..n-1.
 // One 256-thread block per job: the products of a chunk are formed by the
 // whole block into LDS (eight loads in flight per thread), then one lane

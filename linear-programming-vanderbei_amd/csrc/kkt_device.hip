@@ -4081,14 +4081,17 @@ bool KktDevice::finish_pass(bool fused) {
     hipStream_t s = stream_;
     IPO_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_min_abs_partial, dim3(kRedBlocks), dim3(NT), 0, s, dDg_.get(), T_, dPart_.get());
-    hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), 1, 1u, dScal_.get());
     if (xch_) {   // every shard must take the same eps_diag / dependent-pivot / redo decisions
+        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), 1, 1u, dScal_.get());
         hipLaunchKernelGGL(k_flag_to_scalar, dim3(1), dim3(1), 0, s, dFlags_.get(), dScal_.get() + 1);
         hipLaunchKernelGGL(k_flag_to_scalar, dim3(1), dim3(1), 0, s, dFlags_.get() + 1, dScal_.get() + 2);
         xsum(dScal_.get(), 3, RedOp::Max);
+        hipLaunchKernelGGL(k_pack_ints, dim3(1), dim3(3), 0, s, dFlags_.get(), 3, dScal_.get() + 3);
+    } else {
+        // min|d| and the three flags in one read-back, one launch
+        hipLaunchKernelGGL(k_finish_reduce_pack, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), 1, 1u, dScal_.get(),
+                           static_cast<const int*>(dFlags_.get()), 3, dScal_.get() + 3);
     }
-    // min|d| (and the shards' maxima) and the three flags in one read-back
-    hipLaunchKernelGGL(k_pack_ints, dim3(1), dim3(3), 0, s, dFlags_.get(), 3, dScal_.get() + 3);
     IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), 5 * sizeof(double), hipMemcpyDeviceToHost, s));
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev1_, s));
     IPO_HIP_CHECK(hipStreamSynchronize(s));
@@ -4593,11 +4596,17 @@ void KktDevice::solve_multi(int R, const double* dE, const double* dD, double* c
                                dkQ_.get() ? dkQ_.get() : static_cast<const int*>(nullptr), diQ_.get(), dQ_.get(),
                                static_cast<double>(qmax_));
         }
-        hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), nq, (1u << nq) - 1u,
-                           dScal_.get());
-        xsum(dScal_.get(), nq, RedOp::Max);
         // residuals and the consistency flags in one read-back
-        hipLaunchKernelGGL(k_pack_ints, dim3(1), dim3(2), 0, s, dIncons_.get(), 2, dScal_.get() + 6);
+        if (xch_) {
+            hipLaunchKernelGGL(k_finish_reduce, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), nq, (1u << nq) - 1u,
+                               dScal_.get());
+            xsum(dScal_.get(), nq, RedOp::Max);
+            hipLaunchKernelGGL(k_pack_ints, dim3(1), dim3(2), 0, s, dIncons_.get(), 2, dScal_.get() + 6);
+        } else {
+            hipLaunchKernelGGL(k_finish_reduce_pack, dim3(1), dim3(kRedThreads), 0, s, dPart_.get(), nq,
+                               (1u << nq) - 1u, dScal_.get(), static_cast<const int*>(dIncons_.get()), 2,
+                               dScal_.get() + 6);
+        }
         IPO_HIP_CHECK(hipMemcpyAsync(hScal_, dScal_.get(), (pass[0] + pass[1] == 0 ? 8 + 2 * R : 7) * sizeof(double),
                                      hipMemcpyDeviceToHost, s));
         IPO_HIP_CHECK(hipStreamSynchronize(s));

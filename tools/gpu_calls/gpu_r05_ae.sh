@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-5 GPU call ae: ordered dots over the non-zero products only -- the
+# round-5 GPU call ae (also ag): ordered dots over the non-zero products only, finish+pack folded -- the
 # bitwise dot test, the GPU suite, the bench
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
