@@ -172,20 +172,15 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
 // Test entry (ipo_hip_dot_ordered): the ordered dot of two host vectors
 // through launch_reduce, on the default stream.
 double dot_ordered_host(const double* a, const double* b, int n) {
-    double *da = nullptr, *db = nullptr, *dout = nullptr, *dpart = nullptr;
-    IPO_HIP_CHECK(hipMalloc(&da, std::max(1, n) * sizeof(double)));
-    IPO_HIP_CHECK(hipMalloc(&db, std::max(1, n) * sizeof(double)));
-    IPO_HIP_CHECK(hipMalloc(&dout, 8 * sizeof(double)));
-    IPO_HIP_CHECK(hipMalloc(&dpart, 8 * kRedBlocks * sizeof(double)));
-    IPO_HIP_CHECK(hipMemcpy(da, a, n * sizeof(double), hipMemcpyHostToDevice));
-    IPO_HIP_CHECK(hipMemcpy(db, b, n * sizeof(double), hipMemcpyHostToDevice));
+    DevBuf<double> da(std::max(1, n)), db(std::max(1, n)), dout(8), dpart(8 * kRedBlocks);
+    IPO_HIP_CHECK(hipMemcpy(da.get(), a, n * sizeof(double), hipMemcpyHostToDevice));
+    IPO_HIP_CHECK(hipMemcpy(db.get(), b, n * sizeof(double), hipMemcpyHostToDevice));
     RedJobs j{};
     j.nj = 1;
-    j.a[0] = da; j.b[0] = db; j.len[0] = n; j.op[0] = 0;
-    launch_reduce(j, dpart, dout, nullptr);
+    j.a[0] = da.get(); j.b[0] = db.get(); j.len[0] = n; j.op[0] = 0;
+    launch_reduce(j, dpart.get(), dout.get(), nullptr);
     double r = 0.0;
-    IPO_HIP_CHECK(hipMemcpy(&r, dout, sizeof(double), hipMemcpyDeviceToHost));
-    (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout); (void)hipFree(dpart);
+    IPO_HIP_CHECK(hipMemcpy(&r, dout.get(), sizeof(double), hipMemcpyDeviceToHost));
     return r;
 }
 

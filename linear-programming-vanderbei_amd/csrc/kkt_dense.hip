@@ -590,7 +590,7 @@ __device__ __forceinline__ void df_wait(const int* prog, int v, int& seen) {
 // tile against the decision (win_solve) and the panel bails if one fails.
 struct DepState {
     const int* sign;       // node class of the block's columns (c0-relative)
-    int* lv;               // LDS: live mark per column, published with dv
+    int* lv;               // LDS: per column 1 live, 0 dropped, 2 kept with +-1e-8 (dependent), published with dv
     int* spec;             // LDS: the speculation failed (or met a NaN)
     int ndep;              // dependent pivots of this wave's window
 };
@@ -610,9 +610,12 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
                                            int h0, double tau, double (*Ct)[CTS], double (*Lr)[PC], double* dv,
                                            int* prog, DepState& ds) {
     double dk = lane_bcast(a[0], cw0);
-    int alive = 1;
+    int alive = 1, mark = 1;
     if (DEP) {
-        if (fabs(dk) <= tau * lane_bcast(dsc, cw0)) dep_pivot(a[0], cw0, lane, h0, dk, alive, ds);
+        if (fabs(dk) <= tau * lane_bcast(dsc, cw0)) {
+            dep_pivot(a[0], cw0, lane, h0, dk, alive, ds);
+            mark = alive ? 2 : 0;
+        }
     } else {
         tz_any |= fabs(dk) <= tau * lane_bcast(dsc, cw0);   // no short-circuit: no branch
     }
@@ -627,7 +630,7 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
             Ct[k][lane] = c;
             Lr[k][lane] = l;
             dv[k] = dk;                   // every lane stores the same value: no EXEC branch
-            if (DEP) ds.lv[k] = alive;
+            if (DEP) ds.lv[k] = mark;
             // the wavefront fence orders the reads of the row just written
             // (and the published count) after the writes for the compiler;
             // the LDS runs one wave's operations in issue order
@@ -644,7 +647,11 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
                 dk = lane_bcast(a[i + 1], k + 1);
                 if (DEP) {
                     alive = 1;
-                    if (fabs(dk) <= tau * lane_bcast(dsc, k + 1)) dep_pivot(a[i + 1], k + 1, lane, h0, dk, alive, ds);
+                    mark = 1;
+                    if (fabs(dk) <= tau * lane_bcast(dsc, k + 1)) {
+                        dep_pivot(a[i + 1], k + 1, lane, h0, dk, alive, ds);
+                        mark = alive ? 2 : 0;
+                    }
                 } else {
                     tz_any |= fabs(dk) <= tau * lane_bcast(dsc, k + 1);
                 }
@@ -665,27 +672,6 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
 template <bool DSC>
 __device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw, int lane, int cw0,
                                           double (*Ct)[CTS], double (*L)[PC], const int* prog) {
-#ifdef IPO_EXP_APPLY_EAGER
-    // experiment: each column applied as soon as it is published
-    {
-        int seen = 0;
-#pragma unroll 2
-        for (int i = 0; i < WIN; i++) {
-            const int k = kw + i;
-            df_wait(prog, i + 1, seen);
-            if (i + 1 == WIN) PANEL_STAMP(6);
-            const double l = L[k][lane];
-            const double ck = DSC ? Ct[k][lane] : 0.0;
-            double cc[WIN];
-            win_row(&Ct[k][cw0], cc);
-#pragma unroll
-            for (int q = 0; q < WIN; q++) a[q] = a[q] - l * cc[q];
-            if (DSC) dsc = dsc + fabs(l * ck);
-        }
-        PANEL_STAMP(7);
-        return;
-    }
-#endif
     // software-pipelined: step i + 1's LDS operands are read before step i's
     // arithmetic, so the read latency hides under the updates
     int seen = 0;
@@ -719,7 +705,10 @@ __device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw,
 // Window solve of the tile rows (half 1, wave w): solve_rows' form, step i
 // once half 0 has published pivot i of the window (wprog); publishes Lb.
 // DEP: a dropped column (lv 0) gives l = 0, and this tile's entries of it
-// must stay below 1e-2 (the speculation of dep_pivot), else the panel bails.
+// must stay below 1e-2 (the speculation of dep_pivot), else the panel bails;
+// below a dependent pivot kept from the block's rows (lv 2) a NaN in the tile
+// bails too (the reference's max fold over the whole column is order-
+// dependent with a NaN in it: the host repair decides it).
 template <bool FULL, bool DEP>
 __device__ __forceinline__ void win_solve(double (&a)[WIN], int cw0, int nc, bool rok, int lane, double (*Ct)[CTS],
                                           double (*Lb)[PC], const double* dv, const int* wprog, int* prog,
@@ -735,6 +724,7 @@ __device__ __forceinline__ void win_solve(double (&a)[WIN], int cw0, int nc, boo
                 if (__ballot(rok && !(fabs(a[i]) < 1.0e+6 * 1.0e-8)) != 0 && lane == 0) *ds.spec = 1;
                 l = 0.0;
             } else {
+                if (DEP && ds.lv[k] == 2 && __ballot(rok && a[i] != a[i]) != 0 && lane == 0) *ds.spec = 1;
                 l = rok ? a[i] / dv[k] : 0.0;
             }
             a[i] = l;
@@ -799,11 +789,28 @@ struct PanelLds {
 // of the host round trips and relaunches of a repair; the factor is bitwise
 // the repair path's (tests/test_gpu_panel.py).  dep == 2 (IPO_HIP_TAIL_SPEC=2,
 // tests only) treats every drop as contradicted, which exercises the restore.
-template <bool DEP = false>
+// SC (k_tail_run, the persistent dense tail): every access to what other
+// workgroups of the launch write or read (S, dg, dscale, the DEP saves) is
+// an sc1 access (kkt_kernels.h), and pre_wait() -- called once this
+// workgroup's own entries are loading, before block t - 1's operands are --
+// waits for the panels of step t - 1 (false: skip the item, the tail bailed).
+struct NoWait {
+    __device__ bool operator()() const { return true; }
+};
+// post(bailed): called by every thread once the handed-off results are
+// stored (the tile rows and, workgroup 0, D) -- k_tail_run signals step t
+// there, before workgroup 0's L11' / mark / |terms| stores, which only later
+// launches read -- or with true when the panel bails
+struct NoPost {
+    __device__ void operator()(bool) const {}
+};
+
+template <bool DEP = false, bool SC = false, class PreWait = NoWait, class Post = NoPost>
 __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __restrict__ fu_sup,
                                              const int* __restrict__ fu_j, int f0, const TailView& tv, int kb, int bid,
                                              PanelLds& S, double* wtail, bool pre = false,
-                                             const int* bailp = nullptr, int bt = 0, int dep = 0) {
+                                             const int* bailp = nullptr, int bt = 0, int dep = 0,
+                                             PreWait pre_wait = PreWait{}, Post post = Post{}) {
     // a bail flag of an earlier step (dense tail, see k_tail_pr): read first,
     // tested once this workgroup's operand loads are in flight
     const int bailed = bailp ? *bailp : 0;
@@ -849,11 +856,11 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
     for (int q = 0; q < WIN; q++) {
         const int c = cw0 + q;
         const bool ok = rok && c < nc && (h1 || c <= row);
-        const double t = panel[ok ? row + (size_t)c * ld : 0];
+        const double t = ld_h<SC>(panel + (ok ? row + (size_t)c * ld : 0));
         a[q] = ok ? t : 0.0;
     }
     // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
-    double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? p.dscale[c0 + lane] : 0.0;
+    double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? ld_h<SC>(p.dscale + c0 + lane) : 0.0;
     double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
     if (!pre && bailed && bailed - 1 < bt) return false;
     if (DEP && !fu_sup) {
@@ -864,12 +871,13 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
 #pragma unroll
             for (int q = 0; q < WIN; q++) {
                 const int c = cw0 + q;
-                if (c < nc) tv.W[row + (size_t)c * tv.nt] = a[q];
+                if (c < nc) st_h<SC>(tv.W + row + (size_t)c * tv.nt, a[q]);
             }
         }
-        if (j == 0 && !h1 && lane < nc && (lane >> 4) == w) tv.W[lane] = dsc;
+        if (j == 0 && !h1 && lane < nc && (lane >> 4) == w) st_h<SC>(tv.W + lane, dsc);
     }
     if (pre) {
+        if (!pre_wait()) return false;     // workgroup-uniform
         // dense tail, block column kb > 0: block kb - 1's update of this
         // workgroup's rows, k_tail_syrk's MFMA fragments and order; the
         // entries get old - acc and the pivots' |terms| old + sum_k |l w|,
@@ -886,11 +894,11 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
 #pragma unroll
             for (int u = 0; u < NU; u++) {
                 const int k = (tid + u * PNT) / TR;
-                const double x = Lcol[okd ? rd + (size_t)k * nt : 0];
-                const double y = Lcol[okj ? rj + (size_t)k * nt : 0];
+                const double x = ld_h<SC>(Lcol + (okd ? rd + (size_t)k * nt : 0));
+                const double y = ld_h<SC>(Lcol + (okj ? rj + (size_t)k * nt : 0));
                 // W = L21 D of block t - 1 formed here, the product its panel
                 // would have stored (l * d, the same operands: bitwise)
-                const double dk = p.dg[tv.tc + kp + k];
+                const double dk = ld_h<SC>(p.dg + tv.tc + kp + k);
                 vd[u] = okd ? x : 0.0;
                 vj[u] = okj ? y : 0.0;
                 vw[u] = okd ? x * dk : 0.0;
@@ -963,10 +971,7 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
     // half 1, wave w: the same updates on the tile rows, then solve window w.
     // Issue priority: the window chains (factor, solve) and the updates that
     // gate them over the rest.
-#ifndef IPO_EXP_NOH1
-#define IPO_EXP_NOH1 0
-#endif
-    if (w < nwin && (!h1 || (tile && !IPO_EXP_NOH1))) {
+    if (w < nwin && (!h1 || tile)) {
         int* const prog = S.prog + (h1 ? 4 : 0);
         double unused = 0.0;
         for (int t = 0; t < w; t++) {
@@ -1030,8 +1035,10 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
         if (tid == 0) {
             atomicOr(&p.flags[1], fu_sup ? 2 : DEP ? 4 | 16 : 4);   // bit: where it bailed (16: restore first)
             if (!fu_sup) atomicMax(&p.flags[2], kb + 1);   // the dense-tail block column
-            if (DEP && !fu_sup && j == 0) p.flags[3] = 0;   // workgroup 0 added no dependent pivots
+            if (DEP && !fu_sup && j == 0)                  // workgroup 0 added no dependent pivots
+                __hip_atomic_store(p.flags + 3, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        post(true);
         return false;
     }
     // the rows of L21 (half 1) and of R_s inside the first 64 rows (half 0 of
@@ -1041,24 +1048,26 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
 #pragma unroll
         for (int q = 0; q < WIN; q++) {
             const int c = cw0 + q;
-            if (c < nc) panel[row + (size_t)c * ld] = a[q];
+            if (c < nc) st_h<SC>(panel + row + (size_t)c * ld, a[q]);
         }
     }
-    if (!fu_sup && pre && j == 0 && !h1 && lane < nc && (lane >> 4) == w) p.dscale[c0 + lane] = dsc_pre;
+    if (j == 0 && tid < nc) { st_h<SC>(p.dg + c0 + tid, dv[tid]); p.live[c0 + tid] = DEP ? S.lv[tid] != 0 : 1; }
+    post(false);
+    if (!fu_sup && pre && j == 0 && !h1 && lane < nc && (lane >> 4) == w) st_h<SC>(p.dscale + c0 + lane, dsc_pre);
     if (j != 0) return false;
     // workgroup 0: L11' into the upper slot through an LDS transpose (Ct is
-    // free again), D, mark
+    // free again)
     if (!h1) {
 #pragma unroll
         for (int q = 0; q < WIN; q++) Ct[lane][cw0 + q] = a[q];
     }
     __syncthreads();
     for (int rr = 1 + wv; rr < nc; rr += PNT / 64)
-        if (lane < rr) panel[lane + (size_t)rr * ld] = Ct[rr][lane];
-    if (tid < nc) { p.dg[c0 + tid] = dv[tid]; p.live[c0 + tid] = DEP ? S.lv[tid] : 1; }
+        if (lane < rr) st_h<SC>(panel + lane + (size_t)rr * ld, Ct[rr][lane]);
     if (DEP && tid == 0) {
         if (S.ndep) atomicAdd(&p.flags[0], S.ndep);
-        if (!fu_sup) p.flags[3] = S.ndep;          // taken back by k_tail_restore if a later check fails
+        if (!fu_sup)                                // taken back by k_tail_restore if a later check fails
+            __hip_atomic_store(p.flags + 3, S.ndep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     PANEL_STAMP(13);
     return false;
@@ -1216,6 +1225,8 @@ __device__ __forceinline__ void syrk_tile512(const PlanView& p, const TailView& 
 // are loaded into registers while block b's are multiplied from LDS (two
 // blocks in flight measured no faster: tools/ubench_tail, round 4).  On a
 // diagonal tile the |terms| of every block go to dscale (one add).
+// SC: the persistent tail's hand-off form (sc1 loads and stores, panel_w_body).
+template <bool SC = false>
 __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView& tv, int bi, int bj, int b0, int b1,
                                               SyrkLds& L, const int* bailp = nullptr, int bt = 0) {
     // a bail flag of an earlier step (see k_tail_pr), read in the shadow of
@@ -1247,18 +1258,18 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
         if (k0 + PC <= nt) {
 #pragma unroll
             for (int u = 0; u < NU; u++) {
-                xx[u] = Lcol[offa[u]];
-                yy[u] = Lcol[offb[u]];
-                dd[u] = dgb[(tid + u * PNT) / TR];
+                xx[u] = ld_h<SC>(Lcol + offa[u]);
+                yy[u] = ld_h<SC>(Lcol + offb[u]);
+                dd[u] = ld_h<SC>(dgb + (tid + u * PNT) / TR);
             }
         } else {                       // the last, partial block column: columns clamped too
             const int kmax = nt - 1 - k0;
 #pragma unroll
             for (int u = 0; u < NU; u++) {
                 const int idx = tid + u * PNT, k = idx / TR, kc = min(k, kmax);
-                xx[u] = Lcol[offa[u] - (k - kc) * nt];
-                yy[u] = Lcol[offb[u] - (k - kc) * nt];
-                dd[u] = dgb[kc];
+                xx[u] = ld_h<SC>(Lcol + offa[u] - (k - kc) * nt);
+                yy[u] = ld_h<SC>(Lcol + offb[u] - (k - kc) * nt);
+                dd[u] = ld_h<SC>(dgb + kc);
             }
         }
     };
@@ -1272,17 +1283,18 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
     double as = 0.0;
     load(b0, rx, ry, rd);
     // the tile's own entries (no other workgroup of the launch touches
-    // them), read now so their latency hides under the products
-    double old[2][4];
+    // them), read now so their latency hides under the products; column-
+    // coalesced (wave wv holds columns wv, wv + 8, ..., lane = row: one
+    // 512-byte column segment per load), the products come to this layout
+    // through LDS at the end
+    double old[8];
+    const int rgl = bi * TR + lane;
 #pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int rr = wr + a * 16 + (lane >> 4) + 4 * i, cc = wc + (lane & 15);
-            const int rg = bi * TR + rr, cg = bj * TR + cc;
-            const bool ok = rg < nt && cg < nt && !(diag_tile && cc > rr);
-            old[a][i] = tv.S[ok ? rg + (size_t)cg * nt : 0];
-        }
+    for (int u = 0; u < 8; u++) {
+        const int cc = wv + 8 * u, cg = bj * TR + cc;
+        const bool ok = rgl < nt && cg < nt && !(diag_tile && cc > lane);
+        old[u] = ld_h<SC>(tv.S + (ok ? rgl + (size_t)cg * nt : 0));
+    }
     if (bailed && bailed - 1 < bt) return;
     // block b: operands from registers into LDS, block b + 1's loads into
     // the freed registers, then block b's MFMA steps
@@ -1308,15 +1320,21 @@ __device__ __forceinline__ void visit_tile512(const PlanView& p, const TailView&
         VISIT_STAMP(b - b0, 5);
     };
     for (int b = b0; b < b1; b++) step(b, rx, ry, rd);
+    // the products to [column][row] in LDS (free after the last step's barrier)
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int rr = wr + a * 16 + (lane >> 4) + 4 * i, cc = wc + (lane & 15);
-            const int rg = bi * TR + rr, cg = bj * TR + cc;
-            if (rg < nt && cg < nt && !(diag_tile && cc > rr)) tv.S[rg + (size_t)cg * nt] = old[a][i] - acc[a][i];
-        }
-    if (diag_tile && tid < TR && bi * TR + tid < nt) p.dscale[tv.tc + bi * TR + tid] += as;
+        for (int i = 0; i < 4; i++) L.As[wc + (lane & 15)][wr + a * 16 + (lane >> 4) + 4 * i] = acc[a][i];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const int cc = wv + 8 * u, cg = bj * TR + cc;
+        if (rgl < nt && cg < nt && !(diag_tile && cc > lane)) st_h<SC>(tv.S + rgl + (size_t)cg * nt, old[u] - L.As[cc][lane]);
+    }
+    if (diag_tile && tid < TR && bi * TR + tid < nt) {
+        double* dp = p.dscale + tv.tc + bi * TR + tid;
+        st_h<SC>(dp, ld_h<SC>(dp) + as);
+    }
 }
 
 constexpr size_t kTailStepLds0 = sizeof(PanelLds) > sizeof(SyrkLds) ? sizeof(PanelLds) : sizeof(SyrkLds);
@@ -1364,6 +1382,126 @@ k_tail_pr(PlanView p, TailView tv, int t, int gp, int vbase) {
     while (tile >= tv.ntb - c) { tile -= tv.ntb - c; c++; }
     const int b1 = visit_hi(t, c, tv.vk);
     visit_tile512(p, tv, c + tile, c, max(0, b1 - tv.vk), b1, *reinterpret_cast<SyrkLds*>(lds), p.flags + 2, t);
+}
+
+// ----------------------------------------- dense tail: one persistent launch
+// The look-ahead steps t0 .. ntb - 1 as work items of ONE launch
+// (tail_run_schedule): each workgroup draws one item from a ticket counter
+// when it starts (schedule order) and runs it to completion --
+//   panel (t, j): workgroup j of k_tail_pr's panel of step t (pre-update of
+//                 block t - 1 on its rows, then the windowed panel);
+//   visit:        one deferred trailing update of launch t (visit_tile512).
+// An item waits only on items with smaller tickets: every item of launch t
+// on the panels of step t - 1 (what the launch boundary gave k_tail_pr), a
+// panel on the visits of its two tiles (per-tile sequence counters vseq), a
+// visit on the chunks of its tile before it.  So no launch gap separates the
+// steps, a panel starts as soon as its own inputs are final, its entries
+// load before it waits for step t - 1, and the grid drains on any share of
+// the CUs (a ticket is only drawn by a running workgroup).  Hand-offs: the
+// data sc1 both ways, every storing wave's vmcnt(0) and a barrier before one
+// lane's agent-scope add (MI355X_MICROARCH.md's first row).  A panel that
+// bails (flags[2]) still counts itself, so its step's visits complete as in
+// k_tail_pr; every item of a later launch reads the flag after its wait and
+// is skipped without counting, and the host repair resumes the run from
+// step tb + 1 with the counters as they are.
+__host__ __device__ __forceinline__ int tail_gp(int nt, int t) { return max(1, (nt - t * PC + TR - 1) / TR - 1); }
+
+// A panel workgroup that bails adds 1 + kRunBail to pdone[t]: a waiter on
+// the panels of step t learns both in one load.
+constexpr int kRunBail = 1 << 16;
+
+// one lane polls until pdone counter c0 (null: none) reaches v0 and vseq
+// counter c1 (null: none) reaches v1; the workgroup joins a barrier and gets
+// false for "skip the item": step t - 1 bailed (c0's bail bit), or, while a
+// counter is short, a panel of a launch before t has bailed (flags[2]: then
+// the counter may never complete)
+__device__ __forceinline__ bool run_wait(const int* c0, int v0, const int* c1, int v1, const int* bailp, int t,
+                                         int* sh) {
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        for (;;) {
+            const int x0 = c0 ? sc1_load_int(c0) : v0;
+            const int x1 = c1 ? sc1_load_int(c1) : v1;
+            if ((x0 & (kRunBail - 1)) >= v0 && x1 >= v1) {
+                ok = x0 < kRunBail;
+                break;
+            }
+            const int b = sc1_load_int(bailp);
+            if (b && b - 1 < t) {
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *sh = ok;
+    }
+    __syncthreads();
+    return *sh != 0;
+}
+
+__device__ __forceinline__ void run_signal(int* cnt, int v = 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(PNT)
+k_tail_run(PlanView p, TailView tv, TailRun rc) {
+    __shared__ __attribute__((aligned(16))) char lds[kTailStepLds];
+    // the two waits of a panel item report through different words: no
+    // barrier separates a slow wave's read of the first from the second's write
+    __shared__ int sh_item, sh_ok, sh_ok2;
+    const int ntb = tv.ntb;
+    const int* bailp = p.flags + 2;
+    // one item per workgroup, drawn when the workgroup starts (a loop over
+    // items in a persistent grid kept more registers live: 256 VGPRs and
+    // spills against k_tail_pr's 218; the dispatcher starts a workgroup as
+    // soon as a CU frees, so the items still flow in ticket order)
+    if (threadIdx.x == 0) sh_item = __hip_atomic_fetch_add(rc.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int it = sh_item;
+    if (it >= rc.n) return;
+    const uint2 rec = rc.items[it];
+    const int t = rec.y & 0xff, q = (rec.y >> 8) & 0xff;
+    unsigned long long* tr = rc.trace ? rc.trace + 4 * (size_t)it : nullptr;
+    if (tr && threadIdx.x == 0) {
+        tr[0] = __builtin_amdgcn_s_memrealtime();
+        tr[3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));   // HW_REG_XCC_ID bits 0..3
+    }
+    if (rec.y >> 31) {
+        // panel (t, j): column t's visits done for the diagonal tile and tile t + j + 1
+        const int j = rec.x;
+        const int* vd = q ? rc.vseq + t * ntb + t : nullptr;
+        const int* vt = q && t + j + 1 < ntb ? rc.vseq + (t + j + 1) * ntb + t : nullptr;
+        if (!run_wait(vd, q, vt, q, bailp, t, &sh_ok)) return;
+        // (the first step of a run resumed after a repair waits for nothing
+        // before it: the repair's launches came first)
+        auto pw = [&]() {
+            const bool go = t == rc.t0 || run_wait(rc.pdone + t - 1, tail_gp(tv.nt, t - 1), nullptr, 0, bailp, t, &sh_ok2);
+            if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+            return go;
+        };
+        auto post = [&](bool bailed) { run_signal(rc.pdone + t, bailed ? 1 + kRunBail : 1); };
+        if (tr && threadIdx.x == 0 && t == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+        PanelLds& S = *reinterpret_cast<PanelLds*>(lds);
+        if (panel_w_body<false, true>(p, nullptr, nullptr, 0, tv, t, j, S, nullptr, t > 0, nullptr, t, tv.dep, pw,
+                                      post)) {
+            __syncthreads();           // every wave has read the first pass's verdict
+            panel_w_body<true, true>(p, nullptr, nullptr, 0, tv, t, j, S, nullptr, t > 0, nullptr, t, tv.dep, NoWait{},
+                                     post);
+        }
+    } else {
+        // visit: chunk q of tile (bi, c), once the panels of step t - 1 are done
+        const int bi = rec.x & 255, c = (rec.x >> 8) & 255, b0 = (rec.x >> 16) & 255, b1 = rec.x >> 24;
+        int* vs = rc.vseq + bi * ntb + c;
+        if (!run_wait(t > rc.t0 ? rc.pdone + t - 1 : nullptr, t > rc.t0 ? tail_gp(tv.nt, t - 1) : 0, q ? vs : nullptr,
+                      q, bailp, t, &sh_ok))
+            return;
+        if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+        visit_tile512<true>(p, tv, bi, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
+        run_signal(vs);
+    }
+    if (tr && threadIdx.x == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
 }
 
 // A DEP pass of block column kb failed its check in some workgroup (flags[1]
@@ -1628,6 +1766,81 @@ std::vector<unsigned> tail_visit_schedule(int ntb, int nt, int K, int cap, std::
     }
     ptr[ntb] = static_cast<int>(out.size());
     return out;
+}
+
+// Chunks of column c of the persistent tail, latest first: blocks [0, c - 1)
+// (block c - 1 is its panel's pre-update), the latest L blocks one chunk (a
+// visit that must finish within one step: it needs block c - 2, final at the
+// end of step c - 2, before panel c), then K at a time downwards.
+static std::vector<std::pair<int, int>> run_chunks(int c, int K, int L) {
+    std::vector<std::pair<int, int>> v;
+    int b1 = c - 1;
+    for (int k = 0; b1 > 0; k++) {
+        const int b0 = std::max(0, b1 - (k == 0 ? L : K));
+        v.push_back({b0, b1});
+        b1 = b0;
+    }
+    return v;
+}
+
+std::vector<uint2> tail_run_schedule(int ntb, int nt, int K, int L, int cap, std::vector<int>& ptr) {
+    struct V { int bi, c, b0, b1, q; };
+    std::vector<std::vector<V>> Ls(ntb);
+    std::vector<int> tot(ntb, 0), nch(ntb, 0);
+    for (int c = 0; c < ntb; c++) {
+        const std::vector<std::pair<int, int>> ch = run_chunks(c, K, L);
+        nch[c] = static_cast<int>(ch.size());
+        // the k-th chunk from the top in launch c - 1 - k (its blocks < b1 <= c - 1 - k)
+        for (int k = 0; k < nch[c]; k++)
+            for (int bi = c; bi < ntb; bi++) Ls[c - 1 - k].push_back({bi, c, ch[k].first, ch[k].second, nch[c] - 1 - k});
+    }
+    for (int t = 0; t < ntb; t++) tot[t] = tail_gp(nt, t) + static_cast<int>(Ls[t].size());
+    // launches over `cap` items: first chunks (q = 0) into the latest earlier
+    // launch with room where they are ready (launch >= b1), as tail_visit_schedule
+    for (int t = ntb - 1; t > 1; t--) {
+        while (tot[t] > cap) {
+            int best = -1;
+            for (int i = 0; i < static_cast<int>(Ls[t].size()); i++) {
+                const V& v = Ls[t][i];
+                if (v.q != 0) continue;
+                if (best < 0 || v.b1 < Ls[t][best].b1 || (v.b1 == Ls[t][best].b1 && v.c > Ls[t][best].c)) best = i;
+            }
+            if (best < 0) break;
+            int dst = -1;
+            for (int u = t - 1; u >= std::max(1, Ls[t][best].b1); u--)
+                if (tot[u] < cap) { dst = u; break; }
+            if (dst < 0) break;
+            Ls[dst].push_back(Ls[t][best]);
+            tot[dst]++;
+            Ls[t].erase(Ls[t].begin() + best);
+            tot[t]--;
+        }
+    }
+    std::vector<uint2> out;
+    ptr.assign(ntb + 1, 0);
+    for (int t = 0; t < ntb; t++) {
+        ptr[t] = static_cast<int>(out.size());
+        for (int j = 0; j < tail_gp(nt, t); j++)
+            out.push_back(make_uint2(static_cast<unsigned>(j), static_cast<unsigned>(t) |
+                                                                  static_cast<unsigned>(nch[t]) << 8 | 1u << 31));
+        // column t + 1's visits first (its panel waits for them), then by column
+        std::vector<V>& vv = Ls[t];
+        std::stable_sort(vv.begin(), vv.end(), [t](const V& a, const V& b) {
+            const bool ua = a.c == t + 1, ub = b.c == t + 1;
+            if (ua != ub) return ua;
+            return a.c != b.c ? a.c < b.c : a.bi < b.bi;
+        });
+        for (const V& v : vv)
+            out.push_back(make_uint2(static_cast<unsigned>(v.bi) | static_cast<unsigned>(v.c) << 8 |
+                                         static_cast<unsigned>(v.b0) << 16 | static_cast<unsigned>(v.b1) << 24,
+                                     static_cast<unsigned>(t) | static_cast<unsigned>(v.q) << 8));
+    }
+    ptr[ntb] = static_cast<int>(out.size());
+    return out;
+}
+
+void launch_tail_run(const PlanView& pv, const TailView& tv, const TailRun& rc, hipStream_t s) {
+    if (rc.n > 0) hipLaunchKernelGGL(k_tail_run, dim3(rc.n), dim3(PNT), 0, s, pv, tv, rc);
 }
 
 void tail_visit_work(int ntb, int nt, int K, double& flops, double& bytes) {

@@ -24,6 +24,9 @@ namespace ipo {
 // Blocks per visit of the look-ahead dense tail (kkt_dense.hip, visit_hi):
 // IPO_HIP_VISIT_BLOCKS overrides.
 constexpr int kTailVisitBlocks = 6;     // measured on dfl001's tail: 4 -> 2.43 ms, 6 -> 2.26, 8 -> 2.55
+// the persistent tail's latest chunk per column (tail_run_schedule): it must
+// finish within one step (IPO_HIP_VISIT_LATEST overrides)
+constexpr int kTailVisitLatest = 2;
 struct TailView {
     double* S;
     int nt, ntb, tc;
@@ -38,6 +41,23 @@ struct TailView {
     const unsigned* vlist = nullptr;
     const int* vptr = nullptr;
     int sdep = 1;     // dependent pivots inside the sparse fused panels (k_panel_w, k_panel_s; 0: redo the factor)
+};
+
+// The look-ahead dense tail as ONE persistent launch (k_tail_run): the
+// items of launches [t0, ntb) of tail_run_schedule, drawn by ticket.
+// Counters: pdone[t] = panel workgroups of step t done, vseq[bi * ntb + c] =
+// visits of tile (bi, c) done -- both zeroed before a factorisation's first
+// run and kept for a run resumed after a repair; ticket zeroed before every run.
+struct TailRun {
+    const uint2* items;   // the run's first item (launch t0's)
+    int n;                // items in the run
+    int t0;               // its first launch
+    int* ticket;
+    int* pdone;
+    int* vseq;
+    // developer trace (tools/ubench_tail UB_TRACE): per item {drawn, ready,
+    // done} in s_memrealtime ticks (100 MHz) and the workgroup's XCC id; null: off
+    unsigned long long* trace = nullptr;
 };
 
 // Device-time phases of the KKT core (timing mode), with the algorithmic
@@ -269,8 +289,8 @@ class KktDevice {
     int chain_epoch_ = 0;      // the chains' launch epoch (one per launch, never reused)
     int visit_blocks_ = kTailVisitBlocks;   // TailView::vk (IPO_HIP_VISIT_BLOCKS)
     double epsdiag_cap_ = 0.0;     // IPO_HIP_EPSDIAG_MAX (diagnostics; 0: the reference's unbounded growth)
-    int tail_spec_ = 1;
-    int sparse_dep_ = 1;           // TailView::sdep (IPO_HIP_SPARSE_DEP)            // TailView::dep when the host repair backs it (IPO_HIP_TAIL_SPEC: 0 off, 2 tests)
+    int tail_spec_ = 1;            // TailView::dep when the host repair backs it (IPO_HIP_TAIL_SPEC: 0 off, 2 tests)
+    int sparse_dep_ = 1;           // TailView::sdep (IPO_HIP_SPARSE_DEP)
     bool chain_pairs_ = false; // dense-tail chains with two blocks per workgroup (k_tail_fwd_pair / _bwd_pair)
     bool chain_lead_ = false;  // forward dense-tail sweep by one lead workgroup + helpers (k_tail_fwd_lead)
     DevBuf<int> dtail_task_ptr_, dtail_kslot_, dtail_kslot_ptr_;
@@ -278,6 +298,13 @@ class KktDevice {
     long long lead_ticket_next_ = 0;
     DevBuf<unsigned> dvisit_list_;     // TailView::vlist (tail_visit_schedule; IPO_HIP_VISIT_SCHED=0: none)
     std::vector<int> visit_ptr_;       // TailView::vptr
+    // the dense tail as one persistent launch (k_tail_run; IPO_HIP_TAIL_RUN=0: one launch per step)
+    bool tail_run_ = false;
+    DevBuf<uint2> drun_items_;         // tail_run_schedule
+    std::vector<int> run_ptr_;         // first item of each launch
+    DevBuf<int> drun_cnt_;             // ticket, pdone[ntb], vseq[ntb * ntb]
+    // the run of launches [t0, ntb) (reset: a factorisation's first run, counters zeroed)
+    void launch_tail_from(int t0, bool reset);
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;
     DevBuf<double> dDepSt_;        // k_tail_dep's block state and per-tile maxima

@@ -44,24 +44,6 @@ constexpr int TR = kTileRows;     // 64
 constexpr int PC = kPanelCols;    // 64
 constexpr int NT = 256;           // threads per workgroup
 
-// sc1 (agent-scope relaxed atomic) accesses: they bypass the CU's L1, the
-// hand-off form of MI355X_MICROARCH.md for data one workgroup passes to
-// another inside a launch
-__device__ __forceinline__ void sc1_store(double* p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double sc1_load(const double* p) {
-    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// a handed-off value (SC) or a plain one
-template <bool SC>
-__device__ __forceinline__ double ld_h(const double* p) {
-    if constexpr (SC) return sc1_load(p);
-    else return *p;
-}
-
-
-
 // ---------------------------------------------------------------- assembly
 __global__ void __launch_bounds__(NT)
 k_assemble_A(int nz, const double* __restrict__ A, const int64_t* __restrict__ amap, double* __restrict__ Lx) {
@@ -997,11 +979,7 @@ __device__ void fwd_diag(const PlanView& p, int s, const int* __restrict__ yrow_
     // part q sums the entries q, q + P, ... of the row's list in list order
     // (sixteen loads in flight), then a fixed xor-butterfly combines the P
     // partial sums -- the same order in every kernel that calls this.
-#ifdef IPO_FWD_P4
-    const int P = 4;
-#else
     const int P = nc > 32 ? 4 : nc > 16 ? 8 : nc > 8 ? 16 : nc > 4 ? 32 : 64;
-#endif
     // sptr: the rows' list bounds yrow_ptr[c0 .. c0 + nc], staged in LDS by the caller
     const int ebase = sidx ? (sptr ? sptr[0] : yrow_ptr[c0]) : 0;
     // list index e: the staged LDS copy or the global list (no pointer
@@ -3635,6 +3613,24 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             dvisit_list_.upload(vl, s);
             IPO_HIP_CHECK(hipStreamSynchronize(s));   // vl is a local
         }
+        // the persistent run (k_tail_run, default; its bails end in the same
+        // state as the per-step launches', so the repair and the sharded
+        // solve's per-phase redo are unchanged); the latest chunk of each
+        // column IPO_HIP_VISIT_LATEST blocks
+        const char* tr = std::getenv("IPO_HIP_TAIL_RUN");
+        tail_run_ = !(tr && std::atoi(tr) == 0);
+        if (tail_run_) {
+            int dev = 0, cus = 0;
+            IPO_HIP_CHECK(hipGetDevice(&dev));
+            IPO_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            const char* vl = std::getenv("IPO_HIP_VISIT_LATEST");
+            const int latest = vl ? std::max(1, std::atoi(vl)) : kTailVisitLatest;
+            const std::vector<uint2> items =
+                tail_run_schedule(plan_.ntb, plan_.nt, visit_blocks_, latest, cus, run_ptr_);
+            drun_items_.upload(items, s);
+            drun_cnt_.alloc(1 + plan_.ntb + static_cast<size_t>(plan_.ntb) * plan_.ntb);
+            IPO_HIP_CHECK(hipStreamSynchronize(s));   // items is a local
+        }
     }
     if (const char* ts = std::getenv("IPO_HIP_TAIL_SPEC")) tail_spec_ = std::atoi(ts);
     if (const char* sd = std::getenv("IPO_HIP_SPARSE_DEP")) sparse_dep_ = std::atoi(sd);
@@ -4043,7 +4039,9 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
         // shards: S = sum of every shard's assembled + gathered tail (exchange.h)
         xsum(tv.S, static_cast<size_t>(plan_.nt) * plan_.nt, RedOp::Sum);
         xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
-        if (tail_fused) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
+        if (tail_fused && tail_run_) {     // one persistent launch (kkt_dense.hip, k_tail_run)
+            launch_tail_from(0, true);
+        } else if (tail_fused) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
             // one event pair around the steps (a pair per launch added its
             // own ~2.5 us to every launch's time: the phase's average launch
             // would not be the kernel's)
@@ -4128,6 +4126,27 @@ bool KktDevice::finish_pass(bool fused) {
     return !(fused && bail);
 }
 
+// The dense tail's look-ahead steps [t0, ntb) as one persistent launch
+// (k_tail_run).  reset: the factorisation's first run (every counter
+// zeroed); a run resumed by repair_tail keeps pdone / vseq, which hold
+// exactly the items of launches <= tb (later items were skipped uncounted).
+void KktDevice::launch_tail_from(int t0, bool reset) {
+    hipStream_t s = stream_;
+    const PlanView pv = IPO_VIEW();
+    const size_t ncnt = reset ? drun_cnt_.size() : 1;
+    IPO_HIP_CHECK(hipMemsetAsync(drun_cnt_.get(), 0, ncnt * sizeof(int), s));
+    TailRun rc;
+    rc.items = drun_items_.get() + run_ptr_[t0];
+    rc.n = run_ptr_[plan_.ntb] - run_ptr_[t0];
+    rc.t0 = t0;
+    rc.ticket = drun_cnt_.get();
+    rc.pdone = drun_cnt_.get() + 1;
+    rc.vseq = drun_cnt_.get() + 1 + plan_.ntb;
+    ph_begin(s);
+    launch_tail_run(pv, tail_view(), rc, s);
+    ph_end(kPhTail, rc.n > 0, s);
+}
+
 // The look-ahead dense tail bailed at block column tb (a pivot failed the
 // zero test; launches after it did nothing): the sparse factor and block
 // columns < tb stand, column tb holds the updates of blocks <= tb - 2 (its
@@ -4169,9 +4188,13 @@ void KktDevice::repair_tail() {
             tm_.tail_dep_rounds += kDepBatch;
             if (hFlags_[6]) break;
         }
-        ph_begin(s);
-        for (int t = tb + 1; t < plan_.ntb; t++) launch_tail_step(pv, tail_view(), t, s);
-        ph_end(kPhTail, plan_.ntb - tb - 1, s);
+        if (tail_run_) {
+            launch_tail_from(tb + 1, false);
+        } else {
+            ph_begin(s);
+            for (int t = tb + 1; t < plan_.ntb; t++) launch_tail_step(pv, tail_view(), t, s);
+            ph_end(kPhTail, plan_.ntb - tb - 1, s);
+        }
         if (finish_pass(true)) break;
         if ((hFlags_[1] & ~16) != 4 || hFlags_[4] - 1 <= tb)   // cannot happen: a later tail column or nothing
             throw std::runtime_error("kkt: dense-tail repair did not advance");

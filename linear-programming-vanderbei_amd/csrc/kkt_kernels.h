@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "kkt_device.h"
 #include "kkt_plan.h"
@@ -50,6 +51,31 @@ static __device__ __forceinline__ int xcd_chunk(int b, int G) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
 }
 
+// sc1 (agent-scope relaxed atomic) accesses: they bypass the CU's L1, the
+// hand-off form of MI355X_MICROARCH.md (stores all sc1, loads all sc1, one
+// lane signals after every storing wave's vmcnt(0) and a barrier) for data
+// one workgroup passes to another inside a launch
+static __device__ __forceinline__ void sc1_store(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static __device__ __forceinline__ double sc1_load(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+static __device__ __forceinline__ int sc1_load_int(const int* p) {
+    return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a handed-off value (SC) or a plain one
+template <bool SC>
+static __device__ __forceinline__ double ld_h(const double* p) {
+    if constexpr (SC) return sc1_load(p);
+    else return *p;
+}
+template <bool SC>
+static __device__ __forceinline__ void st_h(double* p, double v) {
+    if constexpr (SC) sc1_store(p, v);
+    else *p = v;
+}
+
 // value of v in lane j (j wave-uniform), via two v_readlane_b32
 static __device__ __forceinline__ double lane_bcast(double v, int j) {
     const long long b = __double_as_longlong(v);
@@ -83,6 +109,13 @@ int tail_visit_tiles(int ntb, int t, int K);
 // tiles' first chunks moved into earlier launches where a launch would
 // overflow.  Returns the list (TailView::vlist layout) and ptr[0..ntb].
 std::vector<unsigned> tail_visit_schedule(int ntb, int nt, int K, int cap, std::vector<int>& ptr);
+// Items per launch t (ptr[t] .. ptr[t + 1]): panel workgroups (j, t | chunks
+// of column t << 8 | 1 << 31), then visits (bi | c << 8 | b0 << 16 | b1 << 24,
+// t | chunk index << 8), column t + 1's first.  Column c's chunks: the latest
+// L blocks before c - 1 in launch c - 1, then K at a time in launches c - 2,
+// ...; launches over `cap` items move first chunks earlier.
+std::vector<uint2> tail_run_schedule(int ntb, int nt, int K, int L, int cap, std::vector<int>& ptr);
+void launch_tail_run(const PlanView& pv, const TailView& tv, const TailRun& rc, hipStream_t s);
 // algorithmic flops / bytes of every visit of one factorisation
 void tail_visit_work(int ntb, int nt, int K, double& flops, double& bytes);
 // Repair path, block column kb of the dense tail with the dependent-pivot

@@ -13,6 +13,8 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <mutex>
 #include <stdexcept>
 #include <thread>
 
@@ -66,13 +68,22 @@ class StepPool {
         gen_.fetch_add(1, std::memory_order_release);
         for (auto& t : th_) t.join();
     }
+    // An exception thrown by fn on any thread (bad_alloc in a clique step)
+    // is kept, the step still completes on every thread, and the first one
+    // is rethrown here after the join, so it reaches the C API's catch.
     template <class F>
     void run(F&& f) {
         fn_ = std::ref(f);
+        err_ = nullptr;
         done_.store(0, std::memory_order_relaxed);
         gen_.fetch_add(1, std::memory_order_release);
-        f(0);
+        try {
+            f(0);
+        } catch (...) {
+            keep(std::current_exception());
+        }
         while (done_.load(std::memory_order_acquire) != static_cast<int>(th_.size())) relax();
+        if (err_) std::rethrow_exception(err_);
     }
 
   private:
@@ -87,12 +98,22 @@ class StepPool {
             }
             seen = g;
             if (stop_.load(std::memory_order_relaxed)) return;
-            fn_(tid);
+            try {
+                fn_(tid);
+            } catch (...) {
+                keep(std::current_exception());
+            }
             done_.fetch_add(1, std::memory_order_release);
         }
     }
+    void keep(std::exception_ptr e) {
+        std::lock_guard<std::mutex> g(err_mu_);
+        if (!err_) err_ = e;
+    }
     std::vector<std::thread> th_;
     std::function<void(int)> fn_;
+    std::mutex err_mu_;
+    std::exception_ptr err_;
     std::atomic<unsigned> gen_{0};
     std::atomic<int> done_{0};
     std::atomic<bool> stop_{false};

@@ -208,6 +208,31 @@ def test_tail_visit_schedule_bitwise(name):
     assert _solve_env("IPO_HIP_VISIT_XCD", "0", name) == _solve_env("IPO_HIP_VISIT_XCD", "1", name)
 
 
+@pytest.mark.parametrize("name", ["dfl001", "greenbea", "25fv47"])
+def test_tail_run_bitwise(name):
+    """The dense tail as one persistent launch (k_tail_run, default: ticketed
+    panel and visit items, per-step and per-tile counters) against one launch
+    per look-ahead step (IPO_HIP_TAIL_RUN=0), both with the per-step launches'
+    visit chunks (IPO_HIP_VISIT_LATEST=6: every tile receives the same chunks
+    of blocks in the same order): identical HSD solves (trace and final
+    values) -- the hand-offs inside the launch deliver what the launch
+    boundaries did.  dfl001's solve also takes the run's bail and resumed-run
+    path (dependent pivots the in-panel pass leaves to the host)."""
+    six = (("IPO_HIP_VISIT_LATEST", "6"),)
+    assert _solve_env("IPO_HIP_TAIL_RUN", "0", name, extra=six) == _solve_env("IPO_HIP_TAIL_RUN", "1", name, extra=six)
+
+
+def test_tail_run_resume_bitwise():
+    """The persistent run's bail and resume (IPO_HIP_TAIL_SPEC=0: every
+    dependent pivot of the tail goes to the host repair, which resumes the
+    run after the bailed block column with its counters kept) against the
+    per-step launches' repair: identical dfl001 HSD solves."""
+    ext = (("IPO_HIP_VISIT_LATEST", "6"), ("IPO_HIP_TAIL_SPEC", "0"))
+    a = _solve_env("IPO_HIP_TAIL_RUN", "0", extra=ext)
+    b = _solve_env("IPO_HIP_TAIL_RUN", "1", extra=ext)
+    assert a == b
+
+
 def test_sparse_dependent_pivots_bitwise():
     """Whole dfl001 HSD solves with the sparse panels' dependent pivots
     resolved in the kernels (IPO_HIP_SPARSE_DEP=1) and by redoing the

@@ -15,6 +15,7 @@ EXE = os.path.join(REPO, "linear-programming-vanderbei_amd", "bin", "ipo_hip")
 SKIP = set(os.environ.get("SWEEP_SKIP", "").split(","))
 SAVE = os.environ.get("SWEEP_SAVE")          # directory for the full traces (name.method.txt)
 METHOD = os.environ.get("SWEEP_METHOD", "hsd")
+ONLY = set(filter(None, os.environ.get("SWEEP_ONLY", "").split(",")))   # a subset of the problems
 
 
 def iters_and_last(text):
@@ -24,7 +25,7 @@ def iters_and_last(text):
 
 
 for name in available_problems():
-    if name in SKIP:
+    if name in SKIP or (ONLY and name not in ONLY):
         continue
     t0 = time.time()
     try:

@@ -61,6 +61,45 @@ int main(int argc, char** argv) {
         for (int t = 0; t < ntb; t++) std::printf(" %d", std::max(1, (nt - t * 64 + 63) / 64 - 1) + vptr[t + 1] - vptr[t]);
         std::printf("\n");
     }
+    // the persistent run (UB_RUN=1, k_tail_run, latest chunk UB_LATEST blocks):
+    // timed as one launch, its pivots and factor compared with the per-step
+    // launches' (another grouping of the visits' sums: not bitwise)
+    const bool run = std::getenv("UB_RUN") && std::atoi(std::getenv("UB_RUN")) != 0;
+    std::vector<int> rptr;
+    uint2* ditems = nullptr;
+    int* dcnt = nullptr;
+    int cus_run = 0;
+    if (run) {
+        CK(hipDeviceGetAttribute(&cus_run, hipDeviceAttributeMultiprocessorCount, 0));
+        const int latest = std::getenv("UB_LATEST") ? std::atoi(std::getenv("UB_LATEST")) : ipo::kTailVisitLatest;
+        const std::vector<uint2> items = ipo::tail_run_schedule(ntb, nt, tv.vk, latest, cus_run, rptr);
+        CK(hipMalloc(&ditems, items.size() * sizeof(uint2)));
+        CK(hipMemcpy(ditems, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice));
+        CK(hipMalloc(&dcnt, (1 + ntb + ntb * ntb) * sizeof(int)));
+        std::printf("persistent run: %zu items, latest chunk %d, items per launch", items.size(), latest);
+        for (int t = 0; t < ntb; t++) std::printf(" %d", rptr[t + 1] - rptr[t]);
+        std::printf("\n");
+    }
+    // UB_TRACE=file: the last timed run's per-item trace (k_tail_run's
+    // {drawn, ready, done, xcc}, 100 MHz ticks) with each item's record, binary
+    unsigned long long* dtrace = nullptr;
+    const char* trace_file = std::getenv("UB_TRACE");
+    if (run && trace_file) CK(hipMalloc(&dtrace, (size_t)rptr[ntb] * 4 * sizeof(unsigned long long)));
+    auto run_once = [&](hipStream_t st) {
+        CK(hipMemsetAsync(dcnt, 0, (1 + ntb + ntb * ntb) * sizeof(int), st));
+        ipo::TailRun rc{ditems, rptr[ntb], 0, dcnt, dcnt + 1, dcnt + 1 + ntb, dtrace};
+        ipo::launch_tail_run(pv, tv, rc, st);
+    };
+    std::vector<double> g_step;
+    if (run) {      // the per-step launches' pivots and factor, for the comparison
+        CK(hipMemcpy(dS, dS0, bytes, hipMemcpyDeviceToDevice));
+        CK(hipMemcpy(ddsc, ddsc0, nt * 8, hipMemcpyDeviceToDevice));
+        CK(hipMemset(dflags, 0, 16));
+        for (int t = 0; t < ntb; t++) ipo::launch_tail_step(pv, tv, t, 0);
+        CK(hipDeviceSynchronize());
+        g_step.resize(nt);
+        CK(hipMemcpy(g_step.data(), ddg, nt * 8, hipMemcpyDeviceToHost));
+    }
     std::vector<hipEvent_t> ev(ntb + 1);
     for (auto& e : ev) CK(hipEventCreate(&e));
     std::vector<double> step_us(ntb, 0.0);
@@ -72,16 +111,21 @@ int main(int argc, char** argv) {
         CK(hipMemset(dflags, 0, 16));
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(ev[0], 0));
-        for (int t = 0; t < ntb; t++) {
-            ipo::launch_tail_step(pv, tv, t, 0);
-            CK(hipEventRecord(ev[t + 1], 0));
+        if (run) {
+            run_once(0);
+            CK(hipEventRecord(ev[ntb], 0));
+        } else {
+            for (int t = 0; t < ntb; t++) {
+                ipo::launch_tail_step(pv, tv, t, 0);
+                CK(hipEventRecord(ev[t + 1], 0));
+            }
         }
         CK(hipEventSynchronize(ev[ntb]));
         if (r == 0) continue;       // warm-up
         float ms = 0;
         CK(hipEventElapsedTime(&ms, ev[0], ev[ntb]));
         total += ms;
-        for (int t = 0; t < ntb; t++) {
+        for (int t = 0; t < ntb && !run; t++) {
             CK(hipEventElapsedTime(&ms, ev[t], ev[t + 1]));
             step_us[t] += 1e3 * ms;
         }
@@ -95,6 +139,31 @@ int main(int argc, char** argv) {
     std::printf("per step (us):");
     for (int t = 0; t < ntb; t++) std::printf("%s%.1f", t % 16 ? " " : "\n  ", step_us[t] / reps);
     std::printf("\n");
+    if (run) {
+        std::vector<double> g(nt);
+        CK(hipMemcpy(g.data(), ddg, nt * 8, hipMemcpyDeviceToHost));
+        double mx = 0;
+        int same = 0;
+        for (int k = 0; k < nt; k++) {
+            mx = std::fmax(mx, std::fabs(g[k] - g_step[k]) / std::fabs(g_step[k]));
+            same += g[k] == g_step[k];
+        }
+        std::printf("persistent run vs per-step launches: pivots max relative difference %.2e, %d of %d bitwise\n", mx,
+                    same, nt);
+        if (dtrace) {
+            const size_t ni = rptr[ntb];
+            std::vector<unsigned long long> tr(ni * 4);
+            std::vector<uint2> items(ni);
+            CK(hipMemcpy(tr.data(), dtrace, tr.size() * 8, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(items.data(), ditems, ni * sizeof(uint2), hipMemcpyDeviceToHost));
+            FILE* f = std::fopen(trace_file, "wb");
+            const int hdr[2] = {ntb, (int)ni};
+            std::fwrite(hdr, 4, 2, f);
+            std::fwrite(items.data(), sizeof(uint2), ni, f);
+            std::fwrite(tr.data(), 8, tr.size(), f);
+            std::fclose(f);
+        }
+    }
     if (nt <= 2048) {       // host LDL' (right-looking, the reference form l = a / d, a -= l (l_c d))
         std::vector<double> A = S, d(nt);
         for (int k = 0; k < nt; k++) {
