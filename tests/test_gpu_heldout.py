@@ -85,9 +85,11 @@ def test_heldout_scaled_within_envelope(name):
         else:
             targets, tol = [], 0.0
         if v[0]["status"] != "optimal solution" and name in FALSE_OPTIMAL:
-            # documented: HSD's mu test ends the solve away from feasibility
+            # documented: HSD's mu test ends the solve away from feasibility,
+            # where the reference's own order stops at the iteration limit --
+            # a status only another order ends with; kept visible as xfail
             assert r["stats"]["final_pinf"] > 1e-6 or r["stats"]["final_dinf"] > 1e-6, (name, FALSE_OPTIMAL[name])
-            return
+            pytest.xfail(FALSE_OPTIMAL[name])
         assert targets, f"{name}: GPU 'optimal solution' with no optimum to hold it to"
         ok = [all(abs(g - t) <= tol * max(1.0, abs(t)) for g, t in zip(got, tg)) for tg in targets]
         assert any(ok), (name, got, targets, tol)

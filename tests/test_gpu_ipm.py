@@ -6,8 +6,11 @@ with the oracle restatement.  Stated tolerance (north star):
   * same final status;
   * iteration count within +-1 of the reference;
   * final primal and dual objective within 1e-6 relative (hsd: of the
-    golden last line, printed to 8 digits) -- 1e-4 for problems whose
-    reference run ends far from convergence (large printed infeasibility);
+    golden last line, printed to 8 digits); where the reference run ends
+    far from convergence (large printed infeasibility) and on the rounding-
+    unstable problems, within the reference's own rounding envelope of its
+    final line (final_bracket: [min, max] over its base run and its rounding
+    variants that end optimal, widened by 1e-6);
   * HSD stops only when mu < 1e-12 (hsd.c:24,155), the "duality gap" proxy.
 """
 import json
@@ -75,6 +78,37 @@ def check_envelope(rows, stat, runs):
     statuses = {s for _, s in runs}
     assert stat in statuses or (stat == "optimal solution" and "iteration limit" in statuses), (stat, runs)
     assert len(rows) <= max(i for i, _ in runs) + 1, (len(rows), runs)
+
+
+def final_bracket(v, base):
+    """Where the reference's base run (the golden trace / the unperturbed
+    oracle) ends "optimal solution": per objective, [min, max] of the last
+    printed line over that run and those of its rounding variants that also
+    end optimal (rounding_stability.json "<variant>_last", tools/final_lines.py),
+    widened by 1e-6 relative -- the reference's own rounding envelope of its
+    final line.  None where the base run does not converge (forplan: no
+    final objective is the reference's there)."""
+    if v is None or v.get(f"{base}_status") != "optimal solution" or not v.get(f"{base}_last"):
+        return None
+    lines = [v[f"{k}_last"] for k in (base, "fma", "reverse", "sorted")
+             if v.get(f"{k}_status") == "optimal solution" and v.get(f"{k}_last")]
+    out = []
+    for idx in (1, 2):
+        vals = [ln[idx] for ln in lines]
+        lo, hi = min(vals), max(vals)
+        w = 1e-6 * max(1.0, abs(lo), abs(hi))
+        out.append((lo - w, hi + w))
+    return out
+
+
+def check_final_bracket(rows, v, base):
+    """A GPU "optimal solution" inside final_bracket (pobj, dobj)."""
+    br = final_bracket(v, base)
+    if br is None:
+        return False
+    for col, (lo, hi) in zip((1, 3), br):
+        assert lo <= rows[-1][col] <= hi, (col, rows[-1][col], lo, hi, v)
+    return True
 
 
 def check_optimum(method, name, rows, grows, gstat):
@@ -169,6 +203,7 @@ def check_hsd(name, text):
             raise AssertionError((stat, gstat))
         if stat == "optimal solution":
             check_optimum("hsd", name, rows, grows, gstat)
+            check_final_bracket(rows, v, "golden")
         return
     if gstat == "iteration limit" and stat == "optimal solution":
         # the reference ran out of iterations (MAX_ITER=200) on a problem it
@@ -181,12 +216,15 @@ def check_hsd(name, text):
     # measured 1.1e-5 apart at mu 1.2e-6 on pilot87 with the widened tail
     _check_trajectory(rows, grows, 1e-8 if gstat == "optimal solution" else MU_FLOOR_UNSTABLE)
     assert abs(len(rows) - len(grows)) <= 1
-    if stat == "optimal solution":
-        tol = 1e-6 if grows[-1][2] < 1e-3 else 1e-4
-    else:                   # both stopped at MAX_ITER somewhere along a slow tail
-        tol = 1e-2
-    assert rel(rows[-1][1], grows[-1][1]) <= tol
-    assert rel(rows[-1][3], grows[-1][3]) <= tol
+    if stat == "optimal solution" and grows[-1][2] >= 1e-3:
+        # the reference stops far from feasibility (large printed
+        # infeasibility): the final objectives within its own rounding
+        # envelope (final_bracket) instead of 1e-6 of its one order
+        assert check_final_bracket(rows, v, "golden")
+    else:
+        tol = 1e-6 if stat == "optimal solution" else 1e-2   # 1e-2: both at MAX_ITER along a slow tail
+        assert rel(rows[-1][1], grows[-1][1]) <= tol
+        assert rel(rows[-1][3], grows[-1][3]) <= tol
     if stat == "optimal solution":
         # printed mu of the last iterate; the stop test (mu < 1e-12, hsd.c:155)
         # is on the next one, so this is the reference's own order of magnitude
@@ -249,6 +287,7 @@ def check_oracle_method(method, name, text, ref, table):
     check_envelope(rows, stat, envelope(v, "oracle"))
     if stat == "optimal solution":
         check_optimum(method, name, rows, rrows, rstat)
+        check_final_bracket(rows, v, "oracle")
 
 
 @pytest.mark.parametrize("name", sorted(INTPT))
@@ -273,8 +312,12 @@ def test_dfl001_hsd_headline():
     assert stat == gstat == "optimal solution"
     assert abs(len(rows) - len(grows)) <= 1
     assert rows[-1][5] < 1e-11
-    assert rel(rows[-1][1], grows[-1][1]) <= 1e-4
-    assert rel(rows[-1][3], grows[-1][3]) <= 1e-4
+    # dfl001 is rounding-unstable (the reference's own orders part at
+    # iteration 69 of 116): its final objectives within the reference's own
+    # rounding envelope -- golden -1.1272163e7 / -1.1263430e7, reversed
+    # -1.1271102e7 / -1.1264001e7, FMA -1.1271116e7 / -1.1264015e7, sorted
+    # -1.1271139e7 / -1.1263979e7 -- widened by 1e-6 (final_bracket)
+    assert check_final_bracket(rows, STABILITY["dfl001"], "golden")
 
 
 def test_solver_symbol_abi_trace_and_buffers():
