@@ -54,7 +54,7 @@ METRIC = "IPM iterations/sec (ADA^T factor+solve) on netlib dfl001; duality gap 
 FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 (matrix = vector) dense peak, AMD spec (the guide has no fp64 row)
 PHASE_KERNELS = {"gather": "k_update|k_update_flat|k_update_quad",
                  "diag": "k_panel_w|k_panel_s|k_panel_s1|k_panel_ws|k_diag", "trsm": "k_trsm",
-                 "tail_syrk": "k_tail_syrk", "tail": "k_tail_pr|k_tail_col|k_tail_dep|k_tail_restore",
+                 "tail_syrk": "k_tail_syrk", "tail": "k_tail_run|k_tail_pr|k_tail_col|k_tail_dep|k_tail_restore",
                  "forward": "k_forward|k_fwd_leaf|k_fwd_leaf8|k_fwd_level|k_fwd_diag|k_fwd_gemv|k_fwd_pre|k_fwd_sf|"
                             "k_tail_gather|k_tail_fwd|k_tail_fwd_chain|k_tail_fwd_pair|k_tail_fwd_lead",
                  "backward": "k_backward|k_bwd_leaf|k_bwd_leaf8|k_bwd_level|k_bwd_partial|k_bwd_finish|k_bwd_sf|"
@@ -259,7 +259,7 @@ def oracle_run(mps, method, iters=200):
     return st, r.iters, r.t_total - r.t_setup, r.t_setup
 
 
-def intpt_leg(args, sync):
+def intpt_leg(args, sync, cpu=None):
     """BASELINE configs[1]: netlib 25fv47 by intpt (intpt.c:133-238; one KKT
     factorisation and one refined solve per iteration) on one GPU, problem
     resident in HBM; a step is one complete solve to intpt's own stop
@@ -297,21 +297,31 @@ def intpt_leg(args, sync):
            "final_dobj": st["final_dobj"], "m": p.m, "n": p.n, "nz": p.nz, "lnz": st["lnz"],
            "setup_s": ctx.setup_seconds, "roofline": roof, "phases_one_solve": ph,
            "published_optimum": 5.5018458883e3}
-    if args.cpu_iters > 0:
-        try:
-            t_loop, n_it, n_solves = 0.0, 0, 0
-            while t_loop < 10.0 and n_solves < 40:
-                cst, ci, cl, _ = oracle_run(path, "intpt")
-                t_loop, n_it, n_solves = t_loop + cl, n_it + ci, n_solves + 1
-            out["cpu_baseline"] = {"value": n_it / t_loop, "unit": "iterations/s", "cores": 1, "kind": "port",
-                                   "sample": f"{n_solves} complete 25fv47 intpt solves of {ci} iterations (status "
-                                             f"{cst}), oracle/ C restatement, single thread, symbolic setup excluded, "
-                                             f"{t_loop:.1f}s timed", "oracle_iterations": ci}
-            if out["value"] is not None:
-                out["speedup_vs_cpu_baseline"] = out["value"] / out["cpu_baseline"]["value"]
-        except Exception as e:  # noqa: BLE001 -- the GPU number stands on its own
-            out["cpu_baseline"] = {"error": repr(e)}
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+        if out["value"] is not None and "value" in cpu:
+            out["speedup_vs_cpu_baseline"] = out["value"] / cpu["value"]
     return out
+
+
+def intpt_cpu_baseline():
+    """The oracle's intpt on 25fv47 (one thread, whole solves repeated for
+    ~10 s), pinned to one core before the GPU is initialised."""
+    from conftest import mps_path
+    path = mps_path("25fv47")
+
+    def loop():
+        t_loop, n_it, n_solves = 0.0, 0, 0
+        while t_loop < 10.0 and n_solves < 40:
+            cst, ci, cl, _ = oracle_run(path, "intpt")
+            t_loop, n_it, n_solves = t_loop + cl, n_it + ci, n_solves + 1
+        return t_loop, n_it, n_solves, cst, ci
+    (t_loop, n_it, n_solves, cst, ci), core = pinned(loop)
+    return {"value": n_it / t_loop, "unit": "iterations/s", "cores": 1, "kind": "port",
+            "sample": f"{n_solves} complete 25fv47 intpt solves of {ci} iterations (status "
+                      f"{cst}), oracle/ C restatement, single thread, symbolic setup excluded, "
+                      f"{t_loop:.1f}s timed", "oracle_iterations": ci, "pinned_core": core,
+            "cpu_model": host_cpu_model(), "when": "before the GPU is initialised"}
 
 
 HBM_WORKLOAD = ("synthetic random sparse LP, BASELINE configs[3] uniform variant: m=200,000, n=1,000,000, "
@@ -379,7 +389,7 @@ def pmc_traffic(phase):
     ph = d.get("phases", {}).get(phase)
     if not ph:
         return None
-    return ph["hbm_bytes_per_launch"], os.path.basename(files[-1])
+    return ph["hbm_bytes_per_launch"], os.path.basename(files[-1]), d.get("commit")
 
 
 def pmc_mfma():
@@ -398,13 +408,40 @@ def pmc_mfma():
                        for k, v in d.get("phases", {}).items()}}
 
 
+def host_cpu_model():
+    """The host CPU's model name (/proc/cpuinfo, as lscpu prints it)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def pinned(fn):
+    """fn() on one host core (os.sched_setaffinity of this thread, which runs
+    the oracle through ctypes), the previous mask restored after; returns
+    (result, core).  The CPU legs run before the process touches the GPU."""
+    old = os.sched_getaffinity(0)
+    core = min(old)
+    os.sched_setaffinity(0, {core})
+    try:
+        return fn(), core
+    finally:
+        os.sched_setaffinity(0, old)
+
+
 def cpu_baseline(mps, iters):
-    """Oracle (single-threaded C restatement of ipo) on `iters` HSD iterations of dfl001."""
-    _, it, loop, setup = oracle_run(mps, "hsd", iters)
+    """Oracle (single-threaded C restatement of ipo) on `iters` HSD iterations
+    of dfl001, pinned to one core before the GPU is initialised."""
+    (_, it, loop, setup), core = pinned(lambda: oracle_run(mps, "hsd", iters))
     return {"value": it / loop, "unit": "iterations/s", "cores": 1, "kind": "port",
             "sample": f"dfl001 hsd iterations 0..{it - 1} ({it} of 117), oracle/ C restatement, "
                       f"single thread, symbolic setup {setup:.2f}s excluded, {loop:.1f}s timed",
-            "host_cpus": os.cpu_count()}
+            "pinned_core": core, "cpu_model": host_cpu_model(), "host_cpus": os.cpu_count(),
+            "when": "before the GPU is initialised"}
 
 
 def end_to_end(p, golden, sync):
@@ -450,12 +487,26 @@ def main():
     d = Dist()
     import ipo_amd
     from conftest import mps_path
+    path = mps_path(args.problem)
+    # the CPU baselines first, each pinned to one host core, before anything
+    # in this process touches the GPU (the reference CPU path
+    # timed on the node's own host cores)
+    cpu_hsd = cpu_intpt = None
+    if d.rank == 0 and d.world == 1 and args.cpu_iters > 0:
+        try:
+            cpu_hsd = cpu_baseline(path, args.cpu_iters)
+        except Exception as e:  # noqa: BLE001 -- the GPU number stands on its own
+            cpu_hsd = {"error": repr(e)}
+        if args.intpt == "on":
+            try:
+                cpu_intpt = intpt_cpu_baseline()
+            except Exception as e:  # noqa: BLE001
+                cpu_intpt = {"error": repr(e)}
     ipo_amd.require_gpu()
     if d.world > 1:
         ipo_amd.set_device(d.local)       # one process per GPU
     sync = ipo_amd.device_synchronize
 
-    path = mps_path(args.problem)
     p = ipo_amd.load_mps(path)
     ctx = ipo_amd.Context(p)                       # upload + symbolic (not timed)
     golden = GOLDEN_ITERS.get(args.problem)
@@ -516,7 +567,8 @@ def main():
                     "frac": ach / HBM_PEAK_GBS, "traffic": None}
         tr = pmc_traffic(top)
         if tr is not None:
-            roof["traffic"], roof["traffic_source"] = tr
+            roof["traffic"], roof["traffic_source"], roof["traffic_commit"] = tr
+            roof["traffic_note"] = "from the committed counter profile named, taken at traffic_commit, not this run"
         mf = pmc_mfma()
         if mf is not None and top in mf["phases"]:
             roof["mfma_util"] = mf["phases"][top]["mfma_util"]
@@ -576,13 +628,10 @@ def main():
         "mfma_counters": pmc_mfma(),
         "cpu_baseline": None,
     }
-    if d.rank == 0 and d.world == 1 and args.cpu_iters > 0:
-        try:
-            out["cpu_baseline"] = cpu_baseline(path, args.cpu_iters)
-            if value is not None:
-                out["config"]["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
-        except Exception as e:  # the GPU number stands on its own
-            out["cpu_baseline"] = {"error": str(e)}
+    if cpu_hsd is not None:
+        out["cpu_baseline"] = cpu_hsd
+        if value is not None and "value" in cpu_hsd:
+            out["config"]["speedup_vs_cpu_baseline"] = value / cpu_hsd["value"]
     ctx.close()
     if d.rank == 0:
         try:
@@ -591,7 +640,7 @@ def main():
             out["end_to_end"] = {"error": repr(e)}
     if args.intpt == "on" and d.world == 1:
         try:
-            out["intpt_25fv47"] = intpt_leg(args, sync)
+            out["intpt_25fv47"] = intpt_leg(args, sync, cpu_intpt)
         except Exception as e:  # noqa: BLE001 -- the headline number stands on its own
             out["intpt_25fv47"] = {"workload": INTPT_WORKLOAD, "error": repr(e)}
     if args.banded == "on" and d.world == 1:

@@ -3,7 +3,8 @@
 # round is one of these, run from the repository root on the GPU box as
 #   gpurun --timeout S -- 'bash tools/gpu_recipes.sh <recipe> [args]'
 # so that a number quoted in DESIGN.md or a commit message can be traced to
-# the steps that produced it.  Each GPU step runs under its own time limit
+# the steps that produced it (round 5's one-off call scripts, tools/gpu_calls/,
+# are in the history before this file replaced them).  Each GPU step runs under its own time limit
 # (tools/gpu_step.sh: a fault, abort or timeout stops the call there) and
 # writes its log under gpurun_out/.  The round profile is tools/profile_round.sh.
 #
@@ -17,7 +18,8 @@
 #   ab VAR v0 v1     bench.py dfl001 with VAR=v0, then VAR=v1, twice each
 #   sweep            tools/gpu_sweep.py over every problem (hsd) and the intpt /
 #                    hsdls sets, traces saved (offline parity checks)
-#   profile TAG [p]  tools/profile_round.sh TAG [part]
+#   profile TAG [p]  tools/profile_round.sh TAG [part]; pass the commit the tree
+#                    was taken at as PROFILE_COMMIT=<sha> before the recipe
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 STEP="bash tools/gpu_step.sh"
@@ -28,6 +30,9 @@ recipe=$1; shift
 case "$recipe" in
 ubtail)
     nt=${1:-4441}
+    # the microbenchmark binary does not travel (.gpurunignore): built here
+    [ -x tools/ubench_tail ] || hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off \
+        -I linear-programming-vanderbei_amd/csrc tools/ubench_tail.hip -o tools/ubench_tail || exit 1
     $STEP 60 ub_step_$nt.log tools/ubench_tail $nt 5 || exit 1
     UB_RUN=1 $STEP 60 ub_run_$nt.log tools/ubench_tail $nt 5 || exit 1
     ;;

@@ -34,6 +34,9 @@ os.makedirs(dst, exist_ok=True)
 
 
 LEGS_ONLY = os.environ.get("LEGS_ONLY") == "1"     # tools/profile_round.sh part 2: the synthetic legs alone
+# the commit the profiled tree was taken at (the GPU box has no .git: the
+# caller passes it, tools/gpu_recipes.sh profile); recorded in every summary
+COMMIT = os.environ.get("PROFILE_COMMIT")
 
 
 def short(name):
@@ -69,9 +72,11 @@ def dfl001_part():
 
     steps = [round((e - b) / 1000.0, 1) for b, e in
              c.execute("select start, end from kernels where name like '%k_tail_pr%' order by start limit 700")]
+    runs = [round((e - b) / 1000.0, 1) for b, e in
+            c.execute("select start, end from kernels where name like '%k_tail_run%' order by start limit 200")]
     with open(os.path.join(dst, f"{tag}_tail_steps.json"), "w") as fh:
-        json.dump({"source": "rocprofv3 --kernel-trace, bench.py --steps 2 (dfl001 hsd)", "unit": "us",
-                   "k_tail_pr": steps}, fh)
+        json.dump({"source": "rocprofv3 --kernel-trace, bench.py --steps 2 (dfl001 hsd)", "unit": "us", "commit": COMMIT,
+                   "k_tail_pr": steps, "k_tail_run": runs}, fh)
 
 
     fetch = per_kernel(os.path.join(src, f"{tag}_pmc_fetch", "run_results.db"), "FETCH_SIZE")
@@ -95,7 +100,7 @@ def dfl001_part():
     with open(os.path.join(dst, f"{tag}_pmc_traffic.json"), "w") as fh:
         json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, bench.py --steps 1 --warmup 0 --no-timing "
                              "(dfl001 hsd, first 10 iterations); FETCH_SIZE doubled (gfx950)",
-                   "phases": phases, "kernels": kern}, fh, indent=1)
+                   "commit": COMMIT, "phases": phases, "kernels": kern}, fh, indent=1)
     # f64 MFMA utilisation per kernel / phase: SQ_VALU_MFMA_BUSY_CYCLES (MFMA-busy
     # cycles summed over the SIMDs: 64 per v_mfma_f64_16x16x4f64, calibrated on
     # k_tail_pr whose instruction count is known) over the kernel's active
@@ -138,7 +143,7 @@ def dfl001_part():
                                  "GRBM_GUI_ACTIVE, bench.py --steps 1 --warmup 0 --no-timing (dfl001 hsd); util = "
                                  "MFMA-busy cycles / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs); MOPS_F64 in units of 512 "
                                  "flops; tflops over the kernel-trace average duration",
-                       "phases": mph, "kernels": mk}, fh, indent=1)
+                       "commit": COMMIT, "phases": mph, "kernels": mk}, fh, indent=1)
     # HBM bytes per launch of the hbm_roofline leg's kernels (tools/hbm_probe.py
     # under the same FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled)
     hf = os.path.join(src, f"{tag}_pmc_hfetch", "run_results.db")
@@ -164,7 +169,7 @@ def dfl001_part():
         with open(os.path.join(dst, f"{tag}_pmc_hbm.json"), "w") as fh:
             json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, tools/hbm_probe.py 5 (bench.py's "
                                  "hbm_roofline kernels, BASELINE configs[3] uniform LP); FETCH_SIZE doubled (gfx950)",
-                       "kernels": hk}, fh, indent=1)
+                       "commit": COMMIT, "kernels": hk}, fh, indent=1)
 
 
 if not LEGS_ONLY:
@@ -188,7 +193,7 @@ for leg, probe in (("banded", "tools/banded_probe.py"), ("blockang", "tools/bloc
             w.writerow([short(n), calls, f"{tot:.1f}", f"{avg:.2f}", f"{pct:.2f}"])
     out = {"source": f"rocprofv3 --kernel-trace --stats / --pmc passes, python3 {probe} {iters} 0; FETCH_SIZE "
                      f"doubled (gfx950); per IPM iteration = run total / {iters}",
-           "iterations": iters, "kernel_ms_per_iteration": sum(r[2] for r in krows) / 1000.0 / iters}
+           "iterations": iters, "kernel_ms_per_iteration": sum(r[2] for r in krows) / 1000.0 / iters, "commit": COMMIT}
     f_ = os.path.join(src, f"{tag}_{leg}_pmc_fetch", "run_results.db")
     w_ = os.path.join(src, f"{tag}_{leg}_pmc_write", "run_results.db")
     if os.path.exists(f_) and os.path.exists(w_):
