@@ -90,6 +90,8 @@ typedef struct {
     double phase_bytes[8];   /* algorithmic bytes of one occurrence                   */
     long   tail_repairs;     /* dense-tail block columns redone after a bail-out      */
     long   tail_dep_rounds;  /* k_tail_dep launches of those repairs                  */
+    long   tail_chain_aborts;/* dense-tail chain launches aborted (a contradicted
+                              * dropped column): factorisation redone per step     */
 } ipo_hip_stats;
 
 /* method: 0 = hsd, 1 = intpt, 2 = hsdls.  trace may be NULL (silent).  timing != 0

@@ -86,6 +86,7 @@ void fill_stats(ipo_hip_stats* st, const ipo::IpmResult& r, const ipo::KktDevice
                          r.kkt.phase_launches[ipo::kPhSyrk];
     st->tail_repairs = r.kkt.tail_repairs;
     st->tail_dep_rounds = r.kkt.tail_dep_rounds;
+    st->tail_chain_aborts = r.kkt.tail_chain_aborts;
     static_assert(ipo::kNumPhases <= 8, "ipo_hip_stats holds 8 phases");
     for (int ph = 0; ph < ipo::kNumPhases; ph++) {
         st->phase_ms[ph] = r.kkt.phase_ms[ph];

@@ -593,22 +593,26 @@ struct DepState {
     int* lv;               // LDS: per column 1 live, 0 dropped, 2 kept with +-1e-8 (dependent), published with dv
     int* spec;             // LDS: the speculation failed (or met a NaN)
     int ndep;              // dependent pivots of this wave's window
+    int specv = 1;         // what a failure stores in *spec (k_tail_chain_run: its pass, so no reset is needed)
 };
 
 __device__ __forceinline__ void dep_pivot(double col, int k, int lane, int h0, double& dk, int& alive, DepState& ds) {
     const bool in = lane > k && lane < h0;
     const bool big = __ballot(in && !(fabs(col) < 1.0e+6 * 1.0e-8)) != 0;   // includes NaN
     const bool nan = __ballot(in && col != col) != 0;
-    if (nan && lane == 0) *ds.spec = 1;     // the host repair decides it (the reference's NaN-order max)
+    if (nan && lane == 0) *ds.spec = ds.specv;   // the host repair decides it (the reference's NaN-order max)
     if (big) dk = (ds.sign[k] < 0 ? -1.0 : 1.0) * 1.0e-8;   // y-nodes -, x-nodes +
     else alive = 0;                                        // dropped, d keeps its value
     ds.ndep++;
 }
 
+// pb (all window routines): the progress counters' base -- a window's
+// column i is published as pb + i + 1, so a workgroup that runs several
+// passes (k_tail_chain_run) needs no reset barrier between them.
 template <bool FULL, bool DEP>
 __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& tz_any, int cw0, int nc, int lane,
                                            int h0, double tau, double (*Ct)[CTS], double (*Lr)[PC], double* dv,
-                                           int* prog, DepState& ds) {
+                                           int* prog, DepState& ds, int pb = 0) {
     double dk = lane_bcast(a[0], cw0);
     int alive = 1, mark = 1;
     if (DEP) {
@@ -635,7 +639,7 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
             // (and the published count) after the writes for the compiler;
             // the LDS runs one wave's operations in issue order
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __hip_atomic_store(prog, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(prog, pb + i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (i == WIN - 1) PANEL_STAMP(5);
             dsc = dsc + fabs(l * c);
             double cc[WIN];
@@ -671,12 +675,12 @@ __device__ __forceinline__ void win_factor(double (&a)[WIN], double& dsc, bool& 
 // the updates ran at half the speed.)
 template <bool DSC>
 __device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw, int lane, int cw0,
-                                          double (*Ct)[CTS], double (*L)[PC], const int* prog) {
+                                          double (*Ct)[CTS], double (*L)[PC], const int* prog, int pb = 0) {
     // software-pipelined: step i + 1's LDS operands are read before step i's
     // arithmetic, so the read latency hides under the updates
     int seen = 0;
     double l, ck = 0.0, cc[WIN];
-    df_wait(prog, 1, seen);
+    df_wait(prog, pb + 1, seen);
     l = L[kw][lane];
     if (DSC) ck = Ct[kw][lane];
     win_row(&Ct[kw][cw0], cc);
@@ -685,7 +689,7 @@ __device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw,
         const int k = kw + i;
         double ln = 0.0, ckn = 0.0, cn[WIN];
         if (i + 1 < WIN) {
-            df_wait(prog, i + 2, seen);
+            df_wait(prog, pb + i + 2, seen);
             if (i + 2 == WIN) PANEL_STAMP(6);
             ln = L[k + 1][lane];
             if (DSC) ckn = Ct[k + 1][lane];
@@ -712,24 +716,24 @@ __device__ __forceinline__ void win_apply(double (&a)[WIN], double& dsc, int kw,
 template <bool FULL, bool DEP>
 __device__ __forceinline__ void win_solve(double (&a)[WIN], int cw0, int nc, bool rok, int lane, double (*Ct)[CTS],
                                           double (*Lb)[PC], const double* dv, const int* wprog, int* prog,
-                                          DepState& ds) {
+                                          DepState& ds, int pb = 0) {
     int seen = 0;
 #pragma unroll
     for (int i = 0; i < WIN; i++) {
         const int k = cw0 + i;
         if (FULL || k < nc) {
-            df_wait(wprog, i + 1, seen);
+            df_wait(wprog, pb + i + 1, seen);
             double l;
             if (DEP && !ds.lv[k]) {
-                if (__ballot(rok && !(fabs(a[i]) < 1.0e+6 * 1.0e-8)) != 0 && lane == 0) *ds.spec = 1;
+                if (__ballot(rok && !(fabs(a[i]) < 1.0e+6 * 1.0e-8)) != 0 && lane == 0) *ds.spec = ds.specv;
                 l = 0.0;
             } else {
-                if (DEP && ds.lv[k] == 2 && __ballot(rok && a[i] != a[i]) != 0 && lane == 0) *ds.spec = 1;
+                if (DEP && ds.lv[k] == 2 && __ballot(rok && a[i] != a[i]) != 0 && lane == 0) *ds.spec = ds.specv;
                 l = rok ? a[i] / dv[k] : 0.0;
             }
             a[i] = l;
             Lb[k][lane] = l;
-            df_publish(prog, i + 1);
+            df_publish(prog, pb + i + 1);
             double cc[WIN];
             win_row(&Ct[k][cw0], cc);
 #pragma unroll
@@ -1405,6 +1409,10 @@ k_tail_pr(PlanView p, TailView tv, int t, int gp, int vbase) {
 // is skipped without counting, and the host repair resumes the run from
 // step tb + 1 with the counters as they are.
 __host__ __device__ __forceinline__ int tail_gp(int nt, int t) { return max(1, (nt - t * PC + TR - 1) / TR - 1); }
+// visits (chunks) of block column c in the persistent schedules (run_chunks)
+__host__ __device__ __forceinline__ int run_chunk_count(int c, int K, int L) {
+    return c <= 1 ? 0 : 1 + (max(0, c - 1 - L) + K - 1) / K;
+}
 
 // A panel workgroup that bails adds 1 + kRunBail to pdone[t]: a waiter on
 // the panels of step t learns both in one load.
@@ -1496,6 +1504,643 @@ k_tail_run(PlanView p, TailView tv, TailRun rc) {
         int* vs = rc.vseq + bi * ntb + c;
         if (!run_wait(t > rc.t0 ? rc.pdone + t - 1 : nullptr, t > rc.t0 ? tail_gp(tv.nt, t - 1) : 0, q ? vs : nullptr,
                       q, bailp, t, &sh_ok))
+            return;
+        if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+        visit_tile512<true>(p, tv, bi, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
+        run_signal(vs);
+    }
+    if (tr && threadIdx.x == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ------------------------------- dense tail: one launch around a chain workgroup
+// k_tail_chain_run (default path of the look-ahead tail): the steps of the
+// look-ahead factorisation as ticketed items of one launch, like k_tail_run,
+// but the critical path -- diagonal block t, the tile t + 1 below it, block t
+// + 1's pre-update by block t -- stays inside ONE long-lived workgroup (the
+// chain item, ticket 0, one pass over every block column):
+//   waves 0-3 (half 0) factor diagonal block t by windows (win_factor), and
+//     publish each window, once it and every window before it passed the
+//     zero test, to global memory (c = l d of the block rows, d, marks:
+//     dpub, flag dwin) for the tile items;
+//   waves 4-7 (half 1) solve tile t + 1 against the block's windows through
+//     LDS (win_solve), as k_panel_w's workgroup 0 does;
+//   block t + 1's pre-update by block t, L(t+1, t) W(t+1, t)' with W = L D
+//     (the products k_tail_pr's next launch would reload and form), is
+//     accumulated in the MFMA registers of half 0 as half 1 completes each
+//     window of tile t + 1 -- the operands never leave LDS -- and the |terms|
+//     of block t + 1's pivots beside it, k in order;
+//   tile t + 2's pre-update by block t, L(t+2, t) W(t+1, t)', is formed by
+//     half 1 once the tile item (t, t + 2) has stored its rows, while half 0
+//     already factors block t + 1.
+// Every entry receives the same products in the same order as in k_tail_pr
+// (the same MFMA fragments, k ascending, then old - acc; the same window
+// operations), so the factor is bitwise that of k_tail_run with the same
+// visit chunks.  Tile items (t, R), R >= t + 2: the tile's pre-update (as
+// k_tail_pr's panel workgroups), then tile R solved window by window against
+// the chain's published windows.  Visits: as in k_tail_run.  A dependent
+// pivot in block t: the chain reruns the block with the rule of ldlt.c:600-614
+// from its saved inputs (what it published before the failing window is
+// unchanged); a tile that contradicts a dropped column, a NaN in the rule, or
+// a zero pivot without the in-panel rule (TailView::dep == 0) aborts the
+// launch (flags[1] bit 64) and the host redoes the factorisation with the
+// per-step look-ahead and its repairs.  Waits poll the abort flag, so the
+// grid always drains.
+struct ChainLds {
+    PanelLds P;               // Ct, Lr, Lb, dv, lv, prog[8], tiny, spec, ndep
+    double T[PC][CTS];        // half 1: L(t + 2, t) as [k][row], then the product as [col][row]
+    double dvp[PC];           // D of block t (half 1's product runs while block t + 1 overwrites dv)
+    int hs[2];                // half-0 / half-1 meeting counters (monotonic)
+    int winok[4];             // diagonal window verdicts of the current pass: pass << 2 | 1 clean, | 2 zero pivot
+    int arrive;               // half-1 waves whose step results have drained (monotonic)
+    int sh[2];                // workgroup wait verdicts
+};
+constexpr size_t kChainItemLds = sizeof(ChainLds) > kTailStepLds ? sizeof(ChainLds) : kTailStepLds;
+
+__host__ __device__ __forceinline__ int chain_target(int ntb, int t) { return 1 + max(0, ntb - t - 2); }
+
+__device__ __forceinline__ void chain_abort(const PlanView& p, int* abortp) {
+    atomicOr(&p.flags[1], 64);
+    __hip_atomic_store(abortp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the four waves of one half meet (the other half runs on): each wave bumps
+// an LDS counter once per meeting; gen counts this wave's meetings
+__device__ __forceinline__ void half_sync(int* cnt, int& gen) {
+    gen += 4;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < gen)
+        __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// one wave waits until *c >= v (lane 0 polls); false: the launch aborted
+__device__ __forceinline__ bool wave_poll(const int* c, int v, const int* abortp) {
+    int ok = 1;
+    if ((threadIdx.x & 63) == 0) {
+        while (sc1_load_int(c) < v) {
+            if (sc1_load_int(abortp)) {
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
+// the workgroup waits until *c0 >= v0 and *c1 >= v1 (null: none); false: abort
+__device__ __forceinline__ bool chain_wg_wait(const int* c0, int v0, const int* c1, int v1, const int* abortp, int* sh) {
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        for (;;) {
+            if ((!c0 || sc1_load_int(c0) >= v0) && (!c1 || sc1_load_int(c1) >= v1)) break;
+            if (sc1_load_int(abortp)) {
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *sh = ok;
+    }
+    __syncthreads();
+    return *sh != 0;
+}
+
+// lower 16 x 16 fragments (fx >= fy) of block t + 1's pre-update, three per
+// half-0 wave for waves 0-1, two for 2-3
+__device__ constexpr int kPdFx[12] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3, -1, -1};
+__device__ constexpr int kPdFy[12] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3, -1, -1};
+
+// block column k1's diagonal block after its visits: this wave's window of
+// columns (lower triangle), and the |terms| of the pivots it holds
+__device__ __forceinline__ void chain_load_diag(const TailView& tv, const PlanView& p, int k1, int nc1, int h01, int cw0,
+                                                int lane, int w, double (&sd)[WIN], double& dscl) {
+    const int nt = tv.nt;
+    const bool rk = lane < h01;
+#pragma unroll
+    for (int q = 0; q < WIN; q++) {
+        const int c = cw0 + q;
+        const bool ok = rk && c < nc1 && c <= lane;
+        const double x = sc1_load(tv.S + (ok ? k1 + lane + (size_t)(k1 + c) * nt : 0));
+        sd[q] = ok ? x : 0.0;
+    }
+    dscl = (lane < nc1 && (lane >> 4) == w) ? sc1_load(p.dscale + tv.tc + k1 + lane) : 0.0;
+}
+
+// developer trace of the chain (ChainRun::trace): per step and wave four
+// stamps after the items' records: e 0 own window begins, 1 it ends, 2 the
+// pass's work done, 3 after the pass's barriers
+#define CHAIN_STAMP(t, e)                                                                              \
+    do {                                                                                               \
+        if (rc.trace && (threadIdx.x & 63) == 0)                                                       \
+            rc.trace[4 * ((size_t)rc.n + tv.ntb) + (size_t)(t) * 32 + (threadIdx.x >> 6) * 4 + (e)] =   \
+                __builtin_amdgcn_s_memrealtime();                                                      \
+    } while (0)
+
+// The chain item is two loops over the block columns, one per half of the
+// workgroup (waves 0-3 and 4-7), meeting at the same workgroup barriers (two
+// per pass) and through LDS counters: each half keeps only its own state
+// live (written as one interleaved loop the two halves' registers added up
+// and spilled).
+// Half 0: block t's windows, their publication, block t + 1's pre-update.
+__device__ __forceinline__ void chain_half0(const PlanView& p, const TailView& tv, const ChainRun& rc,
+                                                      ChainLds& C) {
+    PanelLds& S = C.P;
+    const int nt = tv.nt, ntb = tv.ntb, tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6), cw0 = WIN * w;
+    const int li = lane & 15, lk = lane >> 4;
+    int passes = 0, g0 = 0;
+    double a[WIN], dsc;
+    {
+        // step 0: S(0, 0)'s lower triangle and the |terms| of its pivots
+        const int nc = min(PC, nt);
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            const bool ok = lane < nc && c < nc && c <= lane;
+            const double x = sc1_load(tv.S + (ok ? lane + (size_t)c * nt : 0));
+            a[q] = ok ? x : 0.0;
+        }
+        dsc = (lane < nc && (lane >> 4) == w) ? sc1_load(p.dscale + tv.tc + lane) : 0.0;
+    }
+    for (int t = 0; t < ntb; t++) {
+        const int k0 = t * PC, nc = min(PC, nt - k0), h = nt - k0, h0 = min(PC, h), c0 = tv.tc + k0;
+        double* panel = tv.S + k0 + (size_t)k0 * nt;
+        const bool next = t + 1 < ntb;
+        const int nwin = (nc + WIN - 1) / WIN;
+        const bool holder = lane < nc && (lane >> 4) == w;
+        unsigned long long* tr = rc.trace ? rc.trace + 4 * (size_t)(rc.n + t) : nullptr;
+        if (tr && tid == 0) tr[0] = __builtin_amdgcn_s_memrealtime();
+        // the step's inputs, for a dependent-pivot rerun (each wave reloads its own)
+#pragma unroll
+        for (int q = 0; q < WIN; q++) sc1_store(rc.save + (cw0 + q) * PC + lane, a[q]);
+        if (holder) sc1_store(rc.save + 2 * PC * PC + lane, dsc);
+        const double dsc_in = dsc;         // |terms| before the block's own steps: dscale(t)
+        double4_t pacc[3];
+        double asum = 0.0, sd[WIN], dscl = 0.0;
+        bool have_sd = false, dep_pass = false;
+        for (;;) {
+            passes++;
+            const int pb = WIN * passes;
+            if (tid == 0) S.ndep = 0;
+#pragma unroll
+            for (int f = 0; f < 3; f++) pacc[f] = (double4_t){0.0, 0.0, 0.0, 0.0};
+            asum = 0.0;
+            if (w < nwin) {
+                DepState ds{p.sign + c0, S.lv, &S.spec, 0, passes};
+                int* const prog = S.prog;
+                for (int t2 = 0; t2 < w; t2++) {
+                    if (t2 + 1 < w) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(3);
+                    win_apply<true>(a, dsc, WIN * t2, lane, cw0, S.Ct, S.Lr, prog + t2, pb);
+                }
+                __builtin_amdgcn_s_setprio(3);
+                CHAIN_STAMP(t, 0);
+                bool tz = false;
+                const bool full = cw0 + WIN <= nc;
+                if (dep_pass) {
+                    if (full) win_factor<true, true>(a, dsc, tz, cw0, nc, lane, h0, p.tau, S.Ct, S.Lr, S.dv, prog + w, ds, pb);
+                    else win_factor<false, true>(a, dsc, tz, cw0, nc, lane, h0, p.tau, S.Ct, S.Lr, S.dv, prog + w, ds, pb);
+                    if (ds.ndep && lane == 0) atomicAdd(&S.ndep, ds.ndep);
+                } else {
+                    if (full) win_factor<true, false>(a, dsc, tz, cw0, nc, lane, h0, p.tau, S.Ct, S.Lr, S.dv, prog + w, ds, pb);
+                    else win_factor<false, false>(a, dsc, tz, cw0, nc, lane, h0, p.tau, S.Ct, S.Lr, S.dv, prog + w, ds, pb);
+                }
+                __builtin_amdgcn_s_setprio(0);
+                CHAIN_STAMP(t, 1);
+                if (tz && lane == 0) S.tiny = passes;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                if (lane == 0)
+                    __hip_atomic_store(&C.winok[w], passes << 2 | (tz ? 2 : 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // publish the window when it and every window before it passed the
+                // zero test (the dependent-pivot pass: all of them)
+                bool clean = !tz || dep_pass;
+                for (int v = 0; v < w; v++) {
+                    int x;
+                    while (((x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&C.winok[v], __ATOMIC_RELAXED,
+                                                                                   __HIP_MEMORY_SCOPE_WORKGROUP))) >> 2) != passes)
+                        __builtin_amdgcn_s_sleep(1);
+                    clean = clean && (dep_pass || (x & 3) == 1);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                if (clean && t + 2 < ntb) {
+                    double* dst = rc.dpub + ((size_t)t * 4 + w) * kChainWinPub;
+#pragma unroll
+                    for (int kk = 0; kk < WIN; kk++) sc1_store(dst + kk * PC + lane, S.Ct[cw0 + kk][lane]);
+                    if (lane < WIN) {
+                        sc1_store(dst + WIN * PC + lane, S.dv[cw0 + lane]);
+                        sc1_store(dst + WIN * PC + WIN + lane, dep_pass ? static_cast<double>(S.lv[cw0 + lane]) : 1.0);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane == 0) __hip_atomic_store(rc.dwin + t * 4 + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                // block t + 1's pre-update by block t, as half 1 completes each
+                // window of tile t + 1: the fragments k ascending, the |terms| of
+                // block t + 1's pivots (lane r = its row r) beside them
+                if (next) {
+                    const int k1 = k0 + PC, nc1 = min(PC, nt - k1);
+                    for (int v = 0; v < 4; v++) {
+                        if (v == 3 && !have_sd) {
+                            // block t + 1 after its visits, ahead of the step's end (after
+                            // an abort the wait falls through: the chain runs on with
+                            // garbage to its end, every wave in step, and the host
+                            // discards the launch)
+                            wave_poll(rc.vseq + (t + 1) * ntb + t + 1, run_chunk_count(t + 1, tv.vk, rc.latest), rc.abort);
+                            chain_load_diag(tv, p, k1, nc1, min(PC, nt - k1), cw0, lane, w, sd, dscl);
+                            have_sd = true;
+                        }
+                        int seen = 0;
+                        df_wait(S.prog + 4 + v, pb + WIN, seen);
+#pragma unroll
+                        for (int f = 0; f < 3; f++) {
+                            const int fi = w + 4 * f, fx = kPdFx[fi], fy = kPdFy[fi];
+                            if (fx < 0) continue;
+#pragma unroll
+                            for (int s4 = 0; s4 < 4; s4++) {
+                                const int kk = WIN * v + 4 * s4 + lk;
+                                const double av = S.Lb[kk][fx * 16 + li];
+                                const double bv = S.Lb[kk][fy * 16 + li] * S.dv[kk];
+                                pacc[f] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, pacc[f], 0, 0, 0);
+                            }
+                        }
+                        if (lane < nc1 && (lane >> 4) == w) {
+#pragma unroll
+                            for (int u = 0; u < WIN; u++) {
+                                const double x = S.Lb[WIN * v + u][lane];
+                                asum += fabs(x * (x * S.dv[WIN * v + u]));
+                            }
+                        }
+                    }
+                }
+            }
+            CHAIN_STAMP(t, 2);
+            __syncthreads();
+            const bool tiny = S.tiny == passes;
+            const bool spec = S.spec == passes;
+            __syncthreads();           // read by every wave before any can overwrite them
+            CHAIN_STAMP(t, 3);
+            if (!dep_pass && tiny && tv.dep) {
+                // rerun the block with the dependent-pivot rule from the saved inputs
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int q = 0; q < WIN; q++) a[q] = sc1_load(rc.save + (cw0 + q) * PC + lane);
+                dsc = holder ? sc1_load(rc.save + 2 * PC * PC + lane) : 0.0;
+                dep_pass = true;
+                continue;
+            }
+            if (spec || (!dep_pass && tiny)) {
+                if (tid == 0) chain_abort(p, rc.abort);
+                return;
+            }
+            break;
+        }
+        if (tr && tid == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+        // L11' into the block's upper slot (Lr[c][r] = l(r, c)), the rows of the
+        // block below nc (the last, partial block), marks, |terms|
+        for (int rr = 1 + w; rr < nc; rr += 4)
+            if (lane < rr) sc1_store(panel + lane + (size_t)rr * nt, S.Lr[lane][rr]);
+        if (lane >= nc && lane < h0) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++)
+                if (cw0 + q < nc) sc1_store(panel + lane + (size_t)(cw0 + q) * nt, S.Lr[cw0 + q][lane]);
+        }
+        if (tid < nc) p.live[c0 + tid] = dep_pass ? S.lv[tid] != 0 : 1;
+        if (holder && t > 0) sc1_store(p.dscale + c0 + lane, dsc_in);
+        if (dep_pass && tid == 0 && S.ndep) atomicAdd(&p.flags[0], S.ndep);
+        if (tr && tid == 0) tr[2] = __builtin_amdgcn_s_memrealtime();
+        if (!next) break;
+        // block t + 1: its entries after the visits minus block t's product
+        const int k1 = k0 + PC, nc1 = min(PC, nt - k1), h01 = min(PC, nt - k1);
+        if (!have_sd) {
+            wave_poll(rc.vseq + (t + 1) * ntb + t + 1, run_chunk_count(t + 1, tv.vk, rc.latest), rc.abort);
+            chain_load_diag(tv, p, k1, nc1, h01, cw0, lane, w, sd, dscl);
+        }
+        // the fragments to LDS as [col][row] (Ct is free: every window of block t is done)
+#pragma unroll
+        for (int f = 0; f < 3; f++) {
+            const int fi = w + 4 * f, fx = kPdFx[fi], fy = kPdFy[fi];
+            if (fx < 0) continue;
+#pragma unroll
+            for (int i = 0; i < 4; i++) S.Ct[fy * 16 + li][fx * 16 + lk + 4 * i] = pacc[f][i];
+        }
+        half_sync(&C.hs[0], g0);
+        const bool rk = lane < h01;
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            a[q] = (rk && c < nc1 && c <= lane) ? sd[q] - S.Ct[c][lane] : 0.0;
+        }
+        dsc = (lane < nc1 && (lane >> 4) == w) ? dscl + asum : 0.0;
+        // (each wave reads only its own columns of the product, which it alone
+        // overwrites next, with block t + 1's window: no second meeting)
+    }
+}
+
+// Half 1: tile t + 1 against block t's windows; its rows, D and the step's
+// signal; tile t + 2's pre-update by block t for the next step.
+__device__ __forceinline__ void chain_half1(const PlanView& p, const TailView& tv, const ChainRun& rc,
+                                                      ChainLds& C) {
+    PanelLds& S = C.P;
+    const int nt = tv.nt, ntb = tv.ntb, tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), w = (wv + 2) & 3, cw0 = WIN * w;
+    const int li = lane & 15, lk = lane >> 4;
+    int passes = 0, g1 = 0;
+    double a[WIN];
+    {
+        // step 0: tile 1's entries (the rows 64 .. 127 of block column 0)
+        const int nc = min(PC, nt), row = TR + lane;
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            const bool ok = row < nt && c < nc;
+            const double x = sc1_load(tv.S + (ok ? row + (size_t)c * nt : 0));
+            a[q] = ok ? x : 0.0;
+        }
+    }
+    for (int t = 0; t < ntb; t++) {
+        const int k0 = t * PC, nc = min(PC, nt - k0), h = nt - k0, c0 = tv.tc + k0;
+        double* panel = tv.S + k0 + (size_t)k0 * nt;
+        const int row = TR + lane;
+        const bool rok = row < h;
+        const bool tile = TR < h;
+        const int nwin = (nc + WIN - 1) / WIN;
+#pragma unroll
+        for (int q = 0; q < WIN; q++) sc1_store(rc.save + PC * PC + (cw0 + q) * PC + lane, a[q]);
+        bool dep_pass = false;
+        for (;;) {
+            passes++;
+            const int pb = WIN * passes;
+            if (w < nwin && tile) {
+                DepState ds{p.sign + c0, S.lv, &S.spec, 0, passes};
+                int* const prog = S.prog + 4;
+                double unused = 0.0;
+                for (int t2 = 0; t2 < w; t2++) {
+                    if (t2 + 1 < w) __builtin_amdgcn_s_setprio(0);
+                    else __builtin_amdgcn_s_setprio(2);
+                    win_apply<false>(a, unused, WIN * t2, lane, cw0, S.Ct, S.Lb, prog + t2, pb);
+                }
+                __builtin_amdgcn_s_setprio(3);
+                CHAIN_STAMP(t, 0);
+                const bool full = cw0 + WIN <= nc;
+                if (dep_pass) {
+                    if (full) win_solve<true, true>(a, cw0, nc, rok, lane, S.Ct, S.Lb, S.dv, S.prog + w, prog + w, ds, pb);
+                    else win_solve<false, true>(a, cw0, nc, rok, lane, S.Ct, S.Lb, S.dv, S.prog + w, prog + w, ds, pb);
+                } else {
+                    if (full) win_solve<true, false>(a, cw0, nc, rok, lane, S.Ct, S.Lb, S.dv, S.prog + w, prog + w, ds, pb);
+                    else win_solve<false, false>(a, cw0, nc, rok, lane, S.Ct, S.Lb, S.dv, S.prog + w, prog + w, ds, pb);
+                }
+                __builtin_amdgcn_s_setprio(0);
+                CHAIN_STAMP(t, 1);
+            }
+            CHAIN_STAMP(t, 2);
+            __syncthreads();
+            const bool tiny = S.tiny == passes;
+            const bool spec = S.spec == passes;
+            __syncthreads();
+            CHAIN_STAMP(t, 3);
+            if (!dep_pass && tiny && tv.dep) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int q = 0; q < WIN; q++) a[q] = sc1_load(rc.save + PC * PC + (cw0 + q) * PC + lane);
+                dep_pass = true;
+                continue;
+            }
+            if (spec || (!dep_pass && tiny)) return;
+            break;
+        }
+        // tile t + 1's rows of L, D of block t; the last half-1 wave whose
+        // stores drained signals the step (pdone, and tile t + 1's rows)
+        if (w < nwin && tile && rok) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) {
+                const int c = cw0 + q;
+                if (c < nc) sc1_store(panel + row + (size_t)c * nt, a[q]);
+            }
+        }
+        if (wv == 4 && lane < nc) sc1_store(p.dg + c0 + lane, S.dv[lane]);
+        if (wv == 5) C.dvp[lane] = S.dv[lane];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int last = 0;
+        if (lane == 0) last = __hip_atomic_fetch_add(&C.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 4 * t + 3;
+        if (__builtin_amdgcn_readfirstlane(last) && lane == 0) {
+            if (tile) __hip_atomic_store(rc.rdone + t * ntb + t + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(rc.pdone + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (t + 2 >= ntb) continue;
+        // tile t + 2 after the visits minus block t's product L(t+2, t) W(t+1, t)':
+        // its rows of block column t from the tile item (t, t + 2)
+        const int k1 = k0 + PC, nc1 = min(PC, nt - k1);
+        wave_poll(rc.rdone + t * ntb + t + 2, 1, rc.abort);
+        const int r2 = (t + 2) * TR + lane;
+        const bool ok2 = r2 < nt;
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const double x = sc1_load(tv.S + (ok2 ? r2 + (size_t)(k0 + cw0 + q) * nt : 0));
+            C.T[cw0 + q][lane] = ok2 ? x : 0.0;
+        }
+        wave_poll(rc.vseq + (t + 2) * ntb + t + 1, run_chunk_count(t + 1, tv.vk, rc.latest), rc.abort);
+        double st[WIN];
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            const bool ok = ok2 && c < nc1;
+            const double x = sc1_load(tv.S + (ok ? r2 + (size_t)(k1 + c) * nt : 0));
+            st[q] = ok ? x : 0.0;
+        }
+        half_sync(&C.hs[1], g1);       // T holds L(t + 2, t); dvp holds D of block t
+        double4_t acc[4];
+#pragma unroll
+        for (int y = 0; y < 4; y++) acc[y] = (double4_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < PC; kk += 4) {
+            const double av = C.T[kk + lk][w * 16 + li];
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                const double bv = S.Lb[kk + lk][y * 16 + li] * C.dvp[kk + lk];
+                acc[y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[y], 0, 0, 0);
+            }
+        }
+        half_sync(&C.hs[1], g1);       // every operand read
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) C.T[y * 16 + li][w * 16 + lk + 4 * i] = acc[y][i];
+        half_sync(&C.hs[1], g1);
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            a[q] = (ok2 && c < nc1) ? st[q] - C.T[c][lane] : 0.0;
+        }
+    }
+}
+
+// the chain item (see above)
+__device__ void chain_body(const PlanView& p, const TailView& tv, const ChainRun& rc, ChainLds& C) {
+    const int tid = threadIdx.x;
+    if (tid < 8) C.P.prog[tid] = 0;
+    if (tid < 4) C.winok[tid] = 0;
+    if (tid == 0) {
+        C.P.tiny = 0;
+        C.P.spec = 0;
+        C.P.ndep = 0;
+        C.hs[0] = C.hs[1] = 0;
+        C.arrive = 0;
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(tid >> 6) >= 4) chain_half1(p, tv, rc, C);
+    else chain_half0(p, tv, rc, C);
+}
+
+// tile item (t, R), R >= t + 2: tile R's rows of block column t.  Waves 4-7
+// solve it (k_panel_w's half 1) against the chain's published windows of
+// block t, which waves 0-3 load into LDS as the chain publishes them; first
+// block t - 1's update of the tile (k_tail_pr's pre-update, tile half: the
+// same fragments, k ascending, old - acc).
+__device__ __attribute__((noinline)) void chain_tile_body(const PlanView& p, const TailView& tv, const ChainRun& rc, int t, int R, char* lds,
+                                int* sh) {
+    PanelLds& S = *reinterpret_cast<PanelLds*>(lds);
+    const int nt = tv.nt, ntb = tv.ntb, tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const bool solver = wv >= 4;
+    const int w = solver ? (wv + 2) & 3 : wv, cw0 = WIN * w;
+    const int k0 = t * PC, c0 = tv.tc + k0;       // block t is full: a tile lies below it
+    const int row = R * TR + lane;
+    const bool rok = row < nt;
+    const int li = lane & 15, lk = lane >> 4;
+    // the visits of this tile are done: its entries
+    if (!chain_wg_wait(rc.vseq + R * ntb + t, run_chunk_count(t, tv.vk, rc.latest), nullptr, 0, rc.abort, sh)) return;
+    double a[WIN];
+#pragma unroll
+    for (int q = 0; q < WIN; q++) {
+        const double x = sc1_load(tv.S + (solver && rok ? row + (size_t)(k0 + cw0 + q) * nt : 0));
+        a[q] = solver && rok ? x : 0.0;
+    }
+    if (t > 0) {
+        // block t - 1's update: the tile's rows of block column t - 1 (tile item
+        // (t - 1, R)) and block t's (the chain), W = L D formed on the load
+        if (!chain_wg_wait(rc.rdone + (t - 1) * ntb + R, 1, rc.rdone + (t - 1) * ntb + t, 1, rc.abort, sh + 1)) return;
+        PreLds& P = *reinterpret_cast<PreLds*>(lds);
+        const int kp = k0 - PC;
+        const double* Lcol = tv.S + (size_t)kp * nt;
+        constexpr int NU = TR * PC / PNT;
+        double vj[NU], vw[NU];
+        const int rr = tid % TR, rd = k0 + rr, rj = R * TR + rr;
+        const bool okj = rj < nt;
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int k = (tid + u * PNT) / TR;
+            const double x = sc1_load(Lcol + rd + (size_t)k * nt);
+            const double y = sc1_load(Lcol + (okj ? rj + (size_t)k * nt : 0));
+            const double dk = sc1_load(p.dg + tv.tc + kp + k);
+            vj[u] = okj ? y : 0.0;
+            vw[u] = x * dk;
+        }
+#pragma unroll
+        for (int u = 0; u < NU; u++) {
+            const int k = (tid + u * PNT) / TR;
+            P.Aj[rr][k] = vj[u];
+            P.Bs[rr][k] = vw[u];
+        }
+        __syncthreads();
+        // 16 fragments over 8 waves: rows fx of the tile, columns fy, fy + 1 of W
+        const int fx = wv & 3, fy0 = 2 * (wv >> 2);
+        double4_t acc[2];
+        acc[0] = acc[1] = (double4_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < PC; kk += 4) {
+            const double av = P.Aj[fx * 16 + li][kk + lk];
+#pragma unroll
+            for (int y = 0; y < 2; y++)
+                acc[y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, P.Bs[(fy0 + y) * 16 + li][kk + lk], acc[y], 0, 0, 0);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int y = 0; y < 2; y++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) P.Ad[(fy0 + y) * 16 + li][fx * 16 + lk + 4 * i] = acc[y][i];
+        __syncthreads();
+        if (solver && rok) {
+#pragma unroll
+            for (int q = 0; q < WIN; q++) a[q] = a[q] - P.Ad[cw0 + q][lane];
+        }
+        __syncthreads();           // the panel's LDS image overwrites P from here
+    }
+    if (tid < 8) S.prog[tid] = 0;
+    if (tid == 0) S.spec = 0;
+    if (tid == 8) S.tiny = 0;      // here: the launch aborted while this item waited for a window
+    __syncthreads();
+    DepState ds{p.sign + c0, S.lv, &S.spec, 0};
+    if (!solver) {
+        // window w of block t, as the chain publishes it (after an abort: the
+        // window is marked and the solve runs on, so that every wave ends)
+        const bool ok = wave_poll(rc.dwin + t * 4 + w, 1, rc.abort);
+        const double* src = rc.dpub + ((size_t)t * 4 + w) * kChainWinPub;
+        double v[WIN];
+#pragma unroll
+        for (int kk = 0; kk < WIN; kk++) v[kk] = ok ? sc1_load(src + kk * PC + lane) : 0.0;
+        double dd = 1.0, mk = 1.0;
+        if (ok && lane < WIN) {
+            dd = sc1_load(src + WIN * PC + lane);
+            mk = sc1_load(src + WIN * PC + WIN + lane);
+        }
+#pragma unroll
+        for (int kk = 0; kk < WIN; kk++) S.Ct[cw0 + kk][lane] = v[kk];
+        if (lane < WIN) {
+            S.dv[cw0 + lane] = dd;
+            S.lv[cw0 + lane] = static_cast<int>(mk);
+        }
+        if (!ok && lane == 0) S.tiny = 1;
+        df_publish(S.prog + w, WIN);
+    } else {
+        double unused = 0.0;
+        for (int t2 = 0; t2 < w; t2++) win_apply<false>(a, unused, WIN * t2, lane, cw0, S.Ct, S.Lb, S.prog + 4 + t2);
+        win_solve<true, true>(a, cw0, PC, rok, lane, S.Ct, S.Lb, S.dv, S.prog + w, S.prog + 4 + w, ds);
+    }
+    __syncthreads();
+    if (S.tiny) return;                 // the launch aborted: nothing of it is used
+    if (S.spec) {                        // a tile entry contradicts a dropped column
+        if (tid == 0) chain_abort(p, rc.abort);
+        return;
+    }
+    if (solver && rok) {
+#pragma unroll
+        for (int q = 0; q < WIN; q++) sc1_store(tv.S + row + (size_t)(k0 + cw0 + q) * nt, a[q]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __hip_atomic_store(rc.rdone + t * ntb + R, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(rc.pdone + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ void __launch_bounds__(PNT)
+k_tail_chain_run(PlanView p, TailView tv, ChainRun rc) {
+    __shared__ __attribute__((aligned(16))) char lds[kChainItemLds];
+    __shared__ int sh_item, sh_ok[2];
+    const int ntb = tv.ntb;
+    if (threadIdx.x == 0) sh_item = __hip_atomic_fetch_add(rc.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int it = sh_item;
+    if (it >= rc.n) return;
+    const uint2 rec = rc.items[it];
+    const int t = rec.y & 0xff, q = (rec.y >> 8) & 0xff;
+    unsigned long long* tr = rc.trace ? rc.trace + 4 * (size_t)it : nullptr;
+    if (tr && threadIdx.x == 0) {
+        tr[0] = __builtin_amdgcn_s_memrealtime();
+        tr[3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+    }
+    if (rec.y & (1u << 30)) {
+        chain_body(p, tv, rc, *reinterpret_cast<ChainLds*>(lds));
+    } else if (rec.y >> 31) {
+        if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
+        chain_tile_body(p, tv, rc, t, static_cast<int>(rec.x), lds, sh_ok);
+    } else {
+        const int bi = rec.x & 255, c = (rec.x >> 8) & 255, b0 = (rec.x >> 16) & 255, b1 = rec.x >> 24;
+        int* vs = rc.vseq + bi * ntb + c;
+        if (!chain_wg_wait(t > 0 ? rc.pdone + t - 1 : nullptr, t > 0 ? chain_target(ntb, t - 1) : 0, q ? vs : nullptr,
+                           q, rc.abort, sh_ok))
             return;
         if (tr && threadIdx.x == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
         visit_tile512<true>(p, tv, bi, c, b0, b1, *reinterpret_cast<SyrkLds*>(lds));
@@ -1837,6 +2482,30 @@ std::vector<uint2> tail_run_schedule(int ntb, int nt, int K, int L, int cap, std
     }
     ptr[ntb] = static_cast<int>(out.size());
     return out;
+}
+
+// Items of k_tail_chain_run: the chain item first, then per launch t the
+// tile items (t, R), R = t + 2 .. ntb - 1 (R = t + 2 first: the chain waits
+// for it), then launch t's visits as tail_run_schedule places them, with
+// room for the chain's CU.
+std::vector<uint2> tail_chain_schedule(int ntb, int nt, int K, int L, int cap, std::vector<int>& ptr) {
+    std::vector<int> rptr;
+    const std::vector<uint2> run = tail_run_schedule(ntb, nt, K, L, cap - 1, rptr);
+    std::vector<uint2> out;
+    out.push_back(make_uint2(0u, 1u << 30));
+    ptr.assign(ntb + 1, 0);
+    for (int t = 0; t < ntb; t++) {
+        ptr[t] = static_cast<int>(out.size());
+        for (int R = t + 2; R < ntb; R++) out.push_back(make_uint2(static_cast<unsigned>(R), static_cast<unsigned>(t) | 1u << 31));
+        for (int i = rptr[t]; i < rptr[t + 1]; i++)
+            if (!(run[i].y >> 31)) out.push_back(run[i]);          // the visits (panels are the chain's now)
+    }
+    ptr[ntb] = static_cast<int>(out.size());
+    return out;
+}
+
+void launch_tail_chain(const PlanView& pv, const TailView& tv, const ChainRun& rc, hipStream_t s) {
+    if (rc.n > 0) hipLaunchKernelGGL(k_tail_chain_run, dim3(rc.n), dim3(PNT), 0, s, pv, tv, rc);
 }
 
 void launch_tail_run(const PlanView& pv, const TailView& tv, const TailRun& rc, hipStream_t s) {

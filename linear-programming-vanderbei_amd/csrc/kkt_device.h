@@ -60,6 +60,29 @@ struct TailRun {
     unsigned long long* trace = nullptr;
 };
 
+// The dense tail as one launch around a chain workgroup (k_tail_chain_run):
+// the chain item factors every diagonal block and solves tile t + 1 of each
+// step, keeping block t's L in LDS for block t + 1's pre-update; tile items
+// solve the other tiles against its published windows; visits as in TailRun.
+// Every counter and flag is zeroed before each launch (chain_zero_ints).
+struct ChainRun {
+    const uint2* items;   // tail_chain_schedule
+    int n;
+    int* ticket;          // [1]
+    int* abort;           // [1] a contradicted speculation / a bail: the host redoes the factorisation
+    int* pdone;           // [ntb] row tiles of block column t final (the chain 1, the tile items 1 each)
+    int* rdone;           // [ntb * ntb] rows of tile R in block column t final (t * ntb + R)
+    int* vseq;            // [ntb * ntb] visits of tile (bi, c) done (bi * ntb + c)
+    int* dwin;            // [ntb * 4] diagonal window w of block t published (t * 4 + w)
+    double* dpub;         // [ntb * 4 * kChainWinPub] the published windows
+    double* save;         // [2 * 64 * 64 + 64] the chain's step inputs (a dependent-pivot rerun)
+    int latest;           // the visit schedule's latest-chunk blocks (tail_run_schedule's L)
+    unsigned long long* trace = nullptr;   // as TailRun::trace
+};
+// ints of ChainRun's counters for ntb block columns (ticket, abort, pdone, rdone, vseq, dwin)
+inline size_t chain_zero_ints(int ntb) { return 2 + ntb + 2 * static_cast<size_t>(ntb) * ntb + 4 * static_cast<size_t>(ntb); }
+constexpr int kChainWinPub = 16 * 64 + 32;   // one window: c = l d of the block rows (16 x 64), d (16), mark (16)
+
 // Device-time phases of the KKT core (timing mode), with the algorithmic
 // work of one occurrence (one factorisation / one substitution sweep).
 // kPhTail: the look-ahead dense-tail factor (k_tail_pr and its repair launches).
@@ -77,6 +100,7 @@ struct KktTimers {
     long redo_where[4] = {0, 0, 0, 0};   // ... by the kernel that bailed (k_panel, k_panel_w sparse / tail, k_panel_s)
     long tail_repairs = 0;    // dense-tail block columns redone in place (look-ahead resumed after them)
     long tail_dep_rounds = 0; // k_tail_dep launches of those repairs
+    long tail_chain_aborts = 0;   // k_tail_chain_run launches aborted (the factorisation redone per step)
 };
 
 // The Q block of ldlt.c's K (ldlt.c:253-256, 391-394) on the y-nodes:
@@ -305,6 +329,15 @@ class KktDevice {
     DevBuf<int> drun_cnt_;             // ticket, pdone[ntb], vseq[ntb * ntb]
     // the run of launches [t0, ntb) (reset: a factorisation's first run, counters zeroed)
     void launch_tail_from(int t0, bool reset);
+    // the dense tail around a chain workgroup (k_tail_chain_run; IPO_HIP_TAIL_CHAIN=0: the run above)
+    bool tail_chain_ = false;
+    bool chain_off_ = false;           // this factorisation is being redone after an aborted chain launch
+    int run_latest_ = kTailVisitLatest;
+    DevBuf<uint2> dchain_items_;
+    int chain_n_ = 0;
+    DevBuf<int> dchain_cnt_;           // chain_zero_ints(ntb) counters
+    DevBuf<double> dchain_pub_, dchain_save_;
+    void launch_tail_chain_run();
     DevBuf<uint64_t> dtail_tasks_, dutasks_;
     DevBuf<double> dW_;
     DevBuf<double> dDepSt_;        // k_tail_dep's block state and per-tile maxima

@@ -3625,11 +3625,27 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             IPO_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
             const char* vl = std::getenv("IPO_HIP_VISIT_LATEST");
             const int latest = vl ? std::max(1, std::atoi(vl)) : kTailVisitLatest;
+            run_latest_ = latest;
             const std::vector<uint2> items =
                 tail_run_schedule(plan_.ntb, plan_.nt, visit_blocks_, latest, cus, run_ptr_);
             drun_items_.upload(items, s);
             drun_cnt_.alloc(1 + plan_.ntb + static_cast<size_t>(plan_.ntb) * plan_.ntb);
             IPO_HIP_CHECK(hipStreamSynchronize(s));   // items is a local
+            // the chain launch (IPO_HIP_TAIL_CHAIN=1, where the tail has tiles
+            // below its blocks; used when TailView::dep == 1, else the run above)
+            const char* tc = std::getenv("IPO_HIP_TAIL_CHAIN");
+            tail_chain_ = plan_.ntb >= 3 && tc && std::atoi(tc) != 0;
+            if (tail_chain_) {
+                std::vector<int> cptr;
+                const std::vector<uint2> citems =
+                    tail_chain_schedule(plan_.ntb, plan_.nt, visit_blocks_, latest, cus, cptr);
+                chain_n_ = static_cast<int>(citems.size());
+                dchain_items_.upload(citems, s);
+                dchain_cnt_.alloc(chain_zero_ints(plan_.ntb));
+                dchain_pub_.alloc(static_cast<size_t>(plan_.ntb) * 4 * kChainWinPub);
+                dchain_save_.alloc(2 * kPanelCols * kPanelCols + kPanelCols);
+                IPO_HIP_CHECK(hipStreamSynchronize(s));
+            }
         }
     }
     if (const char* ts = std::getenv("IPO_HIP_TAIL_SPEC")) tail_spec_ = std::atoi(ts);
@@ -3957,7 +3973,16 @@ void KktDevice::factor_core(const double* dE, const double* dD) {
     // tail costs a single-workgroup partial substitution per block column
     const char* rp = std::getenv("IPO_HIP_TAIL_REPAIR");
     const bool repair = use_panel_ && !xch_ && (!rp || std::atoi(rp) != 0);
-    if (!factor_pass(dE, dD, use_panel_, use_panel_)) {
+    bool ok = factor_pass(dE, dD, use_panel_, use_panel_);
+    if (!ok && (hFlags_[1] & 64)) {
+        // the chain launch aborted (a tile contradicted a dropped column): the
+        // factorisation again with the per-step look-ahead and its repairs
+        tm_.tail_chain_aborts++;
+        chain_off_ = true;
+        ok = factor_pass(dE, dD, use_panel_, use_panel_);
+        chain_off_ = false;
+    }
+    if (!ok) {
         tm_.panel_redos++;
         for (int b = 0; b < 4; b++) tm_.redo_where[b] += (hFlags_[1] >> b) & 1;
         // bit 16: a dependent-pivot pass of the tail failed its check (restore first)
@@ -4039,7 +4064,9 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
         // shards: S = sum of every shard's assembled + gathered tail (exchange.h)
         xsum(tv.S, static_cast<size_t>(plan_.nt) * plan_.nt, RedOp::Sum);
         xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
-        if (tail_fused && tail_run_) {     // one persistent launch (kkt_dense.hip, k_tail_run)
+        if (tail_fused && tail_chain_ && !chain_off_ && tv.dep == 1) {   // kkt_dense.hip, k_tail_chain_run
+            launch_tail_chain_run();
+        } else if (tail_fused && tail_run_) {     // one persistent launch (kkt_dense.hip, k_tail_run)
             launch_tail_from(0, true);
         } else if (tail_fused) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
             // one event pair around the steps (a pair per launch added its
@@ -4145,6 +4172,30 @@ void KktDevice::launch_tail_from(int t0, bool reset) {
     ph_begin(s);
     launch_tail_run(pv, tail_view(), rc, s);
     ph_end(kPhTail, rc.n > 0, s);
+}
+
+// The dense tail around a chain workgroup (kkt_dense.hip, k_tail_chain_run):
+// every counter zeroed, one launch of the whole schedule.
+void KktDevice::launch_tail_chain_run() {
+    hipStream_t s = stream_;
+    const PlanView pv = IPO_VIEW();
+    IPO_HIP_CHECK(hipMemsetAsync(dchain_cnt_.get(), 0, dchain_cnt_.bytes(), s));
+    const int ntb = plan_.ntb;
+    ChainRun rc;
+    rc.items = dchain_items_.get();
+    rc.n = chain_n_;
+    rc.ticket = dchain_cnt_.get();
+    rc.abort = rc.ticket + 1;
+    rc.pdone = rc.ticket + 2;
+    rc.rdone = rc.pdone + ntb;
+    rc.vseq = rc.rdone + static_cast<size_t>(ntb) * ntb;
+    rc.dwin = rc.vseq + static_cast<size_t>(ntb) * ntb;
+    rc.dpub = dchain_pub_.get();
+    rc.save = dchain_save_.get();
+    rc.latest = run_latest_;
+    ph_begin(s);
+    launch_tail_chain(pv, tail_view(), rc, s);
+    ph_end(kPhTail, 1, s);
 }
 
 // The look-ahead dense tail bailed at block column tb (a pivot failed the

@@ -116,6 +116,11 @@ std::vector<unsigned> tail_visit_schedule(int ntb, int nt, int K, int cap, std::
 // ...; launches over `cap` items move first chunks earlier.
 std::vector<uint2> tail_run_schedule(int ntb, int nt, int K, int L, int cap, std::vector<int>& ptr);
 void launch_tail_run(const PlanView& pv, const TailView& tv, const TailRun& rc, hipStream_t s);
+// The chain launch (k_tail_chain_run, kkt_dense.hip): the chain item, then per
+// launch t the tile items (t, R >= t + 2) and the visits of tail_run_schedule
+// (ptr as there; the chain item is item 0, before ptr[0]).
+std::vector<uint2> tail_chain_schedule(int ntb, int nt, int K, int L, int cap, std::vector<int>& ptr);
+void launch_tail_chain(const PlanView& pv, const TailView& tv, const ChainRun& rc, hipStream_t s);
 // algorithmic flops / bytes of every visit of one factorisation
 void tail_visit_work(int ntb, int nt, int K, double& flops, double& bytes);
 // Repair path, block column kb of the dense tail with the dependent-pivot

@@ -51,7 +51,7 @@ class Stats(C.Structure):
         ("flops_update", C.c_double), ("bytes_update", C.c_double),
         ("phase_ms", C.c_double * 8), ("phase_launches", C.c_long * 8), ("phase_count", C.c_long * 8),
         ("phase_flops", C.c_double * 8), ("phase_bytes", C.c_double * 8),
-        ("tail_repairs", C.c_long), ("tail_dep_rounds", C.c_long),
+        ("tail_repairs", C.c_long), ("tail_dep_rounds", C.c_long), ("tail_chain_aborts", C.c_long),
     ]
 
     def as_dict(self) -> dict:

@@ -15,6 +15,8 @@ def main():
     path = sys.argv[1]
     raw = open(path, "rb").read()
     ntb, ni = struct.unpack_from("ii", raw, 0)
+    if ni < 0:
+        return chain(raw, ntb, -ni)
     items = np.frombuffer(raw, np.uint32, 2 * ni, 8).reshape(ni, 2)
     tr = np.frombuffer(raw, np.uint64, 4 * ni, 8 + 8 * ni).reshape(ni, 4).astype(np.float64)
     t0 = tr[:, 0].min()
@@ -47,6 +49,37 @@ def main():
     if "--steps" in sys.argv:
         for t, gap, r0, r1, d1, span in rows:
             print(f"  step {t:3d}: gap {gap:6.2f} ready {r0:8.1f}..{r1:8.1f} done {d1:8.1f} span {span:6.2f}")
+
+
+def chain(raw, ntb, ni):
+    """k_tail_chain_run's trace: items, then one record per step of the chain
+    {step start, passes done, results stored}."""
+    items = np.frombuffer(raw, np.uint32, 2 * ni, 8).reshape(ni, 2)
+    tr = np.frombuffer(raw, np.uint64, 4 * (ni + ntb), 8 + 8 * ni).reshape(ni + ntb, 4).astype(np.float64)
+    t0 = tr[:ni, 0].min()
+    drawn, ready, done = (tr[:ni, 0] - t0) / 100.0, (tr[:ni, 1] - t0) / 100.0, (tr[:ni, 2] - t0) / 100.0
+    steps = (tr[ni:, :3] - t0) / 100.0
+    tile = (items[:, 1] >> 31) == 1
+    vis = ((items[:, 1] >> 30) == 0)
+    print(f"chain run: {ni} items ({tile.sum()} tile items, {vis.sum()} visits); chain ends {steps[-1, 2]:.1f} us, "
+          f"last item done {done.max():.1f} us")
+    span = np.diff(steps[:, 0])
+    print(f"chain steps: mean {span.mean():.2f} us (start->passes {np.mean(steps[:, 1] - steps[:, 0]):.2f}, "
+          f"passes->results {np.mean(steps[:, 2] - steps[:, 1]):.2f}, results->next start "
+          f"{np.mean(steps[1:, 0] - steps[:-1, 2]):.2f})")
+    vdur = done[vis] - ready[vis]
+    print(f"visits: duration mean {vdur.mean():.2f} us, wait mean {(ready[vis] - drawn[vis]).mean():.2f}")
+    tdur = done[tile] - drawn[tile]
+    print(f"tile items: drawn->done mean {tdur.mean():.2f} us")
+    ws = np.frombuffer(raw, np.uint64, ntb * 32, 8 + 8 * ni + 8 * 4 * (ni + ntb)).reshape(ntb, 8, 4).astype(np.float64)
+    if "--steps" in sys.argv:
+        for t in range(ntb):
+            print(f"  step {t:3d}: start {steps[t, 0]:8.1f} passes {steps[t, 1] - steps[t, 0]:6.2f} "
+                  f"results {steps[t, 2] - steps[t, 1]:6.2f}")
+            if t < 6 or t == ntb // 2:
+                for wv in range(8):
+                    e = (ws[t, wv] - t0) / 100.0 - steps[t, 0]
+                    print(f"      wave {wv}: own window {e[0]:7.2f} .. {e[1]:7.2f}, work done {e[2]:7.2f}, barriers {e[3]:7.2f}")
 
 
 if __name__ == "__main__":

@@ -64,18 +64,27 @@ int main(int argc, char** argv) {
     // the persistent run (UB_RUN=1, k_tail_run, latest chunk UB_LATEST blocks):
     // timed as one launch, its pivots and factor compared with the per-step
     // launches' (another grouping of the visits' sums: not bitwise)
-    const bool run = std::getenv("UB_RUN") && std::atoi(std::getenv("UB_RUN")) != 0;
+    // UB_CHAIN=1: the chain launch (k_tail_chain_run) instead of the run
+    const bool chain = std::getenv("UB_CHAIN") && std::atoi(std::getenv("UB_CHAIN")) != 0;
+    const bool run = chain || (std::getenv("UB_RUN") && std::atoi(std::getenv("UB_RUN")) != 0);
     std::vector<int> rptr;
     uint2* ditems = nullptr;
     int* dcnt = nullptr;
+    double *dpub = nullptr, *dsave = nullptr;
+    int ub_latest = 0;
     int cus_run = 0;
     if (run) {
         CK(hipDeviceGetAttribute(&cus_run, hipDeviceAttributeMultiprocessorCount, 0));
         const int latest = std::getenv("UB_LATEST") ? std::atoi(std::getenv("UB_LATEST")) : ipo::kTailVisitLatest;
-        const std::vector<uint2> items = ipo::tail_run_schedule(ntb, nt, tv.vk, latest, cus_run, rptr);
+        const std::vector<uint2> items = chain ? ipo::tail_chain_schedule(ntb, nt, tv.vk, latest, cus_run, rptr)
+                                               : ipo::tail_run_schedule(ntb, nt, tv.vk, latest, cus_run, rptr);
+        if (chain) rptr[ntb] = static_cast<int>(items.size());
+        ub_latest = latest;
         CK(hipMalloc(&ditems, items.size() * sizeof(uint2)));
         CK(hipMemcpy(ditems, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice));
-        CK(hipMalloc(&dcnt, (1 + ntb + ntb * ntb) * sizeof(int)));
+        CK(hipMalloc(&dcnt, ipo::chain_zero_ints(ntb) * sizeof(int)));
+        CK(hipMalloc(&dpub, (size_t)ntb * 4 * ipo::kChainWinPub * sizeof(double)));
+        CK(hipMalloc(&dsave, (2 * 64 * 64 + 64) * sizeof(double)));
         std::printf("persistent run: %zu items, latest chunk %d, items per launch", items.size(), latest);
         for (int t = 0; t < ntb; t++) std::printf(" %d", rptr[t + 1] - rptr[t]);
         std::printf("\n");
@@ -84,11 +93,29 @@ int main(int argc, char** argv) {
     // {drawn, ready, done, xcc}, 100 MHz ticks) with each item's record, binary
     unsigned long long* dtrace = nullptr;
     const char* trace_file = std::getenv("UB_TRACE");
-    if (run && trace_file) CK(hipMalloc(&dtrace, (size_t)rptr[ntb] * 4 * sizeof(unsigned long long)));
+    const size_t trace_n = (size_t)(rptr.empty() ? 0 : rptr[ntb] + ntb) * 4 + (size_t)ntb * 32;
+    if (run && trace_file) CK(hipMalloc(&dtrace, trace_n * sizeof(unsigned long long)));
     auto run_once = [&](hipStream_t st) {
-        CK(hipMemsetAsync(dcnt, 0, (1 + ntb + ntb * ntb) * sizeof(int), st));
-        ipo::TailRun rc{ditems, rptr[ntb], 0, dcnt, dcnt + 1, dcnt + 1 + ntb, dtrace};
-        ipo::launch_tail_run(pv, tv, rc, st);
+        CK(hipMemsetAsync(dcnt, 0, ipo::chain_zero_ints(ntb) * sizeof(int), st));
+        if (chain) {
+            ipo::ChainRun rc;
+            rc.items = ditems;
+            rc.n = rptr[ntb];
+            rc.ticket = dcnt;
+            rc.abort = dcnt + 1;
+            rc.pdone = dcnt + 2;
+            rc.rdone = rc.pdone + ntb;
+            rc.vseq = rc.rdone + ntb * ntb;
+            rc.dwin = rc.vseq + ntb * ntb;
+            rc.dpub = dpub;
+            rc.save = dsave;
+            rc.latest = ub_latest;
+            rc.trace = dtrace;
+            ipo::launch_tail_chain(pv, tv, rc, st);
+        } else {
+            ipo::TailRun rc{ditems, rptr[ntb], 0, dcnt, dcnt + 1, dcnt + 1 + ntb, dtrace};
+            ipo::launch_tail_run(pv, tv, rc, st);
+        }
     };
     std::vector<double> g_step;
     if (run) {      // the per-step launches' pivots and factor, for the comparison
@@ -152,12 +179,12 @@ int main(int argc, char** argv) {
                     same, nt);
         if (dtrace) {
             const size_t ni = rptr[ntb];
-            std::vector<unsigned long long> tr(ni * 4);
+            std::vector<unsigned long long> tr(chain ? trace_n : ni * 4);
             std::vector<uint2> items(ni);
             CK(hipMemcpy(tr.data(), dtrace, tr.size() * 8, hipMemcpyDeviceToHost));
             CK(hipMemcpy(items.data(), ditems, ni * sizeof(uint2), hipMemcpyDeviceToHost));
             FILE* f = std::fopen(trace_file, "wb");
-            const int hdr[2] = {ntb, (int)ni};
+            const int hdr[2] = {ntb, (int)ni * (chain ? -1 : 1)};
             std::fwrite(hdr, 4, 2, f);
             std::fwrite(items.data(), sizeof(uint2), ni, f);
             std::fwrite(tr.data(), 8, tr.size(), f);
