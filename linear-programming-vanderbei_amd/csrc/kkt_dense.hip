@@ -1746,7 +1746,7 @@ __device__ __forceinline__ void chain_half0(const PlanView& p, const TailView& t
                             // an abort the wait falls through: the chain runs on with
                             // garbage to its end, every wave in step, and the host
                             // discards the launch)
-                            wave_poll(rc.vseq + (t + 1) * ntb + t + 1, run_chunk_count(t + 1, tv.vk, rc.latest), rc.abort);
+                            wave_poll(rc.vseq + (t + 1) * ntb + t + 1, (rc.novisit ? 0 : run_chunk_count(t + 1, tv.vk, rc.latest)), rc.abort);
                             chain_load_diag(tv, p, k1, nc1, min(PC, nt - k1), cw0, lane, w, sd, dscl);
                             have_sd = true;
                         }
@@ -1813,7 +1813,7 @@ __device__ __forceinline__ void chain_half0(const PlanView& p, const TailView& t
         // block t + 1: its entries after the visits minus block t's product
         const int k1 = k0 + PC, nc1 = min(PC, nt - k1), h01 = min(PC, nt - k1);
         if (!have_sd) {
-            wave_poll(rc.vseq + (t + 1) * ntb + t + 1, run_chunk_count(t + 1, tv.vk, rc.latest), rc.abort);
+            wave_poll(rc.vseq + (t + 1) * ntb + t + 1, (rc.novisit ? 0 : run_chunk_count(t + 1, tv.vk, rc.latest)), rc.abort);
             chain_load_diag(tv, p, k1, nc1, h01, cw0, lane, w, sd, dscl);
         }
         // the fragments to LDS as [col][row] (Ct is free: every window of block t is done)
@@ -1939,7 +1939,7 @@ __device__ __forceinline__ void chain_half1(const PlanView& p, const TailView& t
             const double x = sc1_load(tv.S + (ok2 ? r2 + (size_t)(k0 + cw0 + q) * nt : 0));
             C.T[cw0 + q][lane] = ok2 ? x : 0.0;
         }
-        wave_poll(rc.vseq + (t + 2) * ntb + t + 1, run_chunk_count(t + 1, tv.vk, rc.latest), rc.abort);
+        wave_poll(rc.vseq + (t + 2) * ntb + t + 1, (rc.novisit ? 0 : run_chunk_count(t + 1, tv.vk, rc.latest)), rc.abort);
         double st[WIN];
 #pragma unroll
         for (int q = 0; q < WIN; q++) {
@@ -2009,7 +2009,7 @@ __device__ __attribute__((noinline)) void chain_tile_body(const PlanView& p, con
     const bool rok = row < nt;
     const int li = lane & 15, lk = lane >> 4;
     // the visits of this tile are done: its entries
-    if (!chain_wg_wait(rc.vseq + R * ntb + t, run_chunk_count(t, tv.vk, rc.latest), nullptr, 0, rc.abort, sh)) return;
+    if (!chain_wg_wait(rc.vseq + R * ntb + t, (rc.novisit ? 0 : run_chunk_count(t, tv.vk, rc.latest)), nullptr, 0, rc.abort, sh)) return;
     double a[WIN];
 #pragma unroll
     for (int q = 0; q < WIN; q++) {

@@ -77,6 +77,7 @@ struct ChainRun {
     double* dpub;         // [ntb * 4 * kChainWinPub] the published windows
     double* save;         // [2 * 64 * 64 + 64] the chain's step inputs (a dependent-pivot rerun)
     int latest;           // the visit schedule's latest-chunk blocks (tail_run_schedule's L)
+    int novisit = 0;      // developer timing only (tools/ubench_tail UB_NOVISIT): the schedule holds no visits
     unsigned long long* trace = nullptr;   // as TailRun::trace
 };
 // ints of ChainRun's counters for ntb block columns (ticket, abort, pdone, rdone, vseq, dwin)

@@ -79,6 +79,13 @@ int main(int argc, char** argv) {
         const std::vector<uint2> items = chain ? ipo::tail_chain_schedule(ntb, nt, tv.vk, latest, cus_run, rptr)
                                                : ipo::tail_run_schedule(ntb, nt, tv.vk, latest, cus_run, rptr);
         if (chain) rptr[ntb] = static_cast<int>(items.size());
+        if (chain && std::getenv("UB_NOVISIT")) {      // timing of the chain and tile items alone (factor wrong)
+            std::vector<uint2> kept;
+            for (const uint2& it : items)
+                if (it.y >> 30) kept.push_back(it);
+            const_cast<std::vector<uint2>&>(items) = kept;
+            rptr[ntb] = static_cast<int>(kept.size());
+        }
         ub_latest = latest;
         CK(hipMalloc(&ditems, items.size() * sizeof(uint2)));
         CK(hipMemcpy(ditems, items.data(), items.size() * sizeof(uint2), hipMemcpyHostToDevice));
@@ -110,6 +117,7 @@ int main(int argc, char** argv) {
             rc.dpub = dpub;
             rc.save = dsave;
             rc.latest = ub_latest;
+            rc.novisit = std::getenv("UB_NOVISIT") ? 1 : 0;
             rc.trace = dtrace;
             ipo::launch_tail_chain(pv, tv, rc, st);
         } else {
