@@ -769,6 +769,7 @@ struct PanelLds {
     int tiny;
     int spec;                             // DEP pass: a tile (or a NaN) contradicts a dropped column
     int ndep;                             // DEP pass: dependent pivots of the block
+    int wverd[4];                         // half 0's window w factored: 1 every pivot passed the zero test, 2 not
 };
 
 // Workgroup `bid` of a windowed panel: fused unit f0 + bid of a sparse level
@@ -808,13 +809,34 @@ struct NoWait {
 struct NoPost {
     __device__ void operator()(bool) const {}
 };
+// Window hand-off of the persistent tail (k_tail_run; pub null: off).  A
+// tile window of step t is final once it is solved and the diagonal windows
+// up to it passed the zero test (a first pass that meets a dependent pivot
+// in window v reruns with DEP, which computes windows before v again with the
+// same operations): half 1's wave publishes it at once -- its 64 rows of L
+// and the window's 16 pivots, sc1 stores, vmcnt(0), then the flag
+// (t, j, w) = epoch -- and the panels of step t + 1 form their pre-update
+// window by window from those of tiles 0 (their diagonal rows) and j + 1
+// (their tile rows): the MFMA k-steps in the same order, so the same
+// products, bitwise the pre-update that reads S once step t is done.  They
+// wait for the whole step t (pdone: every panel done, none bailed) only after
+// their own window chains, before their first global write.  The first step
+// of a run (t0: after a repair, S holds step t0 - 1) reads S.
+struct RunPub {
+    double* pub = nullptr;     // TailRun::pub
+    const int* wflag = nullptr;
+    int* wflag_w = nullptr;
+    int t0 = 0;
+    int epoch = 0;
+};
 
 template <bool DEP = false, bool SC = false, class PreWait = NoWait, class Post = NoPost>
 __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __restrict__ fu_sup,
                                              const int* __restrict__ fu_j, int f0, const TailView& tv, int kb, int bid,
                                              PanelLds& S, double* wtail, bool pre = false,
                                              const int* bailp = nullptr, int bt = 0, int dep = 0,
-                                             PreWait pre_wait = PreWait{}, Post post = Post{}) {
+                                             PreWait pre_wait = PreWait{}, Post post = Post{},
+                                             RunPub rp = RunPub{}) {
     // a bail flag of an earlier step (dense tail, see k_tail_pr): read first,
     // tested once this workgroup's operand loads are in flight
     const int bailed = bailp ? *bailp : 0;
@@ -880,8 +902,10 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
         }
         if (j == 0 && !h1 && lane < nc && (lane >> 4) == w) st_h<SC>(tv.W + lane, dsc);
     }
+    // the pre-update from the previous step's published windows (RunPub)
+    const bool winpub = SC && rp.pub && pre && kb - 1 >= rp.t0;
     if (pre) {
-        if (!pre_wait()) return false;     // workgroup-uniform
+        if (!winpub && !pre_wait()) return false;     // workgroup-uniform
         // dense tail, block column kb > 0: block kb - 1's update of this
         // workgroup's rows, k_tail_syrk's MFMA fragments and order; the
         // entries get old - acc and the pivots' |terms| old + sum_k |l w|,
@@ -890,7 +914,88 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
         const int nt = tv.nt, kp = (kb - 1) * PC;
         const double* Lcol = tv.S + (size_t)kp * nt;
         constexpr int NU = TR * PC / PNT;
-        {
+        // |terms| of the pivots (half 0, the wave's 16 diagonal rows), k in
+        // order, interleaved with the MFMA steps that read the same k
+        const bool holder = !h1 && lane < nc && (lane >> 4) == w;
+        double asum = 0.0;
+        const int wr = (w & 1) * 32, wc = (w >> 1) * 32, li = lane & 15, lk = lane >> 4;
+        double (*Am)[PRS] = h1 ? P.Aj : P.Ad;
+        double4_t acc[2][2];
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 2; y++) acc[x][y] = (double4_t){0.0, 0.0, 0.0, 0.0};
+        auto mfma_k = [&](int kk) {
+            double av[2], bv[2];
+#pragma unroll
+            for (int x = 0; x < 2; x++) av[x] = Am[wr + x * 16 + li][kk + lk];
+#pragma unroll
+            for (int y = 0; y < 2; y++) bv[y] = P.Bs[wc + y * 16 + li][kk + lk];
+#pragma unroll
+            for (int x = 0; x < 2; x++)
+#pragma unroll
+                for (int y = 0; y < 2; y++)
+                    acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+            if (holder) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) asum += fabs(P.Ad[lane][kk + u] * P.Bs[lane][kk + u]);
+            }
+        };
+        if (winpub) {
+            // window by window as step kb - 1 publishes them: its tile 0 holds
+            // this panel's diagonal rows (and the pivots), tile j + 1 its tile rows
+            __shared__ int pub_ok;
+            const int tp = kb - 1, ntb = tv.ntb;
+            const bool hasj = (kb + j + 1) * TR < nt;
+            const double* p0 = rp.pub + (size_t)(tp & 1) * ntb * 4 * kTailPubWin;
+            const double* pj = p0 + (size_t)(j + 1) * 4 * kTailPubWin;
+            const int* f0 = rp.wflag + (size_t)tp * ntb * 4;
+            const int* fj = f0 + (j + 1) * 4;
+            const int rr = tid % TR, rd = kb * TR + rr, rj = (kb + j + 1) * TR + rr;
+            const bool okd = rd < nt, okj = rj < nt;
+            for (int v = 0; v < 4; v++) {
+                if (tid == 0) {
+                    int ok = 1;
+                    for (;;) {
+                        if (sc1_load_int(f0 + v) == rp.epoch && (!hasj || sc1_load_int(fj + v) == rp.epoch)) break;
+                        const int b = sc1_load_int(p.flags + 2);
+                        if (b && b - 1 < bt) {     // an earlier step bailed: its windows may never come
+                            ok = 0;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    pub_ok = ok;
+                }
+                __syncthreads();
+                if (!pub_ok) return false;
+                const double* q0 = p0 + v * kTailPubWin;
+                const double* qj = pj + v * kTailPubWin;
+                constexpr int NW = TR * WIN / PNT;
+                double vd[NW], vj[NW], vw[NW];
+#pragma unroll
+                for (int u = 0; u < NW; u++) {
+                    const int kl = (tid + u * PNT) / TR;
+                    const double x = sc1_load(q0 + (okd ? kl * TR + rr : 0));
+                    const double y = sc1_load(qj + (okj ? kl * TR + rr : 0));
+                    const double dk = sc1_load(q0 + WIN * TR + kl);
+                    vd[u] = okd ? x : 0.0;
+                    vj[u] = okj ? y : 0.0;
+                    vw[u] = okd ? x * dk : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < NW; u++) {
+                    const int k = WIN * v + (tid + u * PNT) / TR;
+                    P.Ad[rr][k] = vd[u];
+                    P.Aj[rr][k] = vj[u];
+                    P.Bs[rr][k] = vw[u];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int kk = WIN * v; kk < WIN * (v + 1); kk += 4) mfma_k(kk);
+            }
+            PANEL_STAMP(3);
+        } else {
             // all 3 NU loads in flight, then into LDS
             double vd[NU], vj[NU], vw[NU];
             const int rr = tid % TR, rd = kb * TR + rr, rj = (kb + j + 1) * TR + rr;
@@ -915,36 +1020,10 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
                 P.Aj[rr][k] = vj[u];
                 P.Bs[rr][k] = vw[u];
             }
-        }
-        __syncthreads();
-        PANEL_STAMP(3);
-        // |terms| of the pivots (half 0, the wave's 16 diagonal rows), k in
-        // order, interleaved with the MFMA steps that read the same k
-        const bool holder = !h1 && lane < nc && (lane >> 4) == w;
-        double asum = 0.0;
-        const int wr = (w & 1) * 32, wc = (w >> 1) * 32, li = lane & 15, lk = lane >> 4;
-        double (*Am)[PRS] = h1 ? P.Aj : P.Ad;
-        double4_t acc[2][2];
+            __syncthreads();
+            PANEL_STAMP(3);
 #pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int y = 0; y < 2; y++) acc[x][y] = (double4_t){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kk = 0; kk < PC; kk += 4) {
-            double av[2], bv[2];
-#pragma unroll
-            for (int x = 0; x < 2; x++) av[x] = Am[wr + x * 16 + li][kk + lk];
-#pragma unroll
-            for (int y = 0; y < 2; y++) bv[y] = P.Bs[wc + y * 16 + li][kk + lk];
-#pragma unroll
-            for (int x = 0; x < 2; x++)
-#pragma unroll
-                for (int y = 0; y < 2; y++)
-                    acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
-            if (holder) {
-#pragma unroll
-                for (int u = 0; u < 4; u++) asum += fabs(P.Ad[lane][kk + u] * P.Bs[lane][kk + u]);
-            }
+            for (int kk = 0; kk < PC; kk += 4) mfma_k(kk);
         }
         PANEL_STAMP(4);
         __syncthreads();                   // every operand read: Ad / Aj take the products, [col][row]
@@ -967,6 +1046,7 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
         PANEL_STAMP(14);
     }
     if (tid < 8) S.prog[tid] = 0;
+    if (tid < 4) S.wverd[tid] = 0;
     if (tid == 0) { tiny_sh = 0; S.spec = dep == 2 ? -1 : 0; S.ndep = 0; }
     __syncthreads();
     DepState ds{p.sign + c0, S.lv, &S.spec, 0};
@@ -998,10 +1078,38 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
             else win_factor<false, DEP>(a, dsc, tz_any, cw0, nc, lane, h0, p.tau, Ct, Lr, dv, prog + w, ds);
             if (tz_any && lane == 0) tiny_sh = 1;
             if (DEP && ds.ndep && lane == 0) atomicAdd(&S.ndep, ds.ndep);
+            if (lane == 0) __hip_atomic_store(S.wverd + w, tz_any ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {
             __builtin_amdgcn_s_setprio(3);
             if (cw0 + WIN <= nc) win_solve<true, DEP>(a, cw0, nc, rok, lane, Ct, Lb, dv, S.prog + w, prog + w, ds);
             else win_solve<false, DEP>(a, cw0, nc, rok, lane, Ct, Lb, dv, S.prog + w, prog + w, ds);
+            if (SC && rp.pub && kb + 1 < tv.ntb) {
+                // hand the window to step kb + 1 (RunPub) once the diagonal
+                // windows up to it passed the zero test (a DEP pass: at once;
+                // its checks decide at the step's end, which the consumers await)
+                bool ok = true;
+                if (!DEP) {
+                    for (int v = 0; v <= w; v++) {
+                        int x;
+                        while ((x = __hip_atomic_load(S.wverd + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0)
+                            __builtin_amdgcn_s_sleep(1);
+                        ok = ok && x == 1;
+                    }
+                }
+                if (ok) {
+                    double* pb = rp.pub + (((size_t)(kb & 1) * tv.ntb + j) * 4 + w) * kTailPubWin;
+                    if (rok) {
+#pragma unroll
+                        for (int q = 0; q < WIN; q++)
+                            if (cw0 + q < nc) sc1_store(pb + q * TR + lane, a[q]);
+                    }
+                    if (lane < WIN) sc1_store(pb + WIN * TR + lane, dv[cw0 + lane]);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane == 0)
+                        __hip_atomic_store(rp.wflag_w + ((size_t)kb * tv.ntb + j) * 4 + w, rp.epoch, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
         }
         __builtin_amdgcn_s_setprio(0);
         PANEL_STAMP(2);
@@ -1026,6 +1134,10 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    // a pre-update from published windows: the whole of step kb - 1 done and
+    // none of it bailed, before anything of this panel is written (a DEP
+    // pass's saves included)
+    if (winpub && !pre_wait()) return false;
     PANEL_STAMP(12);
     if (!DEP && tiny_sh && dep) return true;      // every workgroup of the panel: rerun with DEP
     // DEP: spec < 0 (dep == 2) with a dropped column in the block counts as contradicted
@@ -1492,11 +1604,12 @@ k_tail_run(PlanView p, TailView tv, TailRun rc) {
         auto post = [&](bool bailed) { run_signal(rc.pdone + t, bailed ? 1 + kRunBail : 1); };
         if (tr && threadIdx.x == 0 && t == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
         PanelLds& S = *reinterpret_cast<PanelLds*>(lds);
+        const RunPub rp{rc.pub, rc.wflag, rc.wflag, rc.t0, rc.epoch};
         if (panel_w_body<false, true>(p, nullptr, nullptr, 0, tv, t, j, S, nullptr, t > 0, nullptr, t, tv.dep, pw,
-                                      post)) {
+                                      post, rp)) {
             __syncthreads();           // every wave has read the first pass's verdict
             panel_w_body<true, true>(p, nullptr, nullptr, 0, tv, t, j, S, nullptr, t > 0, nullptr, t, tv.dep, NoWait{},
-                                     post);
+                                     post, rp);
         }
     } else {
         // visit: chunk q of tile (bi, c), once the panels of step t - 1 are done

@@ -55,10 +55,19 @@ struct TailRun {
     int* ticket;
     int* pdone;
     int* vseq;
+    // window hand-off (kkt_dense.hip RunPub; null: off): tile window (t, j, w)
+    // at pub + (((t & 1) ntb + j) 4 + w) kTailPubWin once wflag[(t ntb + j) 4
+    // + w] == epoch (one epoch per launch, never reused: no reset)
+    double* pub = nullptr;
+    int* wflag = nullptr;
+    int epoch = 0;
     // developer trace (tools/ubench_tail UB_TRACE): per item {drawn, ready,
     // done} in s_memrealtime ticks (100 MHz) and the workgroup's XCC id; null: off
     unsigned long long* trace = nullptr;
 };
+
+// one published tile window: 16 columns of 64 rows of L, then the 16 pivots d
+constexpr int kTailPubWin = 16 * 64 + 16;
 
 // The dense tail as one launch around a chain workgroup (k_tail_chain_run):
 // the chain item factors every diagonal block and solves tile t + 1 of each
@@ -328,6 +337,11 @@ class KktDevice {
     DevBuf<uint2> drun_items_;         // tail_run_schedule
     std::vector<int> run_ptr_;         // first item of each launch
     DevBuf<int> drun_cnt_;             // ticket, pdone[ntb], vseq[ntb * ntb]
+    // the run's window hand-off (TailRun::pub; IPO_HIP_TAIL_WINPUB=0: off)
+    bool run_winpub_ = true;
+    DevBuf<double> drun_pub_;          // [2 * ntb * 4 * kTailPubWin]
+    DevBuf<int> drun_wflag_;           // [ntb * ntb * 4], zeroed once
+    int run_epoch_ = 0;
     // the run of launches [t0, ntb) (reset: a factorisation's first run, counters zeroed)
     void launch_tail_from(int t0, bool reset);
     // the dense tail around a chain workgroup (k_tail_chain_run; IPO_HIP_TAIL_CHAIN=0: the run above)

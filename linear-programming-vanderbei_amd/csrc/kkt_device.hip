@@ -3630,6 +3630,17 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
                 tail_run_schedule(plan_.ntb, plan_.nt, visit_blocks_, latest, cus, run_ptr_);
             drun_items_.upload(items, s);
             drun_cnt_.alloc(1 + plan_.ntb + static_cast<size_t>(plan_.ntb) * plan_.ntb);
+            // each step's tile windows handed to the next step's pre-update as
+            // they complete (kkt_dense.hip RunPub; IPO_HIP_TAIL_WINPUB=0: the
+            // pre-update waits for the whole previous step and reads S)
+            const char* wp = std::getenv("IPO_HIP_TAIL_WINPUB");
+            run_winpub_ = !(wp && std::atoi(wp) == 0);
+            if (run_winpub_) {
+                drun_pub_.alloc(2 * static_cast<size_t>(plan_.ntb) * 4 * kTailPubWin);
+                drun_wflag_.alloc(static_cast<size_t>(plan_.ntb) * plan_.ntb * 4);
+                IPO_HIP_CHECK(hipMemsetAsync(drun_wflag_.get(), 0, drun_wflag_.bytes(), s));
+                run_epoch_ = 0;
+            }
             IPO_HIP_CHECK(hipStreamSynchronize(s));   // items is a local
             // the chain launch (IPO_HIP_TAIL_CHAIN=1, where the tail has tiles
             // below its blocks; used when TailView::dep == 1, else the run above)
@@ -4169,6 +4180,15 @@ void KktDevice::launch_tail_from(int t0, bool reset) {
     rc.ticket = drun_cnt_.get();
     rc.pdone = drun_cnt_.get() + 1;
     rc.vseq = drun_cnt_.get() + 1 + plan_.ntb;
+    if (run_winpub_) {
+        if (run_epoch_ == INT_MAX) {      // (never within a process's life: one epoch per factorisation)
+            IPO_HIP_CHECK(hipMemsetAsync(drun_wflag_.get(), 0, drun_wflag_.bytes(), s));
+            run_epoch_ = 0;
+        }
+        rc.pub = drun_pub_.get();
+        rc.wflag = drun_wflag_.get();
+        rc.epoch = ++run_epoch_;
+    }
     ph_begin(s);
     launch_tail_run(pv, tail_view(), rc, s);
     ph_end(kPhTail, rc.n > 0, s);

@@ -64,6 +64,7 @@ int main(int argc, char** argv) {
     // the persistent run (UB_RUN=1, k_tail_run, latest chunk UB_LATEST blocks):
     // timed as one launch, its pivots and factor compared with the per-step
     // launches' (another grouping of the visits' sums: not bitwise)
+    // UB_WINPUB=0: the run without the window hand-off (RunPub)
     // UB_CHAIN=1: the chain launch (k_tail_chain_run) instead of the run
     const bool chain = std::getenv("UB_CHAIN") && std::atoi(std::getenv("UB_CHAIN")) != 0;
     const bool run = chain || (std::getenv("UB_RUN") && std::atoi(std::getenv("UB_RUN")) != 0);
@@ -102,6 +103,15 @@ int main(int argc, char** argv) {
     const char* trace_file = std::getenv("UB_TRACE");
     const size_t trace_n = (size_t)(rptr.empty() ? 0 : rptr[ntb] + ntb) * 4 + (size_t)ntb * 32;
     if (run && trace_file) CK(hipMalloc(&dtrace, trace_n * sizeof(unsigned long long)));
+    double* dwpub = nullptr;
+    int* dwflag = nullptr;
+    int wepoch = 0;
+    if (run && !chain && !(std::getenv("UB_WINPUB") && std::atoi(std::getenv("UB_WINPUB")) == 0)) {
+        CK(hipMalloc(&dwpub, 2 * (size_t)ntb * 4 * ipo::kTailPubWin * sizeof(double)));
+        CK(hipMalloc(&dwflag, (size_t)ntb * ntb * 4 * sizeof(int)));
+        CK(hipMemset(dwflag, 0, (size_t)ntb * ntb * 4 * sizeof(int)));
+        std::printf("window hand-off on\n");
+    }
     auto run_once = [&](hipStream_t st) {
         CK(hipMemsetAsync(dcnt, 0, ipo::chain_zero_ints(ntb) * sizeof(int), st));
         if (chain) {
@@ -121,7 +131,19 @@ int main(int argc, char** argv) {
             rc.trace = dtrace;
             ipo::launch_tail_chain(pv, tv, rc, st);
         } else {
-            ipo::TailRun rc{ditems, rptr[ntb], 0, dcnt, dcnt + 1, dcnt + 1 + ntb, dtrace};
+            ipo::TailRun rc;
+            rc.items = ditems;
+            rc.n = rptr[ntb];
+            rc.t0 = 0;
+            rc.ticket = dcnt;
+            rc.pdone = dcnt + 1;
+            rc.vseq = dcnt + 1 + ntb;
+            if (dwpub) {          // the window hand-off (UB_WINPUB=0: off), as the library's default
+                rc.pub = dwpub;
+                rc.wflag = dwflag;
+                rc.epoch = ++wepoch;
+            }
+            rc.trace = dtrace;
             ipo::launch_tail_run(pv, tv, rc, st);
         }
     };
