@@ -809,6 +809,39 @@ struct NoWait {
 struct NoPost {
     __device__ void operator()(bool) const {}
 };
+// A panel workgroup that bails adds 1 + kRunBail to pdone[t]: a waiter on
+// the panels of step t learns both in one load.
+constexpr int kRunBail = 1 << 16;
+
+// one lane polls until pdone counter c0 (null: none) reaches v0 and vseq
+// counter c1 (null: none) reaches v1; the workgroup joins a barrier and gets
+// false for "skip the item": step t - 1 bailed (c0's bail bit), or, while a
+// counter is short, a panel of a launch before t has bailed (flags[2]: then
+// the counter may never complete)
+__device__ __forceinline__ bool run_wait(const int* c0, int v0, const int* c1, int v1, const int* bailp, int t,
+                                         int* sh) {
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        for (;;) {
+            const int x0 = c0 ? sc1_load_int(c0) : v0;
+            const int x1 = c1 ? sc1_load_int(c1) : v1;
+            if ((x0 & (kRunBail - 1)) >= v0 && x1 >= v1) {
+                ok = x0 < kRunBail;
+                break;
+            }
+            const int b = sc1_load_int(bailp);
+            if (b && b - 1 < t) {
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *sh = ok;
+    }
+    __syncthreads();
+    return *sh != 0;
+}
+
 // Window hand-off of the persistent tail (k_tail_run; pub null: off).  A
 // tile window of step t is final once it is solved and the diagonal windows
 // up to it passed the zero test (a first pass that meets a dependent pivot
@@ -822,12 +855,20 @@ struct NoPost {
 // wait for the whole step t (pdone: every panel done, none bailed) only after
 // their own window chains, before their first global write.  The first step
 // of a run (t0: after a repair, S holds step t0 - 1) reads S.
+// Such a panel also waits for the visits of its own tiles (vd, vt: vseq
+// counters, q chunks each) only after that pre-update's products, right
+// before it loads its own entries: the visits of its column end late in the
+// previous step and gate nothing else.
 struct RunPub {
     double* pub = nullptr;     // TailRun::pub
     const int* wflag = nullptr;
     int* wflag_w = nullptr;
     int t0 = 0;
     int epoch = 0;
+    const int* vd = nullptr;   // the vseq counters of the panel's diagonal tile and tile (null: none)
+    const int* vt = nullptr;
+    int q = 0;
+    int* sh = nullptr;         // run_wait's LDS word
 };
 
 template <bool DEP = false, bool SC = false, class PreWait = NoWait, class Post = NoPost>
@@ -878,32 +919,40 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
     const bool tile = TR * (j + 1) < h;             // workgroup has tile rows
     const int nwin = (nc + WIN - 1) / WIN;
     double a[WIN];
-#pragma unroll
-    for (int q = 0; q < WIN; q++) {
-        const int c = cw0 + q;
-        const bool ok = rok && c < nc && (h1 || c <= row);
-        const double t = ld_h<SC>(panel + (ok ? row + (size_t)c * ld : 0));
-        a[q] = ok ? t : 0.0;
-    }
     // |terms| of the pivots of this wave's window (half 0; lane r <-> (r, r))
-    double dsc = (!h1 && lane < nc && (lane >> 4) == w) ? ld_h<SC>(p.dscale + c0 + lane) : 0.0;
+    double dsc = 0.0;
+    auto load_own = [&]() {
+#pragma unroll
+        for (int q = 0; q < WIN; q++) {
+            const int c = cw0 + q;
+            const bool ok = rok && c < nc && (h1 || c <= row);
+            const double t = ld_h<SC>(panel + (ok ? row + (size_t)c * ld : 0));
+            a[q] = ok ? t : 0.0;
+        }
+        dsc = (!h1 && lane < nc && (lane >> 4) == w) ? ld_h<SC>(p.dscale + c0 + lane) : 0.0;
+    };
+    auto dep_save = [&]() {
+        if (DEP && !fu_sup) {
+            // what this pass may overwrite, saved for k_tail_restore: the tile
+            // rows (rows >= 64 of the block column, as in S) and workgroup 0's
+            // |terms| of the block's pivots (rows 0..nc-1 of W's column 0)
+            if (h1 && rok && tile) {
+#pragma unroll
+                for (int q = 0; q < WIN; q++) {
+                    const int c = cw0 + q;
+                    if (c < nc) st_h<SC>(tv.W + row + (size_t)c * tv.nt, a[q]);
+                }
+            }
+            if (j == 0 && !h1 && lane < nc && (lane >> 4) == w) st_h<SC>(tv.W + lane, dsc);
+        }
+    };
+    // the pre-update from the previous step's published windows (RunPub):
+    // the own entries are loaded after its products
+    const bool winpub = SC && rp.pub && pre && kb - 1 >= rp.t0;
+    if (!winpub) load_own();
     double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
     if (!pre && bailed && bailed - 1 < bt) return false;
-    if (DEP && !fu_sup) {
-        // what this pass may overwrite, saved for k_tail_restore: the tile
-        // rows (rows >= 64 of the block column, as in S) and workgroup 0's
-        // |terms| of the block's pivots (rows 0..nc-1 of W's column 0)
-        if (h1 && rok && tile) {
-#pragma unroll
-            for (int q = 0; q < WIN; q++) {
-                const int c = cw0 + q;
-                if (c < nc) st_h<SC>(tv.W + row + (size_t)c * tv.nt, a[q]);
-            }
-        }
-        if (j == 0 && !h1 && lane < nc && (lane >> 4) == w) st_h<SC>(tv.W + lane, dsc);
-    }
-    // the pre-update from the previous step's published windows (RunPub)
-    const bool winpub = SC && rp.pub && pre && kb - 1 >= rp.t0;
+    if (!winpub) dep_save();
     if (pre) {
         if (!winpub && !pre_wait()) return false;     // workgroup-uniform
         // dense tail, block column kb > 0: block kb - 1's update of this
@@ -995,6 +1044,11 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
                 for (int kk = WIN * v; kk < WIN * (v + 1); kk += 4) mfma_k(kk);
             }
             PANEL_STAMP(3);
+            // the visits of this panel's tiles, then its own entries (and a
+            // DEP pass's saves of them)
+            if (!run_wait(rp.vd, rp.q, rp.vt, rp.q, p.flags + 2, bt, rp.sh)) return false;
+            load_own();
+            dep_save();
         } else {
             // all 3 NU loads in flight, then into LDS
             double vd[NU], vj[NU], vw[NU];
@@ -1526,39 +1580,6 @@ __host__ __device__ __forceinline__ int run_chunk_count(int c, int K, int L) {
     return c <= 1 ? 0 : 1 + (max(0, c - 1 - L) + K - 1) / K;
 }
 
-// A panel workgroup that bails adds 1 + kRunBail to pdone[t]: a waiter on
-// the panels of step t learns both in one load.
-constexpr int kRunBail = 1 << 16;
-
-// one lane polls until pdone counter c0 (null: none) reaches v0 and vseq
-// counter c1 (null: none) reaches v1; the workgroup joins a barrier and gets
-// false for "skip the item": step t - 1 bailed (c0's bail bit), or, while a
-// counter is short, a panel of a launch before t has bailed (flags[2]: then
-// the counter may never complete)
-__device__ __forceinline__ bool run_wait(const int* c0, int v0, const int* c1, int v1, const int* bailp, int t,
-                                         int* sh) {
-    if (threadIdx.x == 0) {
-        int ok = 1;
-        for (;;) {
-            const int x0 = c0 ? sc1_load_int(c0) : v0;
-            const int x1 = c1 ? sc1_load_int(c1) : v1;
-            if ((x0 & (kRunBail - 1)) >= v0 && x1 >= v1) {
-                ok = x0 < kRunBail;
-                break;
-            }
-            const int b = sc1_load_int(bailp);
-            if (b && b - 1 < t) {
-                ok = 0;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        *sh = ok;
-    }
-    __syncthreads();
-    return *sh != 0;
-}
-
 __device__ __forceinline__ void run_signal(int* cnt, int v = 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1593,7 +1614,10 @@ k_tail_run(PlanView p, TailView tv, TailRun rc) {
         const int j = rec.x;
         const int* vd = q ? rc.vseq + t * ntb + t : nullptr;
         const int* vt = q && t + j + 1 < ntb ? rc.vseq + (t + j + 1) * ntb + t : nullptr;
-        if (!run_wait(vd, q, vt, q, bailp, t, &sh_ok)) return;
+        // (with the window hand-off the panel waits for them itself, after
+        // its pre-update's products: RunPub)
+        const bool winpub = rc.pub && t > 0 && t - 1 >= rc.t0;
+        if (!winpub && !run_wait(vd, q, vt, q, bailp, t, &sh_ok)) return;
         // (the first step of a run resumed after a repair waits for nothing
         // before it: the repair's launches came first)
         auto pw = [&]() {
@@ -1604,7 +1628,7 @@ k_tail_run(PlanView p, TailView tv, TailRun rc) {
         auto post = [&](bool bailed) { run_signal(rc.pdone + t, bailed ? 1 + kRunBail : 1); };
         if (tr && threadIdx.x == 0 && t == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
         PanelLds& S = *reinterpret_cast<PanelLds*>(lds);
-        const RunPub rp{rc.pub, rc.wflag, rc.wflag, rc.t0, rc.epoch};
+        const RunPub rp{rc.pub, rc.wflag, rc.wflag, rc.t0, rc.epoch, vd, vt, q, &sh_ok};
         if (panel_w_body<false, true>(p, nullptr, nullptr, 0, tv, t, j, S, nullptr, t > 0, nullptr, t, tv.dep, pw,
                                       post, rp)) {
             __syncthreads();           // every wave has read the first pass's verdict
