@@ -1650,7 +1650,8 @@ k_tail_run(PlanView p, TailView tv, TailRun rc) {
 }
 
 // ------------------------------- dense tail: one launch around a chain workgroup
-// k_tail_chain_run (default path of the look-ahead tail): the steps of the
+// k_tail_chain_run (opt-in, IPO_HIP_TAIL_CHAIN=1; slower than k_tail_run, DESIGN.md
+// section 6.3): the steps of the
 // look-ahead factorisation as ticketed items of one launch, like k_tail_run,
 // but the critical path -- diagonal block t, the tile t + 1 below it, block t
 // + 1's pre-update by block t -- stays inside ONE long-lived workgroup (the
