@@ -85,6 +85,17 @@ k_assemble_diag(int T, int m, const int* __restrict__ perm, const double* __rest
     live[v] = 1;
 }
 
+// The dense tail's lower block triangle zeroed (column c from the first row
+// of its diagonal block on): nothing reads the tail above its diagonal
+// blocks (gathers, visits and panels write tiles bi >= bj, the sweeps read
+// those and the diagonal blocks' upper slots), so the factorisation's clear
+// skips that half of the nt x nt block.  One workgroup per column.
+__global__ void __launch_bounds__(NT) k_zero_tail_lower(double* __restrict__ S, int nt) {
+    const int c = blockIdx.x;
+    double* col = S + (size_t)c * nt;
+    for (int r = (c / kPanelCols) * kPanelCols + static_cast<int>(threadIdx.x); r < nt; r += NT) col[r] = 0.0;
+}
+
 // ------------------------------------------------------- left-looking gather
 // out(r, c) -= sum_tasks sum_k L(row, k) * (d_k * L(col, k))     (ldlt.c:572,583)
 // for one 64-row x (<= 64)-column output tile.  The inner dimension is the
@@ -2150,7 +2161,7 @@ k_tail_bwd_pair(PlanView p, TailView tv, SweepVecs V, const double* __restrict__
 // Residency: a helper waits only on z the lead publishes, the lead only on
 // helpers' partials over earlier z -- acyclic while the grid (<= ntb
 // workgroups, one per CU by the dynamic LDS) is resident.
-constexpr int kLeadBlocks = 2;
+constexpr int kLeadBlocks = 2;     // K = 1 measured: forward sweep 380 -> 387 us (helpers' partials late)
 // developer stamps (-DIPO_LEAD_STAMPS; compiled out otherwise): one launch's
 // per-step split printed from the device
 #ifdef IPO_LEAD_STAMPS
@@ -4023,7 +4034,14 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
     if (timing_) IPO_HIP_CHECK(hipEventRecord(ev0_, s));
     const PlanView pv = IPO_VIEW();
     const int nz = static_cast<int>(plan_.amap.size());
-    IPO_HIP_CHECK(hipMemsetAsync(dLx_.get(), 0, dLx_.bytes(), s));
+    if (plan_.nt > 0 && !xch_) {
+        // the sparse panels, then the tail's lower block triangle only (the
+        // sharded solve sums the whole tail across shards: cleared whole)
+        if (plan_.off_tail > 0) IPO_HIP_CHECK(hipMemsetAsync(dLx_.get(), 0, plan_.off_tail * sizeof(double), s));
+        hipLaunchKernelGGL(k_zero_tail_lower, dim3(plan_.nt), dim3(NT), 0, s, dLx_.get() + plan_.off_tail, plan_.nt);
+    } else {
+        IPO_HIP_CHECK(hipMemsetAsync(dLx_.get(), 0, dLx_.bytes(), s));
+    }
     if (nz > 0) hipLaunchKernelGGL(k_assemble_A, dim3(ceil_div(nz, NT)), dim3(NT), 0, s, nz, dA_.get(), damap_.get(), dLx_.get());
     if (qnz_ > 0)
         hipLaunchKernelGGL(k_assemble_Q, dim3(ceil_div(qnz_, NT)), dim3(NT), 0, s, qnz_, dQ_.get(), dqmap_.get(),

@@ -23,6 +23,9 @@ def main():
         status, text, st = ipo_amd.run_mps(mps_path(name), meth, timing=True)
         print("\n".join(text.splitlines()[-3:]))
         print(status, {k: st[k] for k in sorted(st) if not isinstance(st[k], (list, dict))}, flush=True)
+        if isinstance(st.get("phase_ms"), (list, tuple)) and isinstance(st.get("phase_count"), (list, tuple)):
+            print("phases (us per occurrence):", {ph: round(1e3 * ms / max(1, n), 1) for ph, ms, n in
+                                                  zip(ipo_amd.PHASES, st["phase_ms"], st["phase_count"]) if n})
 
 
 if __name__ == "__main__":
