@@ -243,6 +243,16 @@ int ipo_hip_synth_block_angular(int nblocks, int mb, int nb, int per_col, int ba
                                 unsigned long long seed, int *m, int *n, int *nz, int *kA, int *iA, double *A,
                                 double *b, double *c, double *xs, double *ys, double *ws, double *zs);
 
+/* The persistent dense tail's work-item schedule (host-only; test entry, no
+ * reference counterpart): kind 0 k_tail_run's (kkt_dense.hip
+ * tail_run_schedule), 1 k_tail_chain_run's, for a tail of nt columns, visit
+ * chunks of K blocks, latest chunk L, at most cap workgroups per launch.
+ * items[2 i], items[2 i + 1] = item i's (x, y) words, ptr[t] = first item of
+ * launch t (ntb + 1 entries, ntb = ceil(nt / 64)); either may be NULL.
+ * Returns the item count (items are written up to max_items), or -1
+ * (ipo_hip_last_error). */
+int ipo_hip_tail_schedule(int kind, int nt, int K, int L, int cap, unsigned *items, int max_items, int *ptr);
+
 int ipo_hip_device_count(void);
 /* hipDeviceSynchronize on the calling thread's device (bench.py brackets its
  * timed region with it); 0 on success. */

@@ -17,6 +17,12 @@
 #include "lp_io.h"
 #include "synth.h"
 
+namespace ipo {
+// kkt_dense.hip (declared in kkt_kernels.h, which holds device code)
+std::vector<uint2> tail_run_schedule(int ntb, int nt, int K, int L, int cap, std::vector<int>& ptr);
+std::vector<uint2> tail_chain_schedule(int ntb, int nt, int K, int L, int cap, std::vector<int>& ptr);
+}  // namespace ipo
+
 namespace {
 
 thread_local std::string g_err;
@@ -729,6 +735,28 @@ int ipo_hip_vector_bench(int m, int n, const int* kA, const int* iA, const doubl
     try {
         ipo::vector_bench(m, n, kA, iA, A, reps, ms3, bytes3);
         return 0;
+    } catch (const std::exception& e) {
+        set_err(e.what());
+        return -1;
+    }
+}
+
+int ipo_hip_tail_schedule(int kind, int nt, int K, int L, int cap, unsigned* items, int max_items, int* ptr) {
+    try {
+        if (nt <= 0 || K <= 0 || L <= 0 || cap <= 1 || (kind != 0 && kind != 1))
+            throw std::invalid_argument("tail_schedule: bad arguments");
+        const int ntb = (nt + ipo::kPanelCols - 1) / ipo::kPanelCols;
+        std::vector<int> pv;
+        const std::vector<uint2> v = kind == 0 ? ipo::tail_run_schedule(ntb, nt, K, L, cap, pv)
+                                               : ipo::tail_chain_schedule(ntb, nt, K, L, cap, pv);
+        const int n = static_cast<int>(v.size());
+        if (items)
+            for (int i = 0; i < std::min(n, max_items); i++) {
+                items[2 * i] = v[i].x;
+                items[2 * i + 1] = v[i].y;
+            }
+        if (ptr) std::copy(pv.begin(), pv.end(), ptr);
+        return n;
     } catch (const std::exception& e) {
         set_err(e.what());
         return -1;
