@@ -23,10 +23,15 @@ namespace ipo {
 // Device view of the dense tail (see kkt_plan.h): S = nt x nt column-major.
 // Blocks per visit of the look-ahead dense tail (kkt_dense.hip, visit_hi):
 // IPO_HIP_VISIT_BLOCKS overrides.
-constexpr int kTailVisitBlocks = 6;     // measured on dfl001's tail: 4 -> 2.43 ms, 6 -> 2.26, 8 -> 2.55
+// Measured on dfl001's tail (tools/ubench_tail): per-step launches (round 4)
+// 4 -> 2.43 ms, 6 -> 2.26, 8 -> 2.55; the persistent run with the window
+// hand-off (round 6, latest chunk L in brackets) 3 -> 1.92 (3), 4 -> 1.79
+// (4), 5 -> 1.80 (2-4), 6 -> 1.85 (2), 7 -> 1.96, 8 -> 2.08
+constexpr int kTailVisitBlocks = 4;
 // the persistent tail's latest chunk per column (tail_run_schedule): it must
-// finish within one step (IPO_HIP_VISIT_LATEST overrides)
-constexpr int kTailVisitLatest = 2;
+// finish within one step (IPO_HIP_VISIT_LATEST overrides); equal to the
+// chunk, every tile receives the per-step launches' chunks (bitwise them)
+constexpr int kTailVisitLatest = 4;
 struct TailView {
     double* S;
     int nt, ntb, tc;

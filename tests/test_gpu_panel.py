@@ -213,13 +213,24 @@ def test_tail_run_bitwise(name):
     """The dense tail as one persistent launch (k_tail_run, default: ticketed
     panel and visit items, per-step and per-tile counters) against one launch
     per look-ahead step (IPO_HIP_TAIL_RUN=0), both with the per-step launches'
-    visit chunks (IPO_HIP_VISIT_LATEST=6: every tile receives the same chunks
-    of blocks in the same order): identical HSD solves (trace and final
-    values) -- the hand-offs inside the launch deliver what the launch
-    boundaries did.  dfl001's solve also takes the run's bail and resumed-run
-    path (dependent pivots the in-panel pass leaves to the host)."""
-    six = (("IPO_HIP_VISIT_LATEST", "6"),)
-    assert _solve_env("IPO_HIP_TAIL_RUN", "0", name, extra=six) == _solve_env("IPO_HIP_TAIL_RUN", "1", name, extra=six)
+    visit chunks (the run's latest chunk equal to the chunk, the default
+    K = L = 4, pinned here: every tile receives the same chunks of blocks in
+    the same order): identical HSD solves (trace and final values) -- the
+    hand-offs inside the launch, the window hand-off between steps included,
+    deliver what the launch boundaries did."""
+    kl = (("IPO_HIP_VISIT_BLOCKS", "4"), ("IPO_HIP_VISIT_LATEST", "4"))
+    assert _solve_env("IPO_HIP_TAIL_RUN", "0", name, extra=kl) == _solve_env("IPO_HIP_TAIL_RUN", "1", name, extra=kl)
+
+
+@pytest.mark.parametrize("name", ["dfl001", "greenbea"])
+def test_tail_window_handoff_bitwise(name):
+    """The run's window hand-off (RunPub, default: step t + 1's pre-update
+    formed window by window from the tile windows step t publishes as they
+    complete, the wait for the whole of step t moved after its window chains)
+    against the pre-update that waits for step t and reads S
+    (IPO_HIP_TAIL_WINPUB=0): the same MFMA k-steps in the same order,
+    identical HSD solves."""
+    assert _solve_env("IPO_HIP_TAIL_WINPUB", "0", name) == _solve_env("IPO_HIP_TAIL_WINPUB", "1", name)
 
 
 def test_tail_run_resume_bitwise():
@@ -227,7 +238,7 @@ def test_tail_run_resume_bitwise():
     dependent pivot of the tail goes to the host repair, which resumes the
     run after the bailed block column with its counters kept) against the
     per-step launches' repair: identical dfl001 HSD solves."""
-    ext = (("IPO_HIP_VISIT_LATEST", "6"), ("IPO_HIP_TAIL_SPEC", "0"))
+    ext = (("IPO_HIP_VISIT_BLOCKS", "4"), ("IPO_HIP_VISIT_LATEST", "4"), ("IPO_HIP_TAIL_SPEC", "0"))
     a = _solve_env("IPO_HIP_TAIL_RUN", "0", extra=ext)
     b = _solve_env("IPO_HIP_TAIL_RUN", "1", extra=ext)
     assert a == b
