@@ -76,6 +76,7 @@ int main(int argc, char** argv) {
     int cus_run = 0;
     if (run) {
         CK(hipDeviceGetAttribute(&cus_run, hipDeviceAttributeMultiprocessorCount, 0));
+        if (const char* cp = std::getenv("UB_CAP")) cus_run = std::atoi(cp);   // the schedule's items per launch
         const int latest = std::getenv("UB_LATEST") ? std::atoi(std::getenv("UB_LATEST")) : ipo::kTailVisitLatest;
         const std::vector<uint2> items = chain ? ipo::tail_chain_schedule(ntb, nt, tv.vk, latest, cus_run, rptr)
                                                : ipo::tail_run_schedule(ntb, nt, tv.vk, latest, cus_run, rptr);
