@@ -855,6 +855,16 @@ __device__ __forceinline__ bool run_wait(const int* c0, int v0, const int* c1, i
 // wait for the whole step t (pdone: every panel done, none bailed) only after
 // their own window chains, before their first global write.  The first step
 // of a run (t0: after a repair, S holds step t0 - 1) reads S.
+__device__ __forceinline__ void run_signal(int* cnt, int v = 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The buffer of step t's windows (t & 1) takes step t + 2's next: a panel
+// of step t counts itself in pread[t] once it has read step t - 1's
+// windows, and step t + 1's half-1 waves wait for that count before they
+// publish into it (a DEP pass reads S, not the buffer).
 // Such a panel also waits for the visits of its own tiles (vd, vt: vseq
 // counters, q chunks each) only after that pre-update's products, right
 // before it loads its own entries: the visits of its column end late in the
@@ -863,6 +873,7 @@ struct RunPub {
     double* pub = nullptr;     // TailRun::pub
     const int* wflag = nullptr;
     int* wflag_w = nullptr;
+    int* pread = nullptr;      // TailRun::pread
     int t0 = 0;
     int epoch = 0;
     const int* vd = nullptr;   // the vseq counters of the panel's diagonal tile and tile (null: none)
@@ -948,7 +959,9 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
     };
     // the pre-update from the previous step's published windows (RunPub):
     // the own entries are loaded after its products
-    const bool winpub = SC && rp.pub && pre && kb - 1 >= rp.t0;
+    // (not in a DEP pass: step kb - 1 is complete by then and S holds it --
+    // the same values; its buffer may already take step kb + 1's windows)
+    const bool winpub = !DEP && SC && rp.pub && pre && kb - 1 >= rp.t0;
     if (!winpub) load_own();
     double dsc_pre = 0.0;                  // pivot |terms| after the pre-update (stored once the panel holds)
     if (!pre && bailed && bailed - 1 < bt) return false;
@@ -1043,6 +1056,7 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
 #pragma unroll
                 for (int kk = WIN * v; kk < WIN * (v + 1); kk += 4) mfma_k(kk);
             }
+            run_signal(rp.pread + kb);     // step kb - 1's windows read (their loads complete)
             PANEL_STAMP(3);
             // the visits of this panel's tiles, then its own entries (and a
             // DEP pass's saves of them)
@@ -1149,6 +1163,22 @@ __device__ __forceinline__ bool panel_w_body(const PlanView& p, const int* __res
                             __builtin_amdgcn_s_sleep(1);
                         ok = ok && x == 1;
                     }
+                }
+                // the buffer's previous windows (step kb - 2's) read by every
+                // panel of step kb - 1 that took them (kb - 1 > t0)
+                if (ok && kb - 1 > rp.t0) {
+                    const int need = max(1, (tv.nt - (kb - 1) * PC + TR - 1) / TR - 1);   // tail_gp(nt, kb - 1)
+                    int got = 0;
+                    if (lane == 0) {
+                        for (;;) {
+                            got = sc1_load_int(rp.pread + kb - 1);
+                            if (got >= need) break;
+                            const int b = sc1_load_int(p.flags + 2);
+                            if (b && b - 1 < kb) break;        // the launch is being abandoned
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
+                    ok = __builtin_amdgcn_readfirstlane(got) >= need;
                 }
                 if (ok) {
                     double* pb = rp.pub + (((size_t)(kb & 1) * tv.ntb + j) * 4 + w) * kTailPubWin;
@@ -1580,11 +1610,6 @@ __host__ __device__ __forceinline__ int run_chunk_count(int c, int K, int L) {
     return c <= 1 ? 0 : 1 + (max(0, c - 1 - L) + K - 1) / K;
 }
 
-__device__ __forceinline__ void run_signal(int* cnt, int v = 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 __global__ void __launch_bounds__(PNT)
 k_tail_run(PlanView p, TailView tv, TailRun rc) {
@@ -1628,7 +1653,7 @@ k_tail_run(PlanView p, TailView tv, TailRun rc) {
         auto post = [&](bool bailed) { run_signal(rc.pdone + t, bailed ? 1 + kRunBail : 1); };
         if (tr && threadIdx.x == 0 && t == 0) tr[1] = __builtin_amdgcn_s_memrealtime();
         PanelLds& S = *reinterpret_cast<PanelLds*>(lds);
-        const RunPub rp{rc.pub, rc.wflag, rc.wflag, rc.t0, rc.epoch, vd, vt, q, &sh_ok};
+        const RunPub rp{rc.pub, rc.wflag, rc.wflag, rc.pread, rc.t0, rc.epoch, vd, vt, q, &sh_ok};
         if (panel_w_body<false, true>(p, nullptr, nullptr, 0, tv, t, j, S, nullptr, t > 0, nullptr, t, tv.dep, pw,
                                       post, rp)) {
             __syncthreads();           // every wave has read the first pass's verdict

@@ -65,6 +65,7 @@ struct TailRun {
     // + w] == epoch (one epoch per launch, never reused: no reset)
     double* pub = nullptr;
     int* wflag = nullptr;
+    int* pread = nullptr;     // [ntb] panels of step t done reading step t - 1's windows
     int epoch = 0;
     // developer trace (tools/ubench_tail UB_TRACE): per item {drawn, ready,
     // done} in s_memrealtime ticks (100 MHz) and the workgroup's XCC id; null: off
@@ -341,7 +342,7 @@ class KktDevice {
     bool tail_run_ = false;
     DevBuf<uint2> drun_items_;         // tail_run_schedule
     std::vector<int> run_ptr_;         // first item of each launch
-    DevBuf<int> drun_cnt_;             // ticket, pdone[ntb], vseq[ntb * ntb]
+    DevBuf<int> drun_cnt_;             // ticket, pdone[ntb], vseq[ntb * ntb], pread[ntb]
     // the run's window hand-off (TailRun::pub; IPO_HIP_TAIL_WINPUB=0: off)
     bool run_winpub_ = true;
     DevBuf<double> drun_pub_;          // [2 * ntb * 4 * kTailPubWin]

@@ -3640,7 +3640,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
             const std::vector<uint2> items =
                 tail_run_schedule(plan_.ntb, plan_.nt, visit_blocks_, latest, cus, run_ptr_);
             drun_items_.upload(items, s);
-            drun_cnt_.alloc(1 + plan_.ntb + static_cast<size_t>(plan_.ntb) * plan_.ntb);
+            drun_cnt_.alloc(1 + plan_.ntb + static_cast<size_t>(plan_.ntb) * plan_.ntb + plan_.ntb);
             // each step's tile windows handed to the next step's pre-update as
             // they complete (kkt_dense.hip RunPub; IPO_HIP_TAIL_WINPUB=0: the
             // pre-update waits for the whole previous step and reads S)
@@ -4205,6 +4205,9 @@ void KktDevice::launch_tail_from(int t0, bool reset) {
         }
         rc.pub = drun_pub_.get();
         rc.wflag = drun_wflag_.get();
+        rc.pread = rc.vseq + static_cast<size_t>(plan_.ntb) * plan_.ntb;
+        // a resumed run: steps >= t0 count their readers afresh
+        if (!reset) IPO_HIP_CHECK(hipMemsetAsync(rc.pread + t0, 0, (plan_.ntb - t0) * sizeof(int), s));
         rc.epoch = ++run_epoch_;
     }
     ph_begin(s);

@@ -142,6 +142,7 @@ int main(int argc, char** argv) {
             if (dwpub) {          // the window hand-off (UB_WINPUB=0: off), as the library's default
                 rc.pub = dwpub;
                 rc.wflag = dwflag;
+                rc.pread = dcnt + 1 + ntb + ntb * ntb;
                 rc.epoch = ++wepoch;
             }
             rc.trace = dtrace;
