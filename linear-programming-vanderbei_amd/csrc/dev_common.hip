@@ -55,11 +55,11 @@ k_finish_reduce_pack(const double* __restrict__ part, int nq, unsigned maxmask, 
 }
 
 // dotprod() of linalg.c:17-25 in its own order: one running sum, i = 0..n-1.
-// One 256-thread block per job: the products of a chunk are formed by the
-// whole block into LDS (eight loads in flight per thread), then one lane
-// adds them in index order with its LDS reads one 16-value batch ahead of
-// the adds, so that only the dependent adds remain on the chain.  Max-type
-// jobs are order-free.
+// One 256-thread block per job: one wave forms a chunk's products (eight
+// loads in flight per lane) and compacts them into LDS while one lane adds
+// the previous chunk's in index order, its LDS reads one 16-value batch
+// ahead of the adds, so that only the dependent adds remain on the chain.
+// Max-type jobs are order-free.
 constexpr int kOrdThreads = 256;
 
 __global__ void __launch_bounds__(kOrdThreads)
@@ -96,77 +96,80 @@ k_reduce_ordered(RedJobs jobs, double* __restrict__ out) {
     }
     // Zero products leave the running sum unchanged: it starts at +0, and a
     // sum of round-to-nearest adds is never -0 unless it adds -0 to -0, so
-    // s + (+-0) == s at every step.  The block compacts each chunk's
-    // non-zero products in index order (thread t scans a contiguous
-    // segment; an exclusive scan of the segments' counts places them), and
-    // lane 0's chain only adds those: the same sum, bit for bit (NaN
-    // products are not zero and stay), over half the chain on dfl001's
-    // b'y and c'x (27 / 51 % of b / c non-zero).
+    // s + (+-0) == s at every step.  Wave 1 forms each chunk's products and
+    // compacts the non-zero ones in index order (a ballot per 64 products,
+    // no block barrier) into one of two LDS buffers, while lane 0 of wave 0
+    // adds the previous chunk's: the same sum, bit for bit (NaN products
+    // are not zero and stay), over half the chain on dfl001's b'y and c'x
+    // (27 / 51 % of b / c non-zero), the forming of chunk k + 1 under the
+    // adds of chunk k.  Hand-offs through LDS words (ready: chunk k + 1
+    // written, freed: chunk k added), release / acquire at workgroup scope.
     constexpr int CH = 4096;
-    __shared__ __attribute__((aligned(16))) double prod[CH];
-    __shared__ __attribute__((aligned(16))) double comp[CH + 16];   // + one batch of read-ahead
-    __shared__ int wsum[kOrdThreads / 64];
-    double s = 0.0e0;
-    for (int base = 0; base < len; base += CH) {
-        const int cnt = min(CH, len - base);
-        __syncthreads();
-        for (int i0 = 0; i0 < cnt; i0 += 8 * kOrdThreads) {
-            double pa[8], pb[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int i = i0 + u * kOrdThreads + tid;
-                pa[u] = i < cnt ? a[base + i] : 0.0;
-                pb[u] = i < cnt ? b[base + i] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int i = i0 + u * kOrdThreads + tid;
-                if (i < cnt) prod[i] = pa[u] * pb[u];
-            }
-        }
-        __syncthreads();
-        constexpr int SEG = CH / kOrdThreads;
-        const int b0 = min(cnt, tid * SEG), b1 = min(cnt, b0 + SEG);
-        int c = 0;
-        for (int i = b0; i < b1; i++) c += prod[i] != 0.0;
-        // exclusive scan of c over the block, in thread order
-        const int lane = tid & 63, wv = tid >> 6;
-        int incl = c;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += t;
-        }
-        if (lane == 63) wsum[wv] = incl;
-        __syncthreads();
-        int off = incl - c;
-        for (int w = 0; w < wv; w++) off += wsum[w];
-        int nz = 0;
-        for (int w = 0; w < kOrdThreads / 64; w++) nz += wsum[w];
-        for (int i = b0; i < b1; i++) {
-            const double v = prod[i];
-            if (v != 0.0) comp[off++] = v;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            const double2* pp = reinterpret_cast<const double2*>(comp);
-            double2 cur[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) cur[u] = pp[u];
-            int i = 0;
-            for (; i + 16 <= nz; i += 16) {
-                double2 nxt[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) nxt[u] = pp[(i + 16) / 2 + u];
-#pragma unroll
-                for (int u = 0; u < 8; u++) { s += cur[u].x; s += cur[u].y; }
-#pragma unroll
-                for (int u = 0; u < 8; u++) cur[u] = nxt[u];
-            }
-            for (; i < nz; i++) s += comp[i];
-        }
+    __shared__ __attribute__((aligned(16))) double comp[2][CH + 16];   // + one batch of read-ahead
+    __shared__ int nzc[2], ready[2], freed[2];
+    if (tid < 2) {
+        ready[tid] = 0;
+        freed[tid] = 0;
     }
-    if (tid == 0) out[j] = s;
+    __syncthreads();
+    const int nch = (len + CH - 1) / CH, lane = tid & 63, wv = tid >> 6;
+    if (wv == 1) {
+        for (int k = 0; k < nch; k++) {
+            const int buf = k & 1;
+            if (k >= 2)
+                while (__hip_atomic_load(&freed[buf], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < k - 1)
+                    __builtin_amdgcn_s_sleep(1);
+            const int base = k * CH, cnt = min(CH, len - base);
+            int off = 0;
+            for (int i0 = 0; i0 < cnt; i0 += 8 * 64) {
+                double pa[8], pb[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int i = i0 + u * 64 + lane;
+                    pa[u] = i < cnt ? a[base + i] : 0.0;
+                    pb[u] = i < cnt ? b[base + i] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const double v = pa[u] * pb[u];
+                    const bool nzf = i0 + u * 64 + lane < cnt && v != 0.0;
+                    const unsigned long long m = __ballot(nzf);
+                    if (nzf) comp[buf][off + __popcll(m & ((1ull << lane) - 1ull))] = v;
+                    off += __popcll(m);
+                }
+            }
+            if (lane == 0) {
+                nzc[buf] = off;
+                __hip_atomic_store(&ready[buf], k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        return;
+    }
+    if (tid != 0) return;
+    double s = 0.0e0;
+    for (int k = 0; k < nch; k++) {
+        const int buf = k & 1;
+        while (__hip_atomic_load(&ready[buf], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < k + 1)
+            __builtin_amdgcn_s_sleep(1);
+        const int nz = nzc[buf];
+        const double2* pp = reinterpret_cast<const double2*>(comp[buf]);
+        double2 cur[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) cur[u] = pp[u];
+        int i = 0;
+        for (; i + 16 <= nz; i += 16) {
+            double2 nxt[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) nxt[u] = pp[(i + 16) / 2 + u];
+#pragma unroll
+            for (int u = 0; u < 8; u++) { s += cur[u].x; s += cur[u].y; }
+#pragma unroll
+            for (int u = 0; u < 8; u++) cur[u] = nxt[u];
+        }
+        for (; i < nz; i++) s += comp[buf][i];
+        __hip_atomic_store(&freed[buf], k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    out[j] = s;
 }
 
 // Test entry (ipo_hip_dot_ordered): the ordered dot of two host vectors
