@@ -3300,6 +3300,7 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
         // 2 every launch of at most kFlatMaxChunks chunks
         int flat_mode = 1;
         if (const char* e = std::getenv("IPO_HIP_GATHER_STAMPS")) gst_group_ = std::atoi(e);
+        if (const char* e = std::getenv("IPO_HIP_GRAPH")) graph_on_ = std::atoi(e) != 0;
         // quadrant gathers (k_update_quad) on the narrow levels of deep trees
         // (IPO_HIP_GATHER_QUAD=0: off)
         bool quad_mode = true;
@@ -3707,12 +3708,19 @@ KktDevice::KktDevice(int m, int n, const int* kA, const int* iA, const double* A
 }
 
 // Sync-free top levels (k_fwd_sf / k_bwd_sf): from sf_level_ up every level
-// is at most kSfWidth supernodes wide.  Their forward update values get
+// is at most kSfWidth supernodes wide (IPO_HIP_SF_WIDTH): 300 for factors
+// of fewer than 2^25 entries, 64 above.  Measured on one box: dfl001 64 /
+// 150 / 300 / 450 / 600 / all -> 290.9 / 292.5 / 292.7 / 292.7 / 292.1 /
+// 224.4 it/s (every level in the launch starves the wide bottom ones),
+// 25fv47 by intpt 932 -> 963 at 300; but banded configs[3] 76.9 -> 68.5 and
+// block-angular configs[4] 47.6 -> 39.3 at 300 (their upper levels hold
+// large chunked supernodes, which the per-level launches spread wider).  Their forward update values get
 // ybuf slices, and their z values zpad slices, of their own 128-B lines;
 // work items, per-supernode arrival counts and parents.  Called from the
 // constructor after the solve chunks are built.
 void KktDevice::build_sync_free_plan() {
-    const int kSfWidth = 64;
+    int kSfWidth = plan_.lx_size < (int64_t(1) << 25) ? 300 : 64;
+    if (const char* e = std::getenv("IPO_HIP_SF_WIDTH")) kSfWidth = std::max(1, std::atoi(e));
     hipStream_t s = stream_;
     const KktPlan& P = plan_;
     const int ns = P.nsup;
@@ -3884,6 +3892,7 @@ KktDevice::~KktDevice() {
     if (ev2_) (void)hipEventDestroy(ev2_);
     if (ev3_) (void)hipEventDestroy(ev3_);
     for (hipEvent_t e : kev_) (void)hipEventDestroy(e);
+    if (lvl_exec_) (void)hipGraphExecDestroy(lvl_exec_);
 }
 
 static PlanView make_view(const KktPlan&, const DevBuf<int>& col0, const DevBuf<int>& rowptr, const DevBuf<int>& rows,
@@ -4051,6 +4060,67 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
                        dFlags_.get(), dkQ_.get() ? dQdiag_.get() : static_cast<const double*>(nullptr),
                        static_cast<double>(qmax_));
     const TailView tv = tail_view();
+    // the sparse levels and the dense tail's gather: the same launches every
+    // factorisation of a plan (fixed arguments), so the fused form is
+    // captured once as a HIP graph and replayed (IPO_HIP_GRAPH=0: launched
+    // one by one; per-phase timing and the gather stamps launch them too)
+    if (graph_on_ && fused && !timing_ && gst_group_ < 0 && !xch_) {
+        if (!lvl_exec_) {
+            hipGraph_t g = nullptr;
+            IPO_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            enqueue_levels(pv, tv, fused, s);
+            IPO_HIP_CHECK(hipStreamEndCapture(s, &g));
+            const hipError_t e = hipGraphInstantiate(&lvl_exec_, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            IPO_HIP_CHECK(e);
+        }
+        IPO_HIP_CHECK(hipGraphLaunch(lvl_exec_, s));
+    } else {
+        enqueue_levels(pv, tv, fused, s);
+    }
+    if (plan_.nt > 0) {
+        // shards: S = sum of every shard's assembled + gathered tail (exchange.h)
+        xsum(tv.S, static_cast<size_t>(plan_.nt) * plan_.nt, RedOp::Sum);
+        xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
+        if (tail_fused && tail_chain_ && !chain_off_ && tv.dep == 1) {   // kkt_dense.hip, k_tail_chain_run
+            launch_tail_chain_run();
+        } else if (tail_fused && tail_run_) {     // one persistent launch (kkt_dense.hip, k_tail_run)
+            launch_tail_from(0, true);
+        } else if (tail_fused) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
+            // one event pair around the steps (a pair per launch added its
+            // own ~2.5 us to every launch's time: the phase's average launch
+            // would not be the kernel's)
+            ph_begin(s);
+            for (int t = 0; t < plan_.ntb; t++) launch_tail_step(pv, tv, t, s);
+            ph_end(kPhTail, plan_.ntb, s);
+        } else
+        for (int kb = 0; kb < plan_.ntb; kb++) {
+            const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
+            const int below = plan_.nt - k0 - nc;
+            ph_begin(s);
+            {
+                launch_diag(pv, nullptr, 0, 1, tv, kb, s);
+                ph_end(kPhDiag, 1, s);
+                if (below > 0) {
+                    ph_begin(s);
+                    launch_trsm(pv, 0, -1, tv, kb, s);
+                    ph_end(kPhTrsm, 1, s);
+                }
+            }
+            if (below > 0) {
+                const int nb = plan_.ntb - kb - 1;
+                ph_begin(s);
+                hipLaunchKernelGGL(k_tail_syrk, dim3(nb * (nb + 1) / 2), dim3(NT), 0, s, pv, tv, kb);
+                ph_end(kPhSyrk, 1, s);
+            }
+        }
+    }
+    return finish_pass(fused || tail_fused);
+}
+
+// The sparse levels (gather, then panels, level by level) and the dense
+// tail's gather of one factorisation, enqueued on s.
+void KktDevice::enqueue_levels(const PlanView& pv, const TailView& tv, bool fused, hipStream_t s) {
     for (int l = 0; l < plan_.nlevels; l++) {
         const int u0 = plan_.unit_level_ptr[l], u1 = plan_.unit_level_ptr[l + 1];
         if (u1 <= u0) continue;
@@ -4090,43 +4160,7 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
         ph_begin(s);
         const int nl = launch_gather(pv, tv, 0, plan_.nlevels, s);
         ph_end(kPhGather, nl, s);
-        // shards: S = sum of every shard's assembled + gathered tail (exchange.h)
-        xsum(tv.S, static_cast<size_t>(plan_.nt) * plan_.nt, RedOp::Sum);
-        xsum(dDscale_.get() + plan_.tail_c0, plan_.nt, RedOp::Sum);
-        if (tail_fused && tail_chain_ && !chain_off_ && tv.dep == 1) {   // kkt_dense.hip, k_tail_chain_run
-            launch_tail_chain_run();
-        } else if (tail_fused && tail_run_) {     // one persistent launch (kkt_dense.hip, k_tail_run)
-            launch_tail_from(0, true);
-        } else if (tail_fused) {     // look-ahead steps (kkt_dense.hip, k_tail_pr)
-            // one event pair around the steps (a pair per launch added its
-            // own ~2.5 us to every launch's time: the phase's average launch
-            // would not be the kernel's)
-            ph_begin(s);
-            for (int t = 0; t < plan_.ntb; t++) launch_tail_step(pv, tv, t, s);
-            ph_end(kPhTail, plan_.ntb, s);
-        } else
-        for (int kb = 0; kb < plan_.ntb; kb++) {
-            const int k0 = kb * kPanelCols, nc = std::min(kPanelCols, plan_.nt - k0);
-            const int below = plan_.nt - k0 - nc;
-            ph_begin(s);
-            {
-                launch_diag(pv, nullptr, 0, 1, tv, kb, s);
-                ph_end(kPhDiag, 1, s);
-                if (below > 0) {
-                    ph_begin(s);
-                    launch_trsm(pv, 0, -1, tv, kb, s);
-                    ph_end(kPhTrsm, 1, s);
-                }
-            }
-            if (below > 0) {
-                const int nb = plan_.ntb - kb - 1;
-                ph_begin(s);
-                hipLaunchKernelGGL(k_tail_syrk, dim3(nb * (nb + 1) / 2), dim3(NT), 0, s, pv, tv, kb);
-                ph_end(kPhSyrk, 1, s);
-            }
-        }
     }
-    return finish_pass(fused || tail_fused);
 }
 
 // min |d| over the factor (ldlt.c:293-306), the dependent-pivot count and
