@@ -301,7 +301,7 @@ class KktDevice {
     bool use_panel_ = true;               // fused diagonal-block + panel kernels (IPO_HIP_PANEL=0: off)
     bool factor_pass(const double* dE, const double* dD, bool fused, bool tail_fused);
     void enqueue_levels(const PlanView& pv, const TailView& tv, bool fused, hipStream_t s);
-    bool graph_on_ = true;                // the levels' fused launches replayed as one HIP graph (IPO_HIP_GRAPH=0: off)
+    bool graph_on_ = false;               // the levels' fused launches replayed as one HIP graph (IPO_HIP_GRAPH=1: on)
     hipGraphExec_t lvl_exec_ = nullptr;   // that graph, captured at the first fused factorisation
     bool finish_pass(bool fused);
     void repair_tail();

@@ -4061,9 +4061,13 @@ bool KktDevice::factor_pass(const double* dE, const double* dD, bool fused, bool
                        static_cast<double>(qmax_));
     const TailView tv = tail_view();
     // the sparse levels and the dense tail's gather: the same launches every
-    // factorisation of a plan (fixed arguments), so the fused form is
-    // captured once as a HIP graph and replayed (IPO_HIP_GRAPH=0: launched
-    // one by one; per-phase timing and the gather stamps launch them too)
+    // factorisation of a plan (fixed arguments), so the fused form can be
+    // captured once as a HIP graph and replayed (IPO_HIP_GRAPH=1, opt-in;
+    // per-phase timing and the gather stamps launch them one by one).
+    // Measured: dfl001 unchanged (292.9 / 292.8 against 293.7 / 291.5 it/s),
+    // 25fv47 by intpt +1-3 %; the launches' cost is on the device (~4.5 us
+    // per dispatch), not the host's enqueue, and rocprofv3 --kernel-trace
+    // --stats crashed in the runtime on the replayed graph, so off
     if (graph_on_ && fused && !timing_ && gst_group_ < 0 && !xch_) {
         if (!lvl_exec_) {
             hipGraph_t g = nullptr;

@@ -87,8 +87,8 @@ def test_sync_free_sweeps_bitwise():
 @pytest.mark.parametrize("name,method", [("dfl001", "hsd"), ("25fv47", "intpt"), ("greenbea", "hsd")])
 def test_level_graph_bitwise(name, method):
     """The sparse levels and the tail gather replayed as one captured HIP
-    graph (default) against the same launches issued one by one
-    (IPO_HIP_GRAPH=0): the same kernels with the same arguments in the same
+    graph (IPO_HIP_GRAPH=1, opt-in) against the same launches issued one by
+    one (default): the same kernels with the same arguments in the same
     order, so the traces are identical."""
     texts = [_with_env("IPO_HIP_GRAPH", v, lambda: ipo_amd.run_mps(mps_path(name), method))[1] for v in ("0", "1")]
     assert texts[0] == texts[1]
